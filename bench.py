@@ -1,0 +1,217 @@
+"""VideoMamba encoder benchmark on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (config C3 of BASELINE.json; the metric is quoted on VideoMamba-M 16f 224):
+VideoMamba-M (d576, depth 32), 16x224x224 clips, bf16, one stateful streaming chunk per
+step (chunk_size 32 > 16 temporal tokens, so the clip is one chunk carrying
+(conv_state, ssm_state) through every layer), random-init weights (seed 0), synthetic
+clips.  A step = one forward of B clips per GPU; clips shard by batch across ranks with
+no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
+excluded) per second summed over all ranks, timed as the max over ranks.
+
+Extra fields: chunk_p50_ms (B=1 chunk latency), roofline of the selective-scan kernel
+(HIP-event timed at the bench shape; algorithmic bytes per launch), cpu_baseline (the
+CPU oracle on one M-16f clip, rank 0 at N=1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),
+    "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti"),
+}
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="clips per GPU")
+    ap.add_argument("--config", default="m16", choices=sorted(CONFIGS))
+    ap.add_argument("--p50-chunks", type=int, default=30)
+    ap.add_argument("--scan-reps", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def _sync_barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def scan_roofline(batch, reps, device):
+    """Time the scan kernel at the bench shape (layer-0 geometry, padded layout) with HIP
+    events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d)."""
+    from videomamba_amd import kernels as K
+    from videomamba_amd.layers import round_up
+
+    D, N, L = 1152, 16, 3137
+    Lp = round_up(L)
+    n = batch * Lp
+    g = torch.Generator(device=device).manual_seed(1)
+    bf = torch.bfloat16
+    u = torch.randn(D, n, device=device, generator=g).to(bf)
+    dt = (0.5 * torch.randn(D, n, device=device, generator=g) - 4.0).to(bf)
+    z = torch.randn(D, n, device=device, generator=g).to(bf)
+    bc = torch.randn(2 * N, n, device=device, generator=g).to(bf)
+    A = -torch.arange(1, N + 1, device=device, dtype=torch.float32).repeat(D, 1).contiguous()
+    Dv = torch.ones(D, device=device)
+    bias = torch.full((D,), -4.0, device=device)
+    h = torch.zeros(batch, D, N, device=device, dtype=bf)
+    y = torch.empty_like(u)
+    rows = (Lp, n)
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def launch():
+        K.scan_raw(u, rows, dt, rows, A, bc[:N], rows, bc[N:], rows, Dv, z, rows, bias, True,
+                   h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, rows, Lp,
+                   batch, D, L, N, 1, stream)
+
+    for _ in range(5):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    avg_s = e0.elapsed_time(e1) / 1e3 / reps
+    e = 2
+    algo = batch * D * L * 4 * e + 2 * batch * N * L * e + 4 * D * N + 8 * D + 2 * batch * D * N * e
+    achieved = algo / avg_s / 1e9
+    return {"bound": "hbm", "kernel": "vm::scan_fwd_kernel", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None, "avg_us": round(avg_s * 1e6, 2), "bytes_per_launch": algo,
+            "shape": f"B={batch} D={D} L={L} N={N} bf16, stateful"}
+
+
+def cpu_baseline(cfg, threads):
+    from oracle import videomamba_oracle as orc
+    from videomamba_amd.videomamba import PretrainVideoMamba
+
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    m = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],
+                           num_frames=cfg["frames"])
+    p = {k: v.detach() for k, v in m.state_dict().items()}
+    ocfg = dict(img_size=224, patch_size=16, depth=cfg["depth"], kernel_size=1,
+                num_frames=cfg["frames"], fused_add_norm=True, rms_norm=True,
+                residual_in_fp32=True, pool_type="cls+avg", norm_epsilon=1e-5, d_state=16,
+                d_conv=4)
+    x = torch.randn(1, 3, cfg["frames"], 224, 224)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        orc.encoder_forward(p, ocfg, x)
+        dt = time.perf_counter() - t0
+    return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
+            "cores": threads, "kind": "port",
+            "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward "
+                      f"({dt:.2f} s), oracle/videomamba_oracle.py"}
+
+
+def main():
+    args = _args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from videomamba_amd.videomamba import PretrainVideoMamba
+
+    cfg = CONFIGS[args.config]
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],
+                               num_frames=cfg["frames"], pool_type="cls+avg")
+    model = model.to(device=device, dtype=torch.bfloat16).eval()
+    B, T = args.batch, cfg["frames"]
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    x = torch.randn(B, 3, T, 224, 224, device=device, generator=g).to(torch.bfloat16)
+    state = model.allocate_state(B, dtype=torch.bfloat16, device=device)
+
+    def step():
+        return model(x, ssm_state=state, temporal_pos_offset=0)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        _sync_barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        _sync_barrier(world)
+        elapsed = time.perf_counter() - t0
+    assert torch.isfinite(out[1].float()).all()
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    tokens = world * B * T * 196 * args.steps
+    value = tokens / elapsed
+
+    # streaming-chunk p50 latency at B=1 (one stateful chunk of the same clip shape)
+    with torch.no_grad():
+        x1 = x[:1].contiguous()
+        st1 = model.allocate_state(1, dtype=torch.bfloat16, device=device)
+        lat = []
+        for i in range(args.p50_chunks + 3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            model(x1, ssm_state=st1, temporal_pos_offset=0)
+            torch.cuda.synchronize()
+            if i >= 3:
+                lat.append((time.perf_counter() - t1) * 1e3)
+        roof = scan_roofline(B, args.scan_reps, device)
+
+    if rank == 0:
+        line = {
+            "metric": "video-tokens/sec per GPU + streaming-chunk p50 latency, VideoMamba-M 16f 224",
+            "value": round(value, 1), "unit": "video-tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic clips (randn), random-init weights (seed 0)",
+            "config": {"workload": f"{cfg['name']} {T}x224^2 bf16, one stateful streaming "
+                                   f"chunk (chunk_size 32) per step",
+                       "model": cfg["name"], "global_batch": world * B, "per_gpu_batch": B,
+                       "frames": T, "seq_len": 1 + T * 196,
+                       "parallelism": f"batch-sharded x{world}, no data-path collectives"},
+            "per_gpu_value": round(value / world, 1),
+            "chunk_p50_ms": round(statistics.median(lat), 3),
+            "chunk_p50_batch": 1,
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * videomamba_hip.h — C ABI of libvideomamba_hip.so (gfx950 / MI355X).
+ *
+ * The drop-in boundary for the VideoMamba encoder hot path.  Each entry point
+ * replaces one third-party kernel call of the reference (tannerhoalst/VideoMamba),
+ * cited as `file:line` under /root/reference:
+ *
+ *   vm_selective_scan_fwd      <- mamba_ssm selective_scan_fn
+ *                                 (models/videomamba/mamba_simple.py:122-152, stateless and
+ *                                  initial_state forms; also replaces the per-token
+ *                                  selective_state_update loop at :153-172)
+ *   vm_selective_state_update  <- mamba_ssm selective_state_update  (mamba_simple.py:483-494)
+ *   vm_causal_conv1d_fwd       <- causal_conv1d_fn (+ conv_state prepend)
+ *                                 (mamba_simple.py:381-404)
+ *   vm_causal_conv1d_update    <- causal_conv1d_update  (mamba_simple.py:468-474)
+ *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
+ *                                 (models/videomamba/videomamba.py:152-166, :904-918)
+ *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
+ *                                 (videomamba.py:359-368, :806-815)
+ *
+ * Conventions (all entry points):
+ *   - Plain device pointers, element counts and element strides; no torch types.
+ *   - The caller owns every buffer; the library never allocates device memory.
+ *   - Sequence ("l") strides are 1; every other stride is passed explicitly.
+ *   - dtype codes: VM_DTYPE_F32 / VM_DTYPE_BF16.  Small parameters (A, D, biases,
+ *     norm / conv weights) are fp32.
+ *   - Work is enqueued on `stream` (a hipStream_t); nothing synchronises, so calls are
+ *     safe to capture into a hipGraph.
+ *   - Return 0 on success, a negative VM_E* code otherwise; vm_last_error() gives the
+ *     message.  Nothing is thrown across the ABI.  Kernels are deterministic (no atomics).
+ */
+#ifndef VIDEOMAMBA_HIP_H
+#define VIDEOMAMBA_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VM_ABI_VERSION 1
+
+#define VM_DTYPE_F32 0
+#define VM_DTYPE_BF16 1
+
+#define VM_OK 0
+#define VM_E_INVALID -1  /* bad argument (shape, dtype, null pointer) */
+#define VM_E_LAUNCH -2   /* HIP launch / runtime error */
+
+typedef void* vm_stream_t; /* hipStream_t */
+
+int vm_abi_version(void);
+const char* vm_last_error(void);
+
+/*
+ * Selective scan, fp32 state (mamba_simple.py:30-106 semantics):
+ *   delta' = softplus?(delta + delta_bias)
+ *   h_t    = exp(delta'_t * A) * h_{t-1} + delta'_t * u_t * B_t      (h_{-1} = h0 or 0)
+ *   y_t    = <h_t, C_t> + D * u_t;   out = y * silu(z)   (z, D optional)
+ * u, delta, z, out: (batch, dim, seqlen) with strides (*_sb, *_sd, 1), dtype `dtype`.
+ * B, C: (batch, dstate, seqlen) with strides (*_sb, *_sn, 1), dtype `dtype`.
+ * A: (dim, dstate) fp32 contiguous.  D, delta_bias: (dim) fp32, nullable.
+ * h0 (nullable) / h_last (nullable): (batch, dim, dstate) with strides (sb, sd, 1) in
+ * their own dtype; h_last may alias h0 (in-place state update).  dstate <= 16.
+ * Columns [seqlen, out_len) of every out row are written as 0 (padded token layouts).
+ */
+int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd,
+                          const void* delta, long long dl_sb, long long dl_sd,
+                          const float* A,
+                          const void* B, long long b_sb, long long b_sn,
+                          const void* C, long long c_sb, long long c_sn,
+                          const float* D, const void* z, long long z_sb, long long z_sd,
+                          const float* delta_bias, int delta_softplus,
+                          const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
+                          void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
+                          void* out, long long o_sb, long long o_sd, int out_len,
+                          int batch, int dim, int seqlen, int dstate, int dtype,
+                          vm_stream_t stream);
+
+/*
+ * One-token scan step on `state` (updated in place, own dtype; fp32 math).
+ * x, dt, z, out: (batch, dim) strides (*_sb, 1); B, C: (batch, dstate) strides (*_sb, 1).
+ * state: (batch, dim, dstate) strides (s_sb, s_sd, 1).
+ */
+int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long long s_sd,
+                              const void* x, long long x_sb, const void* dt, long long dt_sb,
+                              const float* A, const void* B, long long b_sb,
+                              const void* C, long long c_sb, const float* D,
+                              const void* z, long long z_sb, const float* dt_bias,
+                              int dt_softplus, void* out, long long o_sb,
+                              int batch, int dim, int dstate, int dtype, vm_stream_t stream);
+
+/*
+ * Depthwise causal conv1d (+bias, optional SiLU) over the virtual sequence
+ * [conv_state_in (width values) | x], keeping the last `seqlen` outputs.
+ * x: (batch, dim, seqlen) strides (x_sb, x_sd, 1); out: strides (o_sb, o_sd, 1), columns
+ * [seqlen, out_len) of every out row are written as 0.  weight: (dim, width) fp32;
+ * bias: (dim) fp32 nullable.  conv_state_in / conv_state_out: (batch, dim, width)
+ * strides (sb, sd, 1), own dtype, nullable; out state = last `width` raw inputs.
+ * conv_state_out must not alias conv_state_in.  width <= 8.
+ */
+int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd,
+                         const float* weight, const float* bias,
+                         const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
+                         void* cs_out, int cs_out_dtype, long long cso_sb, long long cso_sd,
+                         void* out, long long o_sb, long long o_sd, int out_len,
+                         int batch, int dim, int seqlen, int width, int silu, int dtype,
+                         vm_stream_t stream);
+
+/*
+ * One-token conv step: shift conv_state left by one, append x, dot with weight (+bias),
+ * optional SiLU.  x, out: (batch, dim) strides (*_sb, 1); conv_state in place.
+ */
+int vm_causal_conv1d_update(const void* x, long long x_sb, void* conv_state, int cs_dtype,
+                            long long cs_sb, long long cs_sd, const float* weight,
+                            const float* bias, void* out, long long o_sb,
+                            int batch, int dim, int width, int silu, int dtype,
+                            vm_stream_t stream);
+
+/*
+ * Fused residual add + RMSNorm / LayerNorm over contiguous rows of `cols`:
+ *   s = x (+ residual) in fp32;  y = norm(s) * weight (+ bias)  -> out (out_dtype)
+ *   residual_out (nullable) = s in res_out_dtype.
+ * residual (nullable) and residual_out may alias.
+ */
+int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
+                    const float* weight, const float* bias, void* out, int out_dtype,
+                    void* residual_out, int res_out_dtype, long long rows, int cols,
+                    float eps, int is_rms, vm_stream_t stream);
+
+/*
+ * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,P,P)):
+ *   tok[b, t*Gh*Gw + gh*Gw + gw, c] = e(e(e(conv + bias) + spos[gh*Gw+gw, c]) + tpos[t, c])
+ * where e() rounds to the model dtype (the reference's rounding points).
+ * video: (batch, cin, frames, height, width) contiguous, dtype `dtype`.
+ * weight: (embed, cin*kt*P*P) contiguous, dtype `dtype`; bias: (embed) fp32.
+ * spos: (Gh*Gw, embed), tpos: (frames/kt, embed), dtype `dtype`, contiguous.
+ * out: token rows of `embed` elements; token j of batch b at out + b*out_sb + (row0+j)*embed.
+ */
+int vm_patch_embed_fwd(const void* video, const void* weight, const float* bias,
+                       const void* spos, const void* tpos, void* out, long long out_sb,
+                       int row0, int batch, int cin, int frames, int height, int width,
+                       int kt, int patch, int embed, int dtype, vm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VIDEOMAMBA_HIP_H */

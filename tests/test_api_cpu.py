@@ -1,0 +1,262 @@
+"""CPU tests: public API / streaming contract / builder / loader, mirroring the reference's
+CPU tests (tests/test_public_api_contract.py, tests/test_videomamba_regressions.py), plus
+the C-ABI library load + export check.  No kernel compute happens here (no GPU)."""
+
+import ctypes
+import os
+import re
+from types import SimpleNamespace
+from typing import Any
+
+import pytest
+import torch
+
+import video_mamba
+import videomamba_amd.videomamba as vm_module
+from videomamba_amd import _lib
+from videomamba_amd.mamba_simple import Mamba
+from videomamba_amd.videomamba import PretrainVideoMamba, create_block, load_state_dict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _small_model(**overrides: Any) -> PretrainVideoMamba:
+    kwargs: dict = dict(img_size=8, patch_size=4, depth=2, embed_dim=16, channels=3,
+                        ssm_cfg={"use_fast_path": False}, fused_add_norm=False, rms_norm=False,
+                        residual_in_fp32=False, kernel_size=1, num_frames=4)
+    kwargs.update(overrides)
+    return PretrainVideoMamba(**kwargs)
+
+
+def _cfg(**over):
+    base = dict(img_size=8, patch_size=4, depth=2, embed_dim=16, channels=3,
+                drop_path_rate=0.0, ssm_cfg={"use_fast_path": False}, norm_epsilon=1e-5,
+                fused_add_norm=False, rms_norm=False, residual_in_fp32=False, bimamba=True,
+                pool_type="cls+avg", kernel_size=1, num_frames=4, use_checkpoint=False,
+                checkpoint_num=0, pretrained=None, ckpt_num_frame=4)
+    base.update(over)
+    return SimpleNamespace(vision_encoder=SimpleNamespace(**base))
+
+
+# ------------------------------------------------------------------ public API contract
+def test_public_all_matches_reference_surface():
+    assert set(video_mamba.__all__) == {
+        "DeterminismConfig", "ForwardReturnSemantics", "LayerState", "BiMambaRefinerBlock",
+        "PretrainVideoMamba", "STREAMING_CONTRACT_VERSION", "StateShape", "StreamingState",
+        "add_determinism_args", "allocate_state", "build_videomamba", "configure_determinism",
+        "configure_determinism_from_args", "expected_state_shapes", "forward_return_semantics",
+        "model_forward_return_semantics", "validate_state"}
+    for name in video_mamba.__all__:
+        assert hasattr(video_mamba, name)
+    assert video_mamba.build_videomamba is vm_module.build_videomamba
+    from video_mamba.mamba_simple import Mamba as M2
+    assert M2 is Mamba
+
+
+def test_streaming_contract_allocate_and_validate_cpu():
+    model = _small_model()
+    state = video_mamba.allocate_state(model, batch_size=2, dtype=torch.float32)
+    video_mamba.validate_state(model, state, batch_size=2)
+    shapes = video_mamba.expected_state_shapes(model, batch_size=2)
+    assert len(shapes) == model.depth
+    assert shapes[0].conv_state == (2, model.layers[0].mixer.d_inner, 4)
+    assert shapes[0].ssm_state == (2, model.layers[0].mixer.d_inner, 16)
+    st_d = video_mamba.allocate_state(model, batch_size=2, as_dict=True)
+    video_mamba.validate_state(model, st_d, batch_size=2)
+    assert model.expected_state_shapes(2) == shapes
+
+
+def test_validate_state_error_messages():
+    model = _small_model()
+    state = video_mamba.allocate_state(model, batch_size=1)
+    with pytest.raises(ValueError, match="State length mismatch"):
+        video_mamba.validate_state(model, state[:1], batch_size=1)
+    with pytest.raises(ValueError, match="State dict keys mismatch"):
+        video_mamba.validate_state(model, {0: state[0]}, batch_size=1)
+    with pytest.raises(TypeError, match="list, tuple, or dict"):
+        video_mamba.validate_state(model, "nope", batch_size=1)
+    with pytest.raises(ValueError, match="conv_state shape mismatch"):
+        video_mamba.validate_state(model, state, batch_size=2)
+    with pytest.raises(ValueError, match="batch_size must be a positive integer"):
+        video_mamba.expected_state_shapes(model, 0)
+    with pytest.raises(TypeError, match="2-tuple"):
+        video_mamba.validate_state(model, [state[0][0], state[1][0]], batch_size=1)
+
+
+def test_model_contract_metadata_and_forward_semantics():
+    model = _small_model(add_pool_norm=True)
+    assert model.streaming_contract_version == video_mamba.STREAMING_CONTRACT_VERSION == "1.0.0"
+    sem = model.forward_return_semantics()
+    assert sem.without_state == "(x_vis, x_pool)"
+    assert sem.with_state == "(x_vis, x_pool, next_state)"
+    sem2 = _small_model(add_pool_norm=False).forward_return_semantics()
+    assert sem2.without_state == "x_vis"
+    assert sem2.with_state == "(x_vis, next_state)"
+    assert video_mamba.model_forward_return_semantics(model) == sem
+
+
+def test_configure_determinism_reseeds_torch_rng():
+    video_mamba.configure_determinism(seed=1234, deterministic=True)
+    x1 = torch.randn(8)
+    video_mamba.configure_determinism(seed=1234, deterministic=True)
+    x2 = torch.randn(8)
+    torch.testing.assert_close(x1, x2)
+    torch.use_deterministic_algorithms(False)
+
+
+def test_determinism_cli_roundtrip():
+    import argparse
+    p = video_mamba.add_determinism_args(argparse.ArgumentParser())
+    args = p.parse_args(["--seed", "7", "--deterministic", "--cudnn-benchmark", "off"])
+    cfg = video_mamba.configure_determinism_from_args(args)
+    assert cfg.seed == 7 and cfg.deterministic and not cfg.cudnn_benchmark and not cfg.allow_tf32
+    torch.use_deterministic_algorithms(False)
+
+
+# ------------------------------------------------------------------ builder / loader
+def test_bimamba_false_is_rejected():
+    with pytest.raises(NotImplementedError, match="bimamba=True"):
+        _small_model(bimamba=False)
+
+
+def test_build_videomamba_namespace_with_pretrained(tmp_path):
+    ref = _small_model()
+    path = tmp_path / "mini_ckpt.pt"
+    torch.save(ref.state_dict(), path)
+    model = video_mamba.build_videomamba(_cfg(pretrained=str(path)))
+    assert isinstance(model, PretrainVideoMamba)
+    for k, v in ref.state_dict().items():
+        torch.testing.assert_close(model.state_dict()[k], v)
+
+
+def test_load_state_dict_rejects_wrapped_checkpoint(tmp_path):
+    path = tmp_path / "wrapped.pt"
+    torch.save({"model": _small_model().state_dict()}, path)
+    with pytest.raises(ValueError, match="plain state_dict checkpoint"):
+        video_mamba.build_videomamba(_cfg(pretrained=str(path)))
+
+
+def test_build_videomamba_requires_channels_attr(tmp_path):
+    cfg = _cfg()
+    del cfg.vision_encoder.channels
+    cfg.vision_encoder.in_chans = 3
+    with pytest.raises(AttributeError):
+        video_mamba.build_videomamba(cfg)
+
+
+def test_load_state_dict_uses_weights_only(tmp_path, monkeypatch):
+    model = _small_model()
+    path = tmp_path / "mini_ckpt.pt"
+    torch.save(model.state_dict(), path)
+    seen = {}
+    orig = vm_module.torch.load
+
+    def wrapped(*a, **kw):
+        seen.update(kw)
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(vm_module.torch, "load", wrapped)
+    load_state_dict(str(path), model, ckpt_num_frame=4, num_frames=4)
+    assert seen.get("weights_only") is True
+
+
+def test_load_state_dict_interpolates_pos_embed_for_non_square_target(tmp_path):
+    src = _small_model(img_size=8, patch_size=4)
+    dst = _small_model(img_size=(8, 12), patch_size=4)
+    path = tmp_path / "src.pt"
+    torch.save(src.state_dict(), path)
+    load_state_dict(str(path), dst, ckpt_num_frame=4, num_frames=4)
+    assert dst.pos_embed.shape == (1, 1 + (8 // 4) * (12 // 4), 16)
+
+
+def test_load_state_dict_interpolates_temporal_embedding(tmp_path):
+    src = _small_model(num_frames=4)
+    dst = _small_model(num_frames=8)
+    path = tmp_path / "src.pt"
+    torch.save(src.state_dict(), path)
+    load_state_dict(str(path), dst, ckpt_num_frame=4, num_frames=8)
+    assert dst.temporal_pos_embedding.shape == (1, 8, 16)
+    with pytest.raises(ValueError, match="ckpt_num_frame must be a positive integer"):
+        load_state_dict(str(path), dst, ckpt_num_frame=0, num_frames=8)
+
+
+def test_no_weight_decay_and_num_layers():
+    model = _small_model()
+    assert "temporal_pos_embedding" in model.no_weight_decay()
+    assert model.get_num_layers() == 2
+
+
+def test_state_dict_keys_match_reference_layout():
+    m = _small_model(fused_add_norm=True, rms_norm=True, residual_in_fp32=True)
+    keys = set(m.state_dict())
+    expect = {"cls_token", "pos_embed", "temporal_pos_embedding", "patch_embed.proj.weight",
+              "patch_embed.proj.bias", "norm.weight", "pool_norm.weight", "pool_norm.bias"}
+    for i in range(2):
+        for k in ("A_log", "D", "in_proj.weight", "conv1d.weight", "conv1d.bias",
+                  "x_proj.weight", "dt_proj.weight", "dt_proj.bias", "out_proj.weight"):
+            expect.add(f"layers.{i}.mixer.{k}")
+        expect.add(f"layers.{i}.norm.weight")
+    assert keys == expect
+
+
+def test_param_counts_match_survey():
+    ti = PretrainVideoMamba(depth=24, embed_dim=192, num_frames=8)
+    assert sum(p.numel() for p in ti.parameters()) == 6_228_864
+
+
+# ------------------------------------------------------------------ device guard
+def test_mamba_forward_requires_cuda_tensor_inputs():
+    model = Mamba(d_model=8, d_state=4, d_conv=2, expand=2, use_fast_path=False,
+                  layer_idx=0).eval()
+    with pytest.raises(RuntimeError, match="requires CUDA tensors"):
+        model(torch.randn(1, 2, 8))
+
+
+def test_encoder_forward_requires_cuda_tensor_inputs():
+    model = _small_model().eval()
+    with pytest.raises(RuntimeError, match="requires CUDA tensors"):
+        model(torch.randn(1, 3, 4, 8, 8))
+
+
+def test_tubelet_validation_happens_before_compute():
+    model = _small_model(kernel_size=2, num_frames=8)
+    x = torch.randn(1, 3, 5, 8, 8)
+    with pytest.raises(ValueError, match="must be divisible by tubelet size"):
+        model(x, mask=None, use_image=False)
+    with pytest.raises(ValueError, match="must be divisible by tubelet size"):
+        model.forward_features(x, mask=None, use_image=False)
+    with pytest.raises(ValueError, match="x must have shape"):
+        model(torch.randn(3, 4, 8, 8))
+
+
+def test_block_and_refiner_construct():
+    b = create_block(16, ssm_cfg={"use_fast_path": False}, rms_norm=False, fused_add_norm=False,
+                     residual_in_fp32=False, layer_idx=0)
+    assert b.layer_idx == 0 and b.mixer.bimamba is False
+    r = video_mamba.BiMambaRefinerBlock(16, layer_idx=3)
+    assert r.block_bwd.layer_idx == 1_000_003
+    fs, bs = r.allocate_state(2)
+    assert fs[0].shape == (2, 32, 4) and bs[1].shape == (2, 32, 16)
+
+
+# ------------------------------------------------------------------ C ABI
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _lib.load()
+    assert lib.vm_abi_version() == _lib.ABI_VERSION
+    header = open(os.path.join(ROOT, "include", "videomamba_hip.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(vm_\w+)\(", header, re.M))
+    assert declared == set(_lib.EXPORTED)
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert getattr(raw, name) is not None
+
+
+def test_abi_rejects_bad_arguments_without_gpu():
+    lib = _lib.load()
+    rc = lib.vm_selective_scan_fwd(*([None, 0, 0] * 2), None, *([None, 0, 0] * 2),
+                                   None, None, 0, 0, None, 0, None, 0, 0, 0, None, 0, 0, 0,
+                                   None, 0, 0, 0, 1, 1, 1, 16, 0, None)
+    assert rc == -1
+    assert b"null required pointer" in lib.vm_last_error()
+    rc = lib.vm_add_norm_fwd(None, 0, None, 0, None, None, None, 0, None, 0, 1, 8, 1e-5, 1, None)
+    assert rc == -1

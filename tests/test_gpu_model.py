@@ -1,0 +1,350 @@
+"""GPU model-level parity: Mamba mixer and PretrainVideoMamba on the HIP path vs the
+reference fixtures, the oracle, and the reference's own CUDA tests (mirrored).
+
+Tolerances: fp32 models 1e-4 (fixtures) / 1e-3 (24-layer Ti vs oracle); bf16 models
+5e-2 abs+rel on outputs that went through the same bf16 rounding points (a handful of
+single-ulp flips propagate through the layers).  Streaming contract: chunked == full
+within 1e-4 (fp32, the reference script's tolerance) and 1e-2 relative-norm in bf16.
+"""
+
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+import video_mamba
+from conftest import load_golden
+from oracle import videomamba_oracle as orc
+from videomamba_amd.mamba_simple import Mamba
+from videomamba_amd.videomamba import PretrainVideoMamba, create_block
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _gpu():
+    assert torch.cuda.is_available(), "gpu-marked tests need a HIP device"
+
+
+def _close(a, b, tol):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=tol, atol=tol)
+
+
+def _load(module, npz, name, dt):
+    sd = {k: v.to(dt) for k, v in orc.params_from_npz(npz, name + "/").items()}
+    module.load_state_dict(sd, strict=True)
+    return module.to(dt).to(DEV).eval()
+
+
+MIX, MIX_META = load_golden("mixer_cases.npz")
+
+
+@pytest.mark.parametrize("name", sorted(MIX_META))
+def test_mixer_matches_reference_fixture(name):
+    meta = MIX_META[name]
+    dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    m = _load(Mamba(d_model=meta["d_model"], d_state=meta["d_state"], d_conv=meta["d_conv"],
+                    expand=2, use_fast_path=False, layer_idx=0), MIX, name, dt)
+    g = lambda k: torch.from_numpy(MIX[f"{name}/{k}"].copy())  # noqa: E731
+    x = g("x").to(dt).to(DEV)
+    split = meta["split"]
+    with torch.no_grad():
+        _close(m(x), g("full"), tol)
+        o1, (c1, s1) = m(x[:, :split], return_state=True)
+        _close(o1, g("out1"), tol)
+        _close(c1, g("conv_state1"), tol)
+        _close(s1, g("ssm_state1"), tol)
+        o2, (c2, s2) = m(x[:, split:], state=(c1, s1), return_state=True)
+        _close(o2, g("out2"), tol)
+        _close(c2, g("conv_state2"), tol)
+        _close(s2, g("ssm_state2"), tol)
+        assert s2 is s1  # ssm state updated in place (reference fallback aliasing, F6)
+        ssm = torch.zeros(x.shape[0], m.d_inner, meta["d_state"], dtype=dt, device=DEV)
+        _close(m(x, ssm_state=ssm), g("out_inplace"), tol)
+        _close(ssm, g("ssm_inplace"), tol)
+        if dt == torch.float32:  # scripts/check_streaming_state.py:55
+            torch.testing.assert_close(torch.cat([o1, o2], 1), m(x), rtol=1e-4, atol=1e-4)
+
+
+MOD, MOD_META = load_golden("model_cases.npz")
+
+
+def _model_from_meta(meta):
+    kw = dict(img_size=8, patch_size=4, depth=2, embed_dim=16, channels=3,
+              ssm_cfg={"use_fast_path": False}, fused_add_norm=False, rms_norm=False,
+              residual_in_fp32=False, kernel_size=1, num_frames=4)
+    kw.update(meta["model"])
+    return PretrainVideoMamba(**kw)
+
+
+@pytest.mark.parametrize("name", sorted(MOD_META))
+def test_encoder_matches_reference_fixture(name):
+    meta = MOD_META[name]
+    dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
+    tol = 1e-4 if dt == torch.float32 else 5e-2
+    model = _load(_model_from_meta(meta), MOD, name, dt)
+    g = lambda k: torch.from_numpy(MOD[f"{name}/{k}"].copy())  # noqa: E731
+    x = g("x").to(dt).to(DEV)
+    half = meta["half"]
+    k = model.patch_embed.tubelet_size
+    with torch.no_grad():
+        for pool in ("cls+avg", "cls", "cls_cat_avg", "avg"):
+            model.pool_type = pool
+            xv, xp = model(x)
+            _close(xv, g("x_vis"), tol)
+            _close(xp, g(f"pool[{pool}]"), tol)
+            if pool != "cls":
+                _, xpt = model(x, keep_temporal=True)
+                _close(xpt, g(f"pool_kt[{pool}]"), tol)
+        model.pool_type = "cls+avg"
+        _close(model.forward_features(x), g("features"), tol)
+        mask = g("mask").to(DEV)
+        xv, xp = model(x, mask=mask)
+        _close(xv, g("x_vis_masked"), tol)
+        _close(xp, g("pool_masked"), tol)
+        model.add_pool_norm = False
+        full = model(x)
+        _close(full, g("full_noPool"), tol)
+        state = model.allocate_state(x.shape[0], dtype=dt)
+        c1, st1 = model(x[:, :, :half], ssm_state=state, temporal_pos_offset=0)
+        _close(c1, g("chunk1"), tol)
+        for i, (cs, ss) in enumerate(st1):
+            _close(cs, g(f"state1.{i}.conv"), tol)
+            _close(ss, g(f"state1.{i}.ssm"), tol)
+        st1_copy = [(a.clone(), b.clone()) for a, b in st1]
+        c2, st2 = model(x[:, :, half:], ssm_state=st1, temporal_pos_offset=half // k)
+        _close(c2, g("chunk2"), tol)
+        for i, (cs, ss) in enumerate(st2):
+            _close(cs, g(f"state2.{i}.conv"), tol)
+            _close(ss, g(f"state2.{i}.ssm"), tol)
+        model.add_pool_norm = True
+        model.pool_type = "avg"
+        xv2, xp2, _ = model(x[:, :, half:], ssm_state=st1_copy, temporal_pos_offset=half // k)
+        _close(xv2, g("x_vis_chunk2_avg"), tol)
+        _close(xp2, g("pool_chunk2_avg"), tol)
+
+
+# ------------------------------------------------------------------ reference CUDA tests
+def _small_model(**overrides):
+    kw = dict(img_size=8, patch_size=4, depth=2, embed_dim=16, channels=3,
+              ssm_cfg={"use_fast_path": False}, fused_add_norm=False, rms_norm=False,
+              residual_in_fp32=False, kernel_size=1, num_frames=4)
+    kw.update(overrides)
+    return PretrainVideoMamba(**kw)
+
+
+def test_minimal_cuda_streaming_forward_contract():
+    model = _small_model(add_pool_norm=False).cuda().eval()
+    x = torch.randn(1, 3, 4, 8, 8, device=DEV)
+    state = video_mamba.allocate_state(model, batch_size=1, dtype=x.dtype, device=x.device)
+    with torch.no_grad():
+        first, state = model(x[:, :, :2], mask=None, use_image=False, ssm_state=state,
+                             temporal_pos_offset=0)
+        second, nxt = model(x[:, :, 2:], mask=None, use_image=False, ssm_state=state,
+                            temporal_pos_offset=2)
+    video_mamba.validate_state(model, nxt, batch_size=1)
+    assert first.shape == (1, 1 + 2 * 2 * 2, model.embed_dim)
+    assert second.shape == (1, 2 * 2 * 2, model.embed_dim)
+
+
+def test_forward_shapes_and_feature_semantics():
+    model = _small_model().cuda().eval()
+    x = torch.randn(1, 3, 4, 8, 8, device=DEV)
+    with torch.no_grad():
+        x_vis, x_pool = model(x, mask=None, use_image=False)
+        feats = model.forward_features(x, mask=None, use_image=False)
+    assert x_vis.shape == (1, 16, 16) and x_pool.shape == (1, 1, 16)
+    assert isinstance(feats, torch.Tensor) and feats.shape == (1, 17, 16)
+    state = model.init_state(batch_size=1, dtype=x.dtype, device=x.device)
+    with torch.no_grad():
+        xv, nxt = model.forward_features(x[:, :, :2], ssm_state=state, temporal_pos_offset=0)
+    assert isinstance(nxt, list) and len(nxt) == model.depth
+    tup = tuple(model.init_state(batch_size=1, device=x.device))
+    with torch.no_grad():
+        _, nt = model.forward_features(x[:, :, :2], ssm_state=tup)
+    assert isinstance(nt, tuple)
+    dct = model.init_state(batch_size=1, device=x.device, as_dict=True)
+    with torch.no_grad():
+        _, nd = model.forward_features(x[:, :, :2], ssm_state=dct)
+    assert isinstance(nd, dict) and sorted(nd) == [0, 1]
+    model_np = _small_model(add_pool_norm=False).cuda().eval()
+    with torch.no_grad():
+        assert model_np(x).shape == (1, 17, 16)
+
+
+def test_mask_validation_messages():
+    model = _small_model().cuda().eval()
+    x = torch.randn(2, 3, 4, 8, 8, device=DEV)
+    ok = torch.zeros(2, 17, dtype=torch.bool, device=DEV)
+    with torch.no_grad():
+        xv, xp = model(x, mask=ok)
+        assert xv.shape == (2, 16, 16) and xp.shape[0] == 2
+        with pytest.raises(ValueError, match="mask token length mismatch"):
+            model(x[:1], mask=torch.zeros(1, 16, dtype=torch.bool, device=DEV))
+        m = ok[:1].clone()
+        m[:, 0] = True
+        with pytest.raises(ValueError, match="CLS token visible"):
+            model(x[:1], mask=m)
+        m = torch.ones(1, 17, dtype=torch.bool, device=DEV)
+        m[:, 0] = False
+        with pytest.raises(ValueError, match="at least one patch token visible"):
+            model(x[:1], mask=m, keep_temporal=False)
+        m = ok.clone()
+        m[0, 3:7] = True
+        m[1, 3:11] = True
+        with pytest.raises(ValueError, match="same number of visible tokens"):
+            model(x, mask=m, use_image=True)
+        m = torch.ones(1, 17, dtype=torch.bool, device=DEV)
+        m[:, torch.tensor([0, 1, 2])] = False
+        with pytest.raises(ValueError, match="at least one visible patch token"):
+            model(x[:1], mask=m, keep_temporal=True)
+        m = torch.ones(2, 17, dtype=torch.bool, device=DEV)
+        m[:, torch.tensor([0, 1, 5, 6, 9, 13, 14, 15])] = False
+        _, xp = model(x, mask=m, keep_temporal=True)
+        assert xp.shape == (2, 4, 16)
+
+
+def test_temporal_runtime_length_and_offsets():
+    model = _small_model(num_frames=8).cuda().eval()
+    x = torch.randn(1, 3, 4, 8, 8, device=DEV)
+    with torch.no_grad():
+        xv, xp = model(x, mask=torch.zeros(1, 17, dtype=torch.bool, device=DEV))
+        assert xv.shape[0] == 1 and xp.shape[0] == 1
+        m2 = _small_model(num_frames=8, add_pool_norm=False).cuda().eval()
+        m2.temporal_pos_embedding.copy_(torch.randn_like(m2.temporal_pos_embedding))
+        a = m2.forward_features(x, use_image=True, temporal_pos_offset=0)
+        b = m2.forward_features(x, use_image=True, temporal_pos_offset=2)
+    assert not torch.allclose(a, b)
+
+
+def test_tubelet_and_nonsquare_runtime_resolution():
+    model = _small_model(kernel_size=2, num_frames=4).cuda().eval()
+    x = torch.randn(1, 3, 4, 8, 8, device=DEV)
+    with torch.no_grad():
+        xv, xp = model(x, mask=torch.zeros(1, 1 + 2 * 4, dtype=torch.bool, device=DEV),
+                       use_image=True)
+    assert xv.shape == (1, 8, 16) and xp.shape == (1, 1, 16)
+    m = _small_model(img_size=8).cuda().eval()
+    with torch.no_grad():
+        xv, xp = m(torch.randn(1, 3, 4, 12, 8, device=DEV))
+    assert xv.shape == (1, 4 * 3 * 2, 16) and xp.shape == (1, 1, 16)
+
+
+def test_keep_temporal_cls_cat_avg_shapes():
+    a = _small_model(pool_type="cls+avg").cuda().eval()
+    c = _small_model(pool_type="cls_cat_avg").cuda().eval()
+    c.load_state_dict(a.state_dict(), strict=True)
+    x = torch.randn(1, 3, 4, 8, 8, device=DEV)
+    with torch.no_grad():
+        _, pa = a(x, keep_temporal=True)
+        _, pc = c(x, keep_temporal=True)
+    assert pa.shape == (1, 4, 16) and pc.shape == (1, 5, 16)
+
+
+@pytest.mark.parametrize("pool_type", ["cls+avg", "cls_cat_avg"])
+def test_streaming_rejects_cls_pooling_after_first_chunk(pool_type):
+    model = _small_model(pool_type=pool_type).cuda().eval()
+    x = torch.randn(1, 3, 2, 8, 8, device=DEV)
+    state = model.init_state(batch_size=1, dtype=x.dtype, device=x.device)
+    with pytest.raises(ValueError, match="requires a CLS token"):
+        model(x, keep_temporal=True, ssm_state=state, temporal_pos_offset=1)
+
+
+def test_inference_cache_resizes_and_decode_matches_full():
+    model = Mamba(d_model=8, d_state=4, d_conv=2, expand=2, use_fast_path=False,
+                  layer_idx=0).cuda().eval()
+    cache = SimpleNamespace(seqlen_offset=0, key_value_memory_dict={})
+    with torch.no_grad():
+        out_a = model(torch.randn(2, 1, 8, device=DEV), inference_params=cache)
+        cache.seqlen_offset = 1
+        out_b = model(torch.randn(1, 1, 8, device=DEV), inference_params=cache)
+    cs, ss = cache.key_value_memory_dict[0]
+    assert out_a.shape == (2, 1, 8) and out_b.shape == (1, 1, 8)
+    assert cs.shape[0] == 1 and ss.shape[0] == 1
+    # prefill 5 tokens then decode 7 one at a time == one full pass over 12 tokens
+    m = Mamba(d_model=16, d_state=16, d_conv=4, layer_idx=0).cuda().eval()
+    x = torch.randn(2, 12, 16, device=DEV)
+    cache = SimpleNamespace(seqlen_offset=0, key_value_memory_dict={})
+    with torch.no_grad():
+        full = m(x)
+        outs = [m(x[:, :5], inference_params=cache)]
+        for t in range(5, 12):
+            cache.seqlen_offset = t
+            outs.append(m(x[:, t:t + 1], inference_params=cache))
+    torch.testing.assert_close(torch.cat(outs, 1), full, rtol=1e-4, atol=1e-4)
+
+
+def test_block_return_state_flag_is_respected():
+    block = create_block(d_model=16, ssm_cfg={"use_fast_path": False}, rms_norm=False,
+                         fused_add_norm=False, residual_in_fp32=False, bimamba=True,
+                         layer_idx=0).cuda()
+    x = torch.randn(2, 3, 16, device=DEV)
+    state = block.mixer.allocate_state(batch_size=2, dtype=x.dtype, device=x.device)
+    with torch.no_grad():
+        assert len(block(x, state=state, return_state=False)) == 2
+        assert len(block(x, state=state, return_state=True)) == 3
+
+
+def test_refiner_block_runs_and_reverses_time():
+    blk = video_mamba.BiMambaRefinerBlock(16, layer_idx=0).cuda().eval()
+    x = torch.randn(2, 3, 4, 16, device=DEV)
+    with torch.no_grad():
+        out, st = blk(x)
+    assert out.shape == x.shape and st[0].shape == (2, 32, 4) and st[1].shape == (2, 32, 16)
+
+
+def test_streaming_chunked_full_state_matches_full_sequence_features():
+    model = _small_model(add_pool_norm=False).cuda().eval()
+    x = torch.randn(1, 3, 8, 8, 8, device=DEV)
+    with torch.no_grad():
+        full = model(x)
+        state = model.init_state(batch_size=1, dtype=x.dtype, device=x.device)
+        c1, state = model(x[:, :, :4], ssm_state=state, temporal_pos_offset=0)
+        c2, _ = model(x[:, :, 4:], ssm_state=state, temporal_pos_offset=4)
+    torch.testing.assert_close(torch.cat([c1, c2], 1), full, rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------------------------------ full-size configs
+def test_ti_8f_fp32_matches_oracle():
+    """C1/C2 geometry (VideoMamba-Ti, d192, depth 24, 8x224^2) in fp32: HIP vs oracle."""
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=24, embed_dim=192, num_frames=8).eval()
+    with torch.no_grad():
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    x = torch.randn(1, 3, 8, 224, 224)
+    cfg = dict(img_size=224, patch_size=16, depth=24, kernel_size=1, num_frames=8,
+               fused_add_norm=True, rms_norm=True, residual_in_fp32=True, pool_type="cls+avg",
+               norm_epsilon=1e-5, d_state=16, d_conv=4)
+    torch.set_num_threads(16)
+    ref_v, ref_p, _ = orc.encoder_forward(p, cfg, x)
+    model = model.to(DEV)
+    with torch.no_grad():
+        xv, xp = model(x.to(DEV))
+    _close(xv, ref_v, 1e-3)
+    _close(xp, ref_p, 1e-3)
+
+
+def test_m_16f_bf16_streaming_chunks_match_full_and_fp32():
+    """VideoMamba-M (d576, depth 32) 16x224^2 bf16: 2 chunks of 8 frames with carried
+    fp32 state == one full pass; and the bf16 pass tracks an fp32 pass of the same weights."""
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, add_pool_norm=False)
+    model = model.to(DEV).eval()
+    x = torch.randn(1, 3, 16, 224, 224, device=DEV)
+    with torch.no_grad():
+        full32 = model(x)
+        mb = model.to(torch.bfloat16)
+        xb = x.to(torch.bfloat16)
+        full = mb(xb)
+        st = mb.allocate_state(1, dtype=torch.float32)
+        c1, st = mb(xb[:, :, :8], ssm_state=st, temporal_pos_offset=0)
+        c2, st = mb(xb[:, :, 8:], ssm_state=st, temporal_pos_offset=8)
+    stitched = torch.cat([c1, c2], 1).float()
+    rel = ((stitched - full.float()).norm() / full.float().norm()).item()
+    assert rel < 1e-2, rel
+    rel32 = ((full.float() - full32).norm() / full32.norm()).item()
+    assert rel32 < 5e-2, rel32
+    assert torch.isfinite(full.float()).all()

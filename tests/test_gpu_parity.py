@@ -1,0 +1,220 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the reference fixtures and the oracle.
+
+Tolerances (stated per check):
+* fp32 kernels vs fixtures / oracle: 1e-4 abs+rel (exp2 with folded log2(e), FMA order).
+* bf16 outputs: 2e-2 abs+rel (one bf16 ulp is 2^-8 relative; the reference rounds at
+  the same points, so differences are single-ulp flips of values computed in fp32).
+* states are fp32 inside the kernels: 1e-4 even for bf16 models (1e-2 when stored bf16).
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_golden
+from oracle import videomamba_oracle as orc
+from videomamba_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _gpu():
+    assert torch.cuda.is_available(), "gpu-marked tests need a HIP device"
+
+
+def _t(npz, key, dtype=torch.float32, dev=DEV):
+    return torch.from_numpy(npz[key].copy()).to(dtype).to(dev)
+
+
+def _close(a, b, tol):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=tol, atol=tol)
+
+
+SCAN, SCAN_META = load_golden("scan_cases.npz")
+
+
+@pytest.mark.parametrize("name", sorted(SCAN_META))
+def test_scan_matches_reference_fixture(name):
+    meta = SCAN_META[name]
+    dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
+    g = lambda k, d=dt: _t(SCAN, f"{name}/{k}", d)  # noqa: E731
+    has = lambda k: f"{name}/{k}" in SCAN.files  # noqa: E731
+    out, last = K.selective_scan_fn(
+        g("u"), g("delta"), g("A", torch.float32), g("B"), g("C"),
+        D=g("D", torch.float32) if has("D") else None, z=g("z") if has("z") else None,
+        delta_bias=g("delta_bias", torch.float32) if has("delta_bias") else None,
+        delta_softplus=meta["softplus"],
+        initial_state=g("initial_state", torch.float32) if has("initial_state") else None,
+        return_last_state=True)
+    assert out.dtype == dt and last.dtype == torch.float32
+    _close(out, g("out", torch.float32), 1e-4 if dt == torch.float32 else 2e-2)
+    _close(last, g("last_state", torch.float32), 1e-4)
+
+
+def _rand_scan(Bz, D, L, N, dt, seed, h0=True):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randn(Bz, D, L, generator=g)
+    delta = 0.5 * torch.randn(Bz, D, L, generator=g) - 1.0
+    A = -torch.exp(torch.log(torch.arange(1, N + 1).float()).repeat(D, 1) + 0.1 * torch.randn(D, N, generator=g))
+    Bm = torch.randn(Bz, N, L, generator=g)
+    Cm = torch.randn(Bz, N, L, generator=g)
+    Dv = torch.randn(D, generator=g)
+    z = torch.randn(Bz, D, L, generator=g)
+    bias = 0.1 * torch.randn(D, generator=g)
+    init = torch.randn(Bz, D, N, generator=g) if h0 else None
+    return [t.to(dt) if t is not None and i in (0, 1, 3, 4, 6) else t
+            for i, t in enumerate((u, delta, A, Bm, Cm, Dv, z, bias, init))]
+
+
+@pytest.mark.parametrize("Bz,D,L,N", [(1, 40, 3137, 16),    # 64-lane rows, 7 blocks, ragged dim
+                                      (64, 72, 300, 16),    # 16-lane rows (B*D >= 4096)
+                                      (2, 24, 777, 8), (3, 20, 100, 4), (1, 8, 0, 16)])
+def test_scan_matches_oracle_random(Bz, D, L, N):
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(Bz, D, L, N, torch.float32, 11 + L)
+    ref_y, ref_h = orc.selective_scan(u, delta, A, Bm, Cm, Dv, z, bias, True, init, True)
+    cu = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    y, h = K.selective_scan_fn(cu(u), cu(delta), cu(A), cu(Bm), cu(Cm), cu(Dv), cu(z), cu(bias),
+                               True, True, cu(init))
+    _close(y, ref_y, 1e-4)
+    _close(h, ref_h, 1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_scan_full_size_chunked_equals_full(dt):
+    """Size-independent property at the north-star size (D_inner=1152, L=3137): a scan
+    split at any point with the carried fp32 state equals the full-sequence scan."""
+    u, delta, A, Bm, Cm, Dv, z, bias, _ = _rand_scan(1, 1152, 3137, 16, dt, 5, h0=False)
+    cu = lambda t: t.to(DEV)  # noqa: E731
+    args = [cu(t) for t in (u, delta, A, Bm, Cm, Dv, z, bias)]
+    y_full, h_full = K.selective_scan_fn(*args[:6], z=args[6], delta_bias=args[7],
+                                         delta_softplus=True, return_last_state=True)
+    s = 1000
+    sl = lambda t, a, b: t[..., a:b].contiguous()  # noqa: E731
+    y1, h1 = K.selective_scan_fn(sl(args[0], 0, s), sl(args[1], 0, s), args[2], sl(args[3], 0, s),
+                                 sl(args[4], 0, s), args[5], z=sl(args[6], 0, s), delta_bias=args[7],
+                                 delta_softplus=True, return_last_state=True)
+    y2, h2 = K.selective_scan_fn(sl(args[0], s, None), sl(args[1], s, None), args[2],
+                                 sl(args[3], s, None), sl(args[4], s, None), args[5],
+                                 z=sl(args[6], s, None), delta_bias=args[7], delta_softplus=True,
+                                 return_last_state=True, initial_state=h1)
+    y_ch = torch.cat([y1, y2], dim=-1)
+    rel = ((y_ch.float() - y_full.float()).norm() / y_full.float().norm()).item()
+    assert rel < (1e-5 if dt == torch.float32 else 1e-3), rel
+    assert ((h2 - h_full).norm() / h_full.norm()).item() < 1e-5
+    assert torch.isfinite(y_full.float()).all()
+
+
+def test_scan_inplace_state_alias_and_bf16_state():
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(2, 16, 50, 16, torch.float32, 3)
+    cu = lambda t: t.to(DEV)  # noqa: E731
+    st = cu(init).to(torch.bfloat16)
+    ref = init.to(torch.bfloat16).float()
+    _, ref_h = orc.selective_scan(u, delta, A, Bm, Cm, Dv, z, bias, True, ref, True)
+    _, h = K.selective_scan_fn(cu(u), cu(delta), cu(A), cu(Bm), cu(Cm), cu(Dv), cu(z), cu(bias),
+                               True, True, st, last_state_out=st)
+    assert h is st and h.dtype == torch.bfloat16
+    _close(h, ref_h, 1e-2)
+
+
+# ------------------------------------------------------------------ conv / norm / step
+@pytest.mark.parametrize("with_state", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("L,W", [(37, 4), (3, 4), (1, 4), (16, 2)])
+def test_conv1d_matches_oracle(with_state, dt, L, W):
+    g = torch.Generator().manual_seed(L * 10 + W)
+    x = torch.randn(3, 20, L, generator=g).to(dt)
+    w = torch.randn(20, W, generator=g)
+    b = torch.randn(20, generator=g)
+    cs = torch.randn(3, 20, W, generator=g).to(dt) if with_state else None
+    ref, ref_state = orc.causal_conv1d(x, w, b, True, cs)
+    out, st = K.causal_conv1d_fn(x.to(DEV), w.to(DEV), b.to(DEV), "silu",
+                                 conv_state=None if cs is None else cs.to(DEV),
+                                 return_conv_state=True)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    _close(out, ref, tol)
+    _close(st, ref_state, 0)
+
+
+@pytest.mark.parametrize("cols", [16, 100, 192, 576])
+@pytest.mark.parametrize("is_rms", [True, False])
+@pytest.mark.parametrize("xdt,rdt", [(torch.bfloat16, torch.float32), (torch.float32, None),
+                                     (torch.bfloat16, None)])
+def test_add_norm_matches_oracle(cols, is_rms, xdt, rdt):
+    g = torch.Generator().manual_seed(cols)
+    x = torch.randn(37, cols, generator=g).to(xdt)
+    res = torch.randn(37, cols, generator=g).to(rdt) if rdt is not None else None
+    w = torch.randn(cols, generator=g)
+    b = None if is_rms else torch.randn(cols, generator=g)
+    ry, rr = orc.add_norm(x, res, w, b, 1e-5, True, True, is_rms)
+    fn = K.rms_norm_fn if is_rms else K.layer_norm_fn
+    y, r = fn(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV),
+              residual=None if res is None else res.to(DEV), prenorm=True,
+              residual_in_fp32=True, eps=1e-5)
+    assert y.dtype == xdt and r.dtype == rr.dtype
+    _close(y, ry, 1e-5 if xdt == torch.float32 else 1e-2)
+    _close(r, rr, 1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_one_token_steps_match_oracle(dt):
+    g = torch.Generator().manual_seed(9)
+    Bz, D, N, W = 3, 24, 16, 4
+    st = torch.randn(Bz, D, N, generator=g)
+    x = torch.randn(Bz, D, generator=g).to(dt)
+    dtv = torch.randn(Bz, D, generator=g).to(dt)
+    A = -torch.rand(D, N, generator=g) * 4
+    Bm = torch.randn(Bz, N, generator=g).to(dt)
+    Cm = torch.randn(Bz, N, generator=g).to(dt)
+    Dv = torch.randn(D, generator=g)
+    z = torch.randn(Bz, D, generator=g).to(dt)
+    bias = torch.randn(D, generator=g)
+    st_ref = st.clone()
+    y_ref = orc.selective_state_update(st_ref, x, dtv, A, Bm, Cm, Dv, z, bias, True)
+    st_g = st.to(DEV)
+    y = K.selective_state_update(st_g, x.to(DEV), dtv.to(DEV), A.to(DEV), Bm.to(DEV),
+                                 Cm.to(DEV), Dv.to(DEV), z.to(DEV), bias.to(DEV), True)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    _close(y, y_ref, tol)
+    _close(st_g, st_ref, 1e-5)
+    cs = torch.randn(Bz, D, W, generator=g).to(dt)
+    w = torch.randn(D, W, generator=g)
+    cb = torch.randn(D, generator=g)
+    cs_ref = cs.clone()
+    o_ref = orc.causal_conv1d_update(x, cs_ref, w, cb, True)
+    cs_g = cs.to(DEV)
+    o = K.causal_conv1d_update(x.to(DEV), cs_g, w.to(DEV), cb.to(DEV), "silu")
+    _close(o, o_ref, tol)
+    _close(cs_g, cs_ref, 0)
+
+
+def _patch_oracle(video, w, b, spos, tpos, kt, dt):
+    pe = F.conv3d(video.float(), w.float(), b.float(), stride=(kt, w.shape[-2], w.shape[-1])).to(dt)
+    Bz, C, Tt, gh, gw = pe.shape
+    tok = pe.permute(0, 2, 3, 4, 1).reshape(Bz, Tt, gh * gw, C)
+    tok = (tok + spos.to(dt).unsqueeze(0).unsqueeze(0)).to(dt)
+    tok = (tok + tpos.to(dt).unsqueeze(0).unsqueeze(2)).to(dt)
+    return tok.reshape(Bz, Tt * gh * gw, C)
+
+
+@pytest.mark.parametrize("dt,Bz,T,H,W,P,kt,C", [
+    (torch.bfloat16, 2, 4, 224, 224, 16, 1, 576),   # MFMA path, VideoMamba-M geometry
+    (torch.bfloat16, 1, 4, 64, 48, 16, 2, 192),     # MFMA path, tubelet 2, non-square
+    (torch.float32, 2, 4, 8, 8, 4, 1, 16),          # generic path (reference test model)
+    (torch.bfloat16, 1, 2, 12, 12, 4, 1, 40),       # generic path, bf16
+])
+def test_patch_embed_matches_oracle(dt, Bz, T, H, W, P, kt, C):
+    g = torch.Generator().manual_seed(H + C)
+    video = torch.randn(Bz, 3, T, H, W, generator=g).to(dt)
+    w = (0.02 * torch.randn(C, 3, kt, P, P, generator=g)).to(dt)
+    b = torch.randn(C, generator=g).to(dt)
+    hw = (H // P) * (W // P)
+    spos = (0.02 * torch.randn(hw, C, generator=g)).to(dt)
+    tpos = (0.02 * torch.randn(T // kt, C, generator=g)).to(dt)
+    ref = _patch_oracle(video, w, b, spos, tpos, kt, dt)
+    out = torch.empty(Bz, ref.shape[1] + 3, C, dtype=dt, device=DEV)
+    K.patch_embed(video.to(DEV), w.to(DEV), b.to(DEV), spos.to(DEV), tpos.to(DEV), out, 2,
+                  out.stride(0))
+    _close(out[:, 2:2 + ref.shape[1]], ref, 1e-5 if dt == torch.float32 else 2e-2)

@@ -1,0 +1,96 @@
+"""ctypes binding of ``libvideomamba_hip.so`` (the C ABI in ``include/videomamba_hip.h``).
+
+The library is built in-tree (``make -C videomamba_amd/csrc`` or
+``__graft_entry__.build()``).  There is no fallback: if the library is missing or fails
+to load, every kernel entry point raises.  ``torch`` is imported first so that the HIP
+runtime the library links against (soname ``libamdhip64.so.7``) resolves to the one
+PyTorch already loaded — one runtime, one set of streams.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_longlong, c_void_p
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_NAME = "libvideomamba_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+VM_DTYPE_F32 = 0
+VM_DTYPE_BF16 = 1
+ABI_VERSION = 1
+
+_P = c_void_p
+_LL = c_longlong
+_I = c_int
+
+_SIGNATURES = {
+    "vm_abi_version": ([], _I),
+    "vm_last_error": ([], ctypes.c_char_p),
+    "vm_selective_scan_fwd": (
+        [_P, _LL, _LL,            # u
+         _P, _LL, _LL,            # delta
+         _P,                      # A
+         _P, _LL, _LL,            # B
+         _P, _LL, _LL,            # C
+         _P, _P, _LL, _LL,        # D, z
+         _P, _I,                  # delta_bias, softplus
+         _P, _I, _LL, _LL,        # h0
+         _P, _I, _LL, _LL,        # h_last
+         _P, _LL, _LL, _I,        # out, out_len
+         _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
+         _P], _I),
+    "vm_selective_state_update": (
+        [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
+         _P, _LL, _I, _I, _I, _I, _P], _I),
+    "vm_causal_conv1d_fwd": (
+        [_P, _LL, _LL, _P, _P, _P, _I, _LL, _LL, _P, _I, _LL, _LL, _P, _LL, _LL, _I,
+         _I, _I, _I, _I, _I, _I, _P], _I),
+    "vm_causal_conv1d_update": (
+        [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
+    "vm_add_norm_fwd": (
+        [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _LL, _I, c_float, _I, _P], _I),
+    "vm_patch_embed_fwd": (
+        [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+_load_error: str | None = None
+
+
+def load():
+    """Load (once) and return the CDLL; raises RuntimeError with the reason on failure."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise RuntimeError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f"{LIB_NAME} not found at {LIB_PATH}: build it with "
+                       "`make -C videomamba_amd/csrc` (hipcc --offload-arch=gfx950)")
+        raise RuntimeError(_load_error)
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as exc:
+        _load_error = f"failed to load {LIB_PATH}: {exc}"
+        raise RuntimeError(_load_error) from exc
+    for name, (args, res) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    ver = lib.vm_abi_version()
+    if ver != ABI_VERSION:
+        _load_error = f"{LIB_NAME} ABI version {ver} != expected {ABI_VERSION}"
+        raise RuntimeError(_load_error)
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _lib.vm_last_error().decode(errors="replace") if _lib is not None else ""
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")

@@ -1,0 +1,88 @@
+// Shared device/host helpers for the VideoMamba gfx950 kernels.
+// Storage types: float (VM_DTYPE_F32) and bf16 held as uint16_t (VM_DTYPE_BF16).
+// All arithmetic is fp32; bf16 is produced with a round-to-nearest-even cast
+// (lowered to v_cvt_pk_bf16_f32 on gfx950, which keeps NaN a NaN).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "../../include/videomamba_hip.h"
+
+namespace vm {
+
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) {
+  __hip_bfloat16 h = __float2bfloat16(v);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+// Round-trip through the storage type (models the reference's "->e" rounding points).
+template <typename T> __device__ __forceinline__ float round_to(float v) {
+  return to_f32(from_f32<T>(v));
+}
+
+// Load/store of a value whose storage dtype is only known at run time (state tensors).
+__device__ __forceinline__ float load_dyn(const void* p, long long i, int dtype) {
+  if (dtype == VM_DTYPE_BF16) return to_f32(reinterpret_cast<const bf16_t*>(p)[i]);
+  return reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void store_dyn(void* p, long long i, int dtype, float v) {
+  if (dtype == VM_DTYPE_BF16) reinterpret_cast<bf16_t*>(p)[i] = from_f32<bf16_t>(v);
+  else reinterpret_cast<float*>(p)[i] = v;
+}
+
+// 8 consecutive elements <-> 8 floats, 16-byte (bf16) or 2x16-byte (fp32) accesses.
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  uint4 q = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = static_cast<uint32_t>(from_f32<bf16_t>(v[2 * i])) |
+           (static_cast<uint32_t>(from_f32<bf16_t>(v[2 * i + 1])) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// torch F.softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus(float x) { return x <= 20.0f ? log1pf(__expf(x)) : x; }
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+}  // namespace vm
+
+// ------------------------------------------------------------------ host-side helpers
+namespace vmhost {
+void set_error(const char* fmt, ...);
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline int dsize(int dtype) { return dtype == VM_DTYPE_BF16 ? 2 : 4; }
+inline bool dtype_ok(int dtype) { return dtype == VM_DTYPE_F32 || dtype == VM_DTYPE_BF16; }
+int launch_status(const char* what);
+}  // namespace vmhost

@@ -1,0 +1,304 @@
+"""Host-side operator shims over the HIP C ABI, mirroring the reference's kernel seams.
+
+Public functions keep the call shapes the reference uses for its third-party kernels
+(``models/videomamba/mamba_simple.py:11-14``, ``videomamba.py:11``):
+
+* ``selective_scan_fn``      <- mamba_ssm ``selective_scan_fn`` (+ ``initial_state``)
+* ``selective_state_update`` <- mamba_ssm Triton ``selective_state_update``
+* ``causal_conv1d_fn`` / ``causal_conv1d_update`` <- causal-conv1d
+* ``rms_norm_fn`` / ``layer_norm_fn`` <- mamba_ssm Triton layer norm
+
+plus ``patch_embed`` (PatchEmbed Conv3d + positional adds).  Every function runs the HIP
+kernels of ``libvideomamba_hip.so`` on the tensors' device and current stream; CPU
+tensors raise ``RuntimeError`` (as the reference does at ``mamba_simple.py:304-308``),
+and a missing library raises — there is no fallback path.
+
+The ``*_raw`` launchers take explicit element strides and are what the model uses for
+its padded channel-major layouts.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+_DT = {torch.float32: _lib.VM_DTYPE_F32, torch.bfloat16: _lib.VM_DTYPE_BF16}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return _DT[dt]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dt}: the HIP kernels take float32 or bfloat16")
+
+
+def require_gpu(*tensors: Optional[Tensor], what: str = "VideoMamba") -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                f"{what} requires CUDA tensors in this package because its HIP kernels "
+                "(libvideomamba_hip, gfx950) are GPU-only; move the model and inputs to the "
+                "ROCm device (.cuda())."
+            )
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def f32c(t: Optional[Tensor]) -> Optional[Tensor]:
+    """fp32 contiguous view/copy of a small parameter (A, D, biases, weights)."""
+    if t is None:
+        return None
+    t = t.detach()
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _lastdim_contig(t: Optional[Tensor]) -> Optional[Tensor]:
+    if t is None:
+        return None
+    return t if (t.stride(-1) == 1 or t.shape[-1] <= 1) else t.contiguous()
+
+
+# --------------------------------------------------------------------------- raw launchers
+def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, softplus,
+             h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen, dstate, dtype,
+             stream):
+    lib = _lib.load()
+    rc = lib.vm_selective_scan_fwd(
+        _p(u), u_s[0], u_s[1], _p(delta), dl_s[0], dl_s[1], _p(A32),
+        _p(B), b_s[0], b_s[1], _p(C), c_s[0], c_s[1],
+        _p(D32), _p(z), z_s[0], z_s[1], _p(bias32), int(softplus),
+        _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
+        _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
+        _p(out), o_s[0], o_s[1], out_len, batch, dim, seqlen, dstate, dtype, stream)
+    _lib.check(rc, "vm_selective_scan_fwd")
+
+
+def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, batch, dim,
+             seqlen, width, silu, dtype, stream):
+    lib = _lib.load()
+    rc = lib.vm_causal_conv1d_fwd(
+        _p(x), x_s[0], x_s[1], _p(w32), _p(b32),
+        _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
+        _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
+        _p(out), o_s[0], o_s[1], out_len, batch, dim, seqlen, width, int(silu), dtype, stream)
+    _lib.check(rc, "vm_causal_conv1d_fwd")
+
+
+def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_rms, stream):
+    lib = _lib.load()
+    rc = lib.vm_add_norm_fwd(
+        _p(x), dtype_code(x.dtype), _p(residual),
+        dtype_code(residual.dtype) if residual is not None else 0,
+        _p(w32), _p(b32), _p(out), dtype_code(out.dtype), _p(residual_out),
+        dtype_code(residual_out.dtype) if residual_out is not None else 0,
+        rows, cols, float(eps), int(is_rms), stream)
+    _lib.check(rc, "vm_add_norm_fwd")
+
+
+# --------------------------------------------------------------------------- selective scan
+def selective_scan_fn(u: Tensor, delta: Tensor, A: Tensor, B: Tensor, C: Tensor,
+                      D: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                      delta_bias: Optional[Tensor] = None, delta_softplus: bool = False,
+                      return_last_state: bool = False, initial_state: Optional[Tensor] = None,
+                      *, last_state_out: Optional[Tensor] = None):
+    """mamba-ssm ``selective_scan_fn`` with the ``initial_state`` extension the reference
+    probes for (``mamba_simple.py:17-22``, ``:138-152``).
+
+    u, delta, z: (b, d, l); A: (d, n) real; B, C: (b, n, l) (input-dependent); D,
+    delta_bias: (d,).  Returns ``out`` (u.dtype) or ``(out, last_state)``; last_state is a
+    new fp32 (b, d, n) tensor unless ``last_state_out`` is given, in which case it is
+    written there (in its dtype; may be ``initial_state`` itself) and returned.
+    """
+    require_gpu(u, delta, A, B, C, D, z, delta_bias, initial_state, what="selective_scan_fn")
+    if A.is_complex():
+        raise NotImplementedError("complex A is not supported")
+    if B.dim() != 3 or C.dim() != 3:
+        raise NotImplementedError("selective_scan_fn supports input-dependent B/C of shape "
+                                  "(batch, dstate, seqlen) only (the reference's usage)")
+    batch, dim, seqlen = u.shape
+    dstate = A.shape[1]
+    dt = dtype_code(u.dtype)
+    if seqlen == 0 or batch == 0 or dim == 0:  # nothing to scan: the state passes through
+        out = u.new_empty((batch, dim, seqlen))
+        if not return_last_state:
+            return out
+        h = (initial_state.float() if initial_state is not None else
+             torch.zeros((batch, dim, dstate), dtype=torch.float32, device=u.device))
+        if last_state_out is not None:
+            last_state_out.copy_(h)
+            h = last_state_out
+        return out, h
+    u = _lastdim_contig(u)
+    delta = _lastdim_contig(delta.to(u.dtype))
+    z = _lastdim_contig(None if z is None else z.to(u.dtype))
+    B = _lastdim_contig(B.to(u.dtype))
+    C = _lastdim_contig(C.to(u.dtype))
+    out = torch.empty((batch, dim, seqlen), dtype=u.dtype, device=u.device)
+    h0 = None
+    if initial_state is not None:
+        h0 = _lastdim_contig(initial_state)
+    hl = None
+    if return_last_state:
+        hl = last_state_out if last_state_out is not None else torch.empty(
+            (batch, dim, dstate), dtype=torch.float32, device=u.device)
+        if hl.stride(-1) != 1:
+            raise ValueError("last_state_out must have unit stride on the state axis")
+    scan_raw(u, (u.stride(0), u.stride(1)), delta, (delta.stride(0), delta.stride(1)),
+             f32c(A), B, (B.stride(0), B.stride(1)), C, (C.stride(0), C.stride(1)),
+             f32c(D), z, (z.stride(0), z.stride(1)) if z is not None else (0, 0),
+             f32c(delta_bias), delta_softplus,
+             h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
+             hl, (hl.stride(0), hl.stride(1)) if hl is not None else (0, 0),
+             out, (out.stride(0), out.stride(1)), seqlen, batch, dim, seqlen, dstate, dt,
+             _stream(u))
+    return (out, hl) if return_last_state else out
+
+
+def selective_state_update(state: Tensor, x: Tensor, dt: Tensor, A: Tensor, B: Tensor,
+                           C: Tensor, D: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                           dt_bias: Optional[Tensor] = None, dt_softplus: bool = False) -> Tensor:
+    """One-token scan step; ``state`` (b, d, n) updated in place (its dtype).  x, dt, z:
+    (b, d); B, C: (b, n).  Returns out (b, d) in x.dtype."""
+    require_gpu(state, x, dt, A, B, C, D, z, dt_bias, what="selective_state_update")
+    batch, dim = x.shape
+    dstate = A.shape[1]
+    if state.stride(-1) != 1:
+        raise ValueError("state must have unit stride on the state axis")
+    x = _lastdim_contig(x)
+    dt_ = _lastdim_contig(dt.to(x.dtype))
+    B = _lastdim_contig(B.to(x.dtype))
+    C = _lastdim_contig(C.to(x.dtype))
+    z = _lastdim_contig(None if z is None else z.to(x.dtype))
+    out = torch.empty((batch, dim), dtype=x.dtype, device=x.device)
+    lib = _lib.load()
+    rc = lib.vm_selective_state_update(
+        _p(state), dtype_code(state.dtype), state.stride(0), state.stride(1),
+        _p(x), x.stride(0), _p(dt_), dt_.stride(0), _p(f32c(A)), _p(B), B.stride(0),
+        _p(C), C.stride(0), _p(f32c(D)), _p(z), z.stride(0) if z is not None else 0,
+        _p(f32c(dt_bias)), int(dt_softplus), _p(out), out.stride(0),
+        batch, dim, dstate, dtype_code(x.dtype), _stream(x))
+    _lib.check(rc, "vm_selective_state_update")
+    return out
+
+
+# --------------------------------------------------------------------------- causal conv1d
+def causal_conv1d_fn(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None,
+                     activation: Optional[str] = None, *, conv_state: Optional[Tensor] = None,
+                     return_conv_state: bool = False):
+    """causal-conv1d ``causal_conv1d_fn(x, weight, bias, activation)``; x: (b, d, l),
+    weight: (d, w).  With ``conv_state`` (b, d, w) the conv runs over
+    ``cat([conv_state, x])`` and keeps the last l outputs (``mamba_simple.py:382-390``).
+    ``return_conv_state`` also returns the last w raw inputs (new tensor)."""
+    require_gpu(x, weight, bias, conv_state, what="causal_conv1d_fn")
+    if activation not in (None, "silu", "swish"):
+        raise NotImplementedError(f"activation {activation!r}")
+    if weight.dim() == 3:
+        weight = weight.reshape(weight.shape[0], weight.shape[-1])
+    batch, dim, seqlen = x.shape
+    width = weight.shape[1]
+    x = _lastdim_contig(x)
+    out = torch.empty((batch, dim, seqlen), dtype=x.dtype, device=x.device)
+    cs_in = _lastdim_contig(conv_state)
+    cs_out = None
+    if return_conv_state:
+        cs_dtype = conv_state.dtype if conv_state is not None else x.dtype
+        cs_out = torch.empty((batch, dim, width), dtype=cs_dtype, device=x.device)
+    conv_raw(x, (x.stride(0), x.stride(1)), f32c(weight), f32c(bias),
+             cs_in, (cs_in.stride(0), cs_in.stride(1)) if cs_in is not None else (0, 0),
+             cs_out, (cs_out.stride(0), cs_out.stride(1)) if cs_out is not None else (0, 0),
+             out, (out.stride(0), out.stride(1)), seqlen, batch, dim, seqlen, width,
+             activation is not None, dtype_code(x.dtype), _stream(x))
+    return (out, cs_out) if return_conv_state else out
+
+
+def causal_conv1d_update(x: Tensor, conv_state: Tensor, weight: Tensor,
+                         bias: Optional[Tensor] = None, activation: Optional[str] = None) -> Tensor:
+    """causal-conv1d ``causal_conv1d_update`` for one token: x (b, d); ``conv_state``
+    (b, d, w) is shifted in place."""
+    require_gpu(x, conv_state, weight, bias, what="causal_conv1d_update")
+    if weight.dim() == 3:
+        weight = weight.reshape(weight.shape[0], weight.shape[-1])
+    batch, dim = x.shape
+    width = weight.shape[1]
+    if conv_state.stride(-1) != 1:
+        raise ValueError("conv_state must have unit stride on the width axis")
+    x = _lastdim_contig(x)
+    out = torch.empty((batch, dim), dtype=x.dtype, device=x.device)
+    lib = _lib.load()
+    rc = lib.vm_causal_conv1d_update(
+        _p(x), x.stride(0), _p(conv_state), dtype_code(conv_state.dtype), conv_state.stride(0),
+        conv_state.stride(1), _p(f32c(weight)), _p(f32c(bias)), _p(out), out.stride(0),
+        batch, dim, width, int(activation in ("silu", "swish")), dtype_code(x.dtype), _stream(x))
+    _lib.check(rc, "vm_causal_conv1d_update")
+    return out
+
+
+# --------------------------------------------------------------------------- norms
+def _norm(x, weight, bias, residual, prenorm, residual_in_fp32, eps, is_rms, out=None,
+          residual_out=None):
+    require_gpu(x, weight, bias, residual, what="rms_norm_fn/layer_norm_fn")
+    shape = x.shape
+    cols = shape[-1]
+    x2 = x.reshape(-1, cols)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    r2 = None
+    if residual is not None:
+        r2 = residual.reshape(-1, cols)
+        if not r2.is_contiguous():
+            r2 = r2.contiguous()
+    rows = x2.shape[0]
+    y = out if out is not None else torch.empty(shape, dtype=x.dtype, device=x.device)
+    ro = None
+    if prenorm:
+        if residual_out is not None:
+            ro = residual_out
+        else:
+            rdt = residual.dtype if residual is not None else (
+                torch.float32 if residual_in_fp32 else x.dtype)
+            ro = torch.empty(shape, dtype=rdt, device=x.device)
+    add_norm_raw(x2, r2, f32c(weight), f32c(bias), y, ro, rows, cols, eps, is_rms, _stream(x))
+    return (y, ro) if prenorm else y
+
+
+def rms_norm_fn(x: Tensor, weight: Tensor, bias: Optional[Tensor], residual: Optional[Tensor] = None,
+                prenorm: bool = False, residual_in_fp32: bool = False, eps: float = 1e-6, **_):
+    """mamba-ssm ``rms_norm_fn``: returns y, or (y, residual_out) with ``prenorm``."""
+    return _norm(x, weight, bias, residual, prenorm, residual_in_fp32, eps, True)
+
+
+def layer_norm_fn(x: Tensor, weight: Tensor, bias: Optional[Tensor], residual: Optional[Tensor] = None,
+                  prenorm: bool = False, residual_in_fp32: bool = False, eps: float = 1e-6,
+                  is_rms_norm: bool = False, **_):
+    """mamba-ssm ``layer_norm_fn`` (LayerNorm unless ``is_rms_norm``)."""
+    return _norm(x, weight, bias, residual, prenorm, residual_in_fp32, eps, is_rms_norm)
+
+
+# --------------------------------------------------------------------------- patch embed
+def patch_embed(video: Tensor, weight: Tensor, bias: Tensor, spos: Tensor, tpos: Tensor,
+                out: Tensor, row0: int, out_batch_stride: int) -> None:
+    """Conv3d tubelet embed + bias + spatial/temporal positional adds, written as token
+    rows into ``out`` (token j of batch b at ``out[b*out_batch_stride + (row0+j)*C]``)."""
+    require_gpu(video, weight, bias, spos, tpos, out, what="patch_embed")
+    Bsz, cin, T, H, W = video.shape
+    C, _, kt, P, _ = weight.shape
+    dt = dtype_code(weight.dtype)
+    video = video.to(weight.dtype).contiguous()
+    lib = _lib.load()
+    rc = lib.vm_patch_embed_fwd(
+        _p(video), _p(weight.contiguous()), _p(f32c(bias)), _p(spos.to(weight.dtype).contiguous()),
+        _p(tpos.to(weight.dtype).contiguous()), _p(out), out_batch_stride, row0,
+        Bsz, cin, T, H, W, kt, P, C, dt, _stream(video))
+    _lib.check(rc, "vm_patch_embed_fwd")

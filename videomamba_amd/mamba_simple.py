@@ -1,0 +1,290 @@
+"""Mamba mixer on the HIP kernels (``models/videomamba/mamba_simple.py:175-590`` surface).
+
+Construction, parameter names / shapes and initialisation follow the reference exactly
+(so state_dicts interchange and a seeded build gives the same weights).  The forward
+replaces the reference's kernel calls with this package's HIP kernels and a layout
+chosen for them:
+
+    hn (B, Lp, C) token-major, Lp = round_up(L, 8), rows >= L zero
+    xz = W_in @ hn^T            -> (2D, B*Lp)   channel-major, batch-interleaved rows
+    u  = silu(conv1d(x [+ conv_state]))  HIP  (D, B*Lp), padded columns written 0
+    x_dbl = W_x @ u             -> (R+2N, B*Lp) (dt_low, B, C rows)
+    dt = W_dt @ dt_low          -> (D, B*Lp)
+    y  = selective_scan(u, dt, A, B, C, D, z, dt_bias, softplus)  HIP, fp32 state
+    out = y^T @ W_out^T         -> (B*Lp, C)
+
+Rounding points match the reference slow path (xz, u, x_dbl, dt, y, out in the model
+dtype).  The GEMMs are plain library GEMMs (hipBLASLt via torch.matmul) on this layout;
+no transpose copies are materialised.  The scan runs once per chunk — never per token —
+and keeps the state in fp32 internally.  State semantics:
+
+* ``state=(conv, ssm), return_state=True``: conv over ``[conv_state | x]``; the new
+  conv state is a fresh tensor (last d_conv raw inputs); the ssm state is updated in
+  place and returned (the reference's fallback aliases it the same way).
+* ``ssm_state=t`` alone (legacy): conv restarts from zeros, ``t`` updated in place.
+* ``inference_params``: prefill (offset 0) fills the cache; offset > 0 runs ``step``.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+from typing import Any, MutableMapping, Optional, Protocol, Tuple, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+from . import kernels as K
+from .layers import round_up, warn_if_grad
+
+_CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP "
+               "kernels (libvideomamba_hip, gfx950) are GPU-only.")
+
+
+class InferenceParamsLike(Protocol):
+    seqlen_offset: int
+    key_value_memory_dict: MutableMapping[int, Tuple[Tensor, Tensor]]
+
+
+class Mamba(nn.Module):
+    def __init__(self, d_model: int, d_state: int = 16, d_conv: int = 4, expand: int = 2,
+                 dt_rank: Union[int, str] = "auto", dt_min: float = 0.001,
+                 dt_max: float = 0.1, dt_init: str = "random", dt_scale: float = 1.0,
+                 dt_init_floor: float = 1e-4, conv_bias: bool = True, bias: bool = False,
+                 use_fast_path: bool = True, layer_idx: Optional[int] = None,
+                 bimamba: bool = True, device=None, dtype=None, **_: Any):
+        fk = {k: v for k, v in (("device", device), ("dtype", dtype)) if v is not None}
+        super().__init__()
+        self.d_model = d_model
+        self.d_state = d_state
+        self.d_conv = d_conv
+        self.expand = expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else int(dt_rank)
+        self.bimamba = bool(bimamba)  # API compatibility; the mixer scans one direction
+        if os.getenv("VIDEOMAMBA_DISABLE_FUSED", "").lower() in {"1", "true", "yes", "y", "on"}:
+            use_fast_path = False
+        # Both settings run the same fused HIP path; the flag is kept for API parity.
+        self.use_fast_path = use_fast_path
+        self.layer_idx = layer_idx
+
+        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=bias, **fk)
+        self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, kernel_size=d_conv,
+                                groups=self.d_inner, padding=d_conv - 1, bias=conv_bias, **fk)
+        self.activation = "silu"
+        self.act = nn.SiLU()
+        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + 2 * d_state, bias=False, **fk)
+        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True, **fk)
+
+        # dt_proj init: variance-preserving weights; bias = softplus^-1(U[dt_min, dt_max])
+        std = self.dt_rank ** -0.5 * dt_scale
+        if dt_init == "constant":
+            nn.init.constant_(self.dt_proj.weight, std)
+        elif dt_init == "random":
+            nn.init.uniform_(self.dt_proj.weight, -std, std)
+        else:
+            raise NotImplementedError
+        dt = torch.exp(torch.rand(self.d_inner, **fk) * (math.log(dt_max) - math.log(dt_min))
+                       + math.log(dt_min)).clamp(min=dt_init_floor)
+        with torch.no_grad():
+            self.dt_proj.bias.copy_(dt + torch.log(-torch.expm1(-dt)))
+        self.dt_proj.bias._no_reinit = True
+
+        # S4D-real A, kept as log in fp32; D skip in fp32
+        a = torch.arange(1, d_state + 1, dtype=torch.float32, device=device)
+        self.A_log = nn.Parameter(torch.log(a).unsqueeze(0).repeat(self.d_inner, 1).contiguous())
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
+        self.D._no_weight_decay = True
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
+        self._pcache_key = None
+        self._pcache = None
+
+    # ------------------------------------------------------------------ params (fp32)
+    def _fp32_params(self):
+        """A = -exp(A_log), D, dt bias, conv weight/bias as fp32 contiguous (cached per
+        parameter version so bf16 models convert once, not per call)."""
+        srcs = (self.A_log, self.D, self.dt_proj.bias, self.conv1d.weight, self.conv1d.bias)
+        key = tuple(None if p is None else (p.data_ptr(), p._version, p.dtype, p.device)
+                    for p in srcs)
+        if key != self._pcache_key:
+            with torch.no_grad():
+                A = (-torch.exp(self.A_log.float())).contiguous()
+                Dv = K.f32c(self.D)
+                bias = K.f32c(self.dt_proj.bias)
+                w = K.f32c(self.conv1d.weight.reshape(self.d_inner, self.d_conv))
+                cb = K.f32c(self.conv1d.bias)
+            self._pcache = (A, Dv, bias, w, cb)
+            self._pcache_key = key
+        return self._pcache
+
+    # ------------------------------------------------------------------ core
+    def _forward_padded(self, hn: Tensor, seqlen: int, *, conv_state_in: Optional[Tensor] = None,
+                        conv_state_out: Optional[Tensor] = None, h0: Optional[Tensor] = None,
+                        h_last: Optional[Tensor] = None) -> Tensor:
+        """hn: (B, Lp, C) contiguous, rows >= seqlen zero.  Returns (B, Lp, C) with rows
+        >= seqlen zero.  States are read/written by the kernels (see module doc)."""
+        Bsz, Lp, C = hn.shape
+        Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
+        n = Bsz * Lp
+        dt_code = K.dtype_code(hn.dtype)
+        stream = torch.cuda.current_stream(hn.device).cuda_stream
+        A, Dv, dbias, cw, cb = self._fp32_params()
+        rows = (Lp, n)  # (batch stride, channel stride) of a (ch, B*Lp) buffer
+
+        xz = torch.matmul(self.in_proj.weight, hn.view(n, C).t())  # (2D, B*Lp)
+        if self.in_proj.bias is not None:
+            xz += self.in_proj.bias.to(xz.dtype)[:, None]
+        x, z = xz[:Dm], xz[Dm:]
+        u = torch.empty((Dm, n), dtype=hn.dtype, device=hn.device)
+        K.conv_raw(x, rows, cw, cb,
+                   conv_state_in, (conv_state_in.stride(0), conv_state_in.stride(1))
+                   if conv_state_in is not None else (0, 0),
+                   conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
+                   if conv_state_out is not None else (0, 0),
+                   u, rows, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
+        x_dbl = torch.matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
+        dt = torch.matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
+        y = torch.empty_like(u)
+        K.scan_raw(u, rows, dt, rows, A, x_dbl[R:R + N], rows, x_dbl[R + N:], rows, Dv,
+                   z, rows, dbias, True,
+                   h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
+                   h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
+                   y, rows, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+        out = torch.matmul(y.t(), self.out_proj.weight.t())  # (B*Lp, C)
+        if self.out_proj.bias is not None:
+            out += self.out_proj.bias.to(out.dtype)
+        return out.view(Bsz, Lp, C)
+
+    def _check_state(self, t: Tensor, last: int, what: str, batch: int) -> Tensor:
+        want = (batch, self.d_inner, last)
+        if tuple(t.shape) != want:
+            raise ValueError(f"{what} shape mismatch: expected {want}, got {tuple(t.shape)}.")
+        if t.stride(-1) != 1:
+            raise ValueError(f"{what} must have unit stride on its last axis")
+        return t
+
+    def forward_padded(self, hn: Tensor, seqlen: int, *, ssm_state: Optional[Tensor] = None,
+                       state: Optional[Tuple[Tensor, Tensor]] = None,
+                       return_state: bool = False):
+        """Model-internal entry on the padded layout (no inference_params).  Same state
+        semantics as :meth:`forward`."""
+        conv_state = None
+        if state is not None:
+            conv_state, ssm_state = state
+        Bsz = hn.shape[0]
+        if conv_state is not None:
+            self._check_state(conv_state, self.d_conv, "conv_state", Bsz)
+        if ssm_state is not None:
+            self._check_state(ssm_state, self.d_state, "ssm_state", Bsz)
+        use_inplace = ssm_state is not None and state is None and not return_state
+        cs_out = None
+        if return_state:
+            cs_dtype = conv_state.dtype if conv_state is not None else hn.dtype
+            cs_out = torch.empty((Bsz, self.d_inner, self.d_conv), dtype=cs_dtype,
+                                 device=hn.device)
+        h_last = None
+        if return_state or use_inplace:
+            h_last = ssm_state if ssm_state is not None else torch.empty(
+                (Bsz, self.d_inner, self.d_state), dtype=torch.float32, device=hn.device)
+        out = self._forward_padded(hn, seqlen, conv_state_in=conv_state, conv_state_out=cs_out,
+                                   h0=ssm_state, h_last=h_last)
+        if return_state:
+            return out, (cs_out, h_last)
+        return out
+
+    def forward(self, hidden_states: Tensor, inference_params: Optional[InferenceParamsLike] = None,
+                ssm_state: Optional[Tensor] = None, state: Optional[Tuple[Tensor, Tensor]] = None,
+                return_state: bool = False):
+        """hidden_states: (B, L, D) -> (B, L, D) [, (conv_state, ssm_state)]."""
+        if state is not None and ssm_state is not None:
+            raise ValueError("Pass either state or ssm_state, not both.")
+        if inference_params is not None and state is not None:
+            raise ValueError("state is not supported with inference_params.")
+        if not hidden_states.is_cuda:
+            raise RuntimeError(_CUDA_ERROR)
+        warn_if_grad(hidden_states, self.in_proj.weight)
+        with torch.no_grad():
+            return self._forward(hidden_states, inference_params, ssm_state, state, return_state)
+
+    def _forward(self, hs, inference_params, ssm_state, state, return_state):
+        batch, seqlen, dm = hs.shape
+        Lp = round_up(max(seqlen, 1))
+        if Lp == seqlen and hs.is_contiguous():
+            hp = hs
+        else:
+            hp = torch.zeros((batch, Lp, dm), dtype=hs.dtype, device=hs.device)
+            hp[:, :seqlen] = hs
+
+        def trim(o):
+            return o if Lp == seqlen else o[:, :seqlen].contiguous()
+
+        if inference_params is not None:
+            conv_state, cache_state = self._get_states_from_cache(inference_params, batch)
+            if ssm_state is None:
+                ssm_state = cache_state
+            if inference_params.seqlen_offset > 0:
+                out, _, _ = self.step(hs, conv_state, ssm_state)
+                return out
+            # prefill: conv restarts from zeros, the cache receives the last d_conv raw
+            # inputs and the final ssm state (in place); return_state is ignored.
+            self._check_state(ssm_state, self.d_state, "ssm_state", batch)
+            out = self._forward_padded(hp, seqlen, conv_state_out=conv_state, h0=ssm_state,
+                                       h_last=ssm_state)
+            return trim(out)
+        res = self.forward_padded(hp, seqlen, ssm_state=ssm_state, state=state,
+                                  return_state=return_state)
+        if return_state:
+            return trim(res[0]), res[1]
+        return trim(res)
+
+    def step(self, hidden_states: Tensor, conv_state: Tensor, ssm_state: Tensor):
+        """One-token decode (``mamba_simple.py:453-497``); states updated in place."""
+        if not hidden_states.is_cuda:
+            raise RuntimeError(_CUDA_ERROR)
+        assert hidden_states.shape[1] == 1, "Only support decoding with 1 token at a time for now"
+        with torch.no_grad():
+            A, Dv, dbias, cw, cb = self._fp32_params()
+            xz = self.in_proj(hidden_states.squeeze(1))  # (B, 2D)
+            x, z = xz.chunk(2, dim=-1)
+            x = K.causal_conv1d_update(x, conv_state, cw, cb, self.activation)
+            x_db = self.x_proj(x)
+            dt, Bm, Cm = torch.split(x_db, [self.dt_rank, self.d_state, self.d_state], dim=-1)
+            dt = F.linear(dt, self.dt_proj.weight)  # bias is added inside the step kernel
+            y = K.selective_state_update(ssm_state, x, dt, A, Bm, Cm, Dv, z=z, dt_bias=dbias,
+                                         dt_softplus=True)
+            out = self.out_proj(y)
+        return out.unsqueeze(1), conv_state, ssm_state
+
+    # ------------------------------------------------------------------ state allocation
+    def _zeros_states(self, batch_size, conv_dtype, ssm_dtype, device):
+        conv = torch.zeros(batch_size, self.d_inner, self.d_conv, device=device, dtype=conv_dtype)
+        ssm = torch.zeros(batch_size, self.d_inner, self.d_state, device=device, dtype=ssm_dtype)
+        return conv, ssm
+
+    def allocate_inference_cache(self, batch_size: int, max_seqlen: int, dtype=None, **kwargs):
+        return self._zeros_states(batch_size, self.conv1d.weight.dtype if dtype is None else dtype,
+                                  self.dt_proj.weight.dtype if dtype is None else dtype,
+                                  self.out_proj.weight.device)
+
+    def allocate_state(self, batch_size: int, dtype=None, device=None):
+        """Zero (conv_state, ssm_state) for chunked streaming."""
+        return self._zeros_states(batch_size, self.conv1d.weight.dtype if dtype is None else dtype,
+                                  self.dt_proj.weight.dtype if dtype is None else dtype,
+                                  self.out_proj.weight.device if device is None else device)
+
+    def _get_states_from_cache(self, inference_params: InferenceParamsLike, batch_size: int,
+                               initialize_states: bool = False):
+        assert self.layer_idx is not None
+        cache = inference_params.key_value_memory_dict
+        entry = cache.get(self.layer_idx)
+        if entry is None or entry[0].shape[0] != batch_size or entry[1].shape[0] != batch_size:
+            entry = self._zeros_states(batch_size, self.conv1d.weight.dtype,
+                                       self.dt_proj.weight.dtype, self.conv1d.weight.device)
+            cache[self.layer_idx] = entry
+        elif initialize_states:
+            entry[0].zero_()
+            entry[1].zero_()
+        return entry

@@ -1,0 +1,640 @@
+"""VideoMamba encoder on the HIP kernels (``models/videomamba/videomamba.py`` surface).
+
+Public classes and functions keep the reference's names, signatures, state_dict keys,
+initialisation, error types and messages: ``Block``, ``create_block``, ``PatchEmbed``,
+``PretrainVideoMamba``, ``load_state_dict``, ``build_videomamba``.
+
+``PretrainVideoMamba.forward_features`` runs its own layer loop on a padded token buffer
+(B, Lp, C), Lp = round_up(L, 8), padded rows held at exactly zero:
+
+    tubelet patch embed + pos adds (HIP, MFMA) -> [CLS row] -> optional mask gather
+    per layer: fused residual-add + RMSNorm (HIP) -> Mamba mixer (HIP conv/scan + GEMMs)
+    final fused add + norm (HIP) -> pooling (small torch ops) -> (x_vis, x_pool[, state])
+
+which is the same computation as calling ``Block.forward`` per layer on the unpadded
+tokens (``Block.forward`` itself is kept for callers that use blocks directly).
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+from functools import partial
+from typing import Any, Callable, Dict, List, Optional, Tuple, Union, cast
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+from . import kernels as K
+from .layers import DropPath, RMSNorm, round_up, to_2tuple, trunc_normal_, warn_if_grad
+from .mamba_simple import InferenceParamsLike, Mamba
+from .streaming import (STREAMING_CONTRACT_VERSION, ForwardReturnSemantics, StateShape,
+                        forward_return_semantics as _return_semantics)
+
+logger = logging.getLogger(__name__)
+
+LayerState = Union[Tensor, Tuple[Tensor, Tensor]]
+StateCollection = Union[List[LayerState], Tuple[LayerState, ...], Dict[int, LayerState]]
+
+
+def _infer_spatial_grid(token_count: int, reference_grid: Tuple[int, int]) -> Tuple[int, int]:
+    """Factor ``token_count`` into (h, w) closest in aspect ratio, then size, to the
+    reference grid (``videomamba.py:32-55``)."""
+    if token_count <= 0:
+        raise ValueError("Position embedding must contain at least one spatial token.")
+    rh, rw = reference_grid
+    target = float(rh) / float(rw)
+    candidates = []
+    for h in range(1, int(math.sqrt(token_count)) + 1):
+        if token_count % h == 0:
+            w = token_count // h
+            candidates += [(h, w), (w, h)]
+    if not candidates:
+        raise ValueError(f"Unable to infer spatial grid from token count {token_count}.")
+    return min(candidates, key=lambda hw: (abs(hw[0] / hw[1] - target),
+                                           abs(hw[0] - rh) + abs(hw[1] - rw)))
+
+
+def _norm_kind(norm: nn.Module) -> bool:
+    """True for RMSNorm, False for LayerNorm (the two norms fused_add_norm supports)."""
+    return isinstance(norm, RMSNorm)
+
+
+# ----------------------------------------------------------------------------- Block
+class Block(nn.Module):
+    """Add -> norm -> mixer block returning (hidden_states, residual[, state])
+    (``videomamba.py:87-253``)."""
+
+    def __init__(self, dim: int, mixer_cls: Callable[[int], nn.Module],
+                 norm_cls: Callable[[int], nn.Module] = nn.LayerNorm,
+                 fused_add_norm: bool = False, residual_in_fp32: bool = False,
+                 drop_path: float = 0.0):
+        super().__init__()
+        self.residual_in_fp32 = residual_in_fp32
+        self.fused_add_norm = fused_add_norm
+        self.mixer = mixer_cls(dim)
+        self.norm = norm_cls(dim)
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+        if self.fused_add_norm:
+            assert isinstance(self.norm, (nn.LayerNorm, RMSNorm)), \
+                "Only LayerNorm and RMSNorm are supported for fused_add_norm"
+
+    def _add_norm(self, hidden_states: Tensor, residual: Optional[Tensor], inplace: bool = False):
+        nw, nb, eps = self.norm.weight, self.norm.bias, self.norm.eps
+        is_rms = _norm_kind(self.norm)
+        if self.fused_add_norm:
+            h = hidden_states if residual is None else self.drop_path(hidden_states)
+            # internal residual buffers are updated in place; a caller's tensor never is
+            return K._norm(h, nw, nb, residual, True, self.residual_in_fp32, eps, is_rms,
+                           residual_out=residual if inplace and residual is not None else None)
+        residual = hidden_states if residual is None else residual + self.drop_path(hidden_states)
+        hidden = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms)
+        if self.residual_in_fp32:
+            residual = residual.to(torch.float32)
+        return hidden, residual
+
+    def forward(self, hidden_states: Tensor, residual: Optional[Tensor] = None,
+                inference_params: Optional[InferenceParamsLike] = None,
+                use_checkpoint: bool = False, ssm_state: Optional[Tensor] = None,
+                state: Optional[Tuple[Tensor, Tensor]] = None, return_state: bool = False):
+        """hidden_states = Mixer(Norm(residual + hidden_states)).  ``use_checkpoint`` is
+        accepted for API parity (the HIP path is inference-only, nothing to recompute)."""
+        if state is not None and ssm_state is not None:
+            raise ValueError("Pass either state or ssm_state, not both.")
+        K.require_gpu(hidden_states, residual, what="VideoMamba")
+        with torch.no_grad():
+            hidden, residual = self._add_norm(hidden_states, residual)
+        if state is not None:
+            if return_state:
+                hidden, new_state = self.mixer(hidden, inference_params=inference_params,
+                                               state=state, return_state=True)
+                return hidden, residual, new_state
+            hidden = self.mixer(hidden, inference_params=inference_params, state=state,
+                                return_state=False)
+            return hidden, residual
+        hidden = self.mixer(hidden, inference_params=inference_params, ssm_state=ssm_state)
+        return hidden, residual
+
+    def forward_padded(self, hidden: Tensor, residual: Optional[Tensor], seqlen: int,
+                       state=None, ssm_state=None, return_state: bool = False):
+        """Model-internal: same as ``forward`` on the padded (B, Lp, C) buffers."""
+        hn, residual = self._add_norm(hidden, residual, inplace=True)
+        res = self.mixer.forward_padded(hn, seqlen, ssm_state=ssm_state, state=state,
+                                        return_state=return_state)
+        if return_state:
+            return res[0], residual, res[1]
+        return res, residual, None
+
+    def allocate_inference_cache(self, batch_size: int, max_seqlen: int, dtype=None, **kwargs):
+        return self.mixer.allocate_inference_cache(batch_size, max_seqlen, dtype=dtype, **kwargs)
+
+
+def create_block(d_model: int, ssm_cfg: Optional[Dict[str, object]] = None,
+                 norm_epsilon: float = 1e-5, drop_path: float = 0.0, rms_norm: bool = True,
+                 residual_in_fp32: bool = True, fused_add_norm: bool = True,
+                 layer_idx: Optional[int] = None, bimamba: bool = True, device=None, dtype=None):
+    """``videomamba.py:256-291``: blocks are always unidirectional (bimamba=False); the
+    bidirectional composition lives in ``BiMambaRefinerBlock``."""
+    fk = {k: v for k, v in (("device", device), ("dtype", dtype)) if v is not None}
+    mixer_cls = partial(Mamba, layer_idx=layer_idx, bimamba=False, **(ssm_cfg or {}), **fk)
+    norm_cls = partial(RMSNorm if rms_norm else nn.LayerNorm, eps=norm_epsilon)
+    block = Block(d_model, mixer_cls, norm_cls=norm_cls, drop_path=drop_path,
+                  fused_add_norm=fused_add_norm, residual_in_fp32=residual_in_fp32)
+    object.__setattr__(block, "layer_idx", layer_idx)
+    return block
+
+
+def _init_weights(module, n_layer, initializer_range=0.02, rescale_prenorm_residual=True,
+                  n_residuals_per_layer=1):
+    """Mamba init (``videomamba.py:295-324``): zero Linear biases (except dt bias), and
+    kaiming-uniform / sqrt(n_layer) for every mixer's out_proj."""
+    if isinstance(module, nn.Linear):
+        if module.bias is not None and not getattr(module.bias, "_no_reinit", False):
+            nn.init.zeros_(module.bias)
+    elif isinstance(module, nn.Embedding):
+        nn.init.normal_(module.weight, std=initializer_range)
+    if rescale_prenorm_residual:
+        for name, p in module.named_parameters():
+            if name in ("out_proj.weight", "fc2.weight"):
+                nn.init.kaiming_uniform_(p, a=math.sqrt(5))
+                with torch.no_grad():
+                    p /= math.sqrt(n_residuals_per_layer * n_layer)
+
+
+def segm_init_weights(m):
+    if isinstance(m, nn.Linear):
+        trunc_normal_(m.weight, std=0.02)
+        if m.bias is not None:
+            nn.init.constant_(m.bias, 0)
+    elif isinstance(m, nn.LayerNorm):
+        nn.init.constant_(m.bias, 0)
+        nn.init.constant_(m.weight, 1.0)
+
+
+# ----------------------------------------------------------------------------- patch embed
+class PatchEmbed(nn.Module):
+    """Tubelet embedding Conv3d(kernel = stride = (kernel_size, P, P)); the conv runs as
+    the HIP implicit-GEMM kernel."""
+
+    def __init__(self, img_size=224, patch_size=16, kernel_size=1, in_chans=3, embed_dim=768):
+        super().__init__()
+        img = to_2tuple(img_size)
+        patch = to_2tuple(patch_size)
+        self.img_size = img
+        self.patch_size = patch
+        self.num_patches = (img[1] // patch[1]) * (img[0] // patch[0])
+        self.tubelet_size = kernel_size
+        self.proj = nn.Conv3d(in_chans, embed_dim, kernel_size=(kernel_size, patch[0], patch[1]),
+                              stride=(kernel_size, patch[0], patch[1]))
+
+    def embed_tokens(self, x: Tensor, spos: Tensor, tpos: Tensor, out: Tensor, row0: int):
+        if self.patch_size[0] != self.patch_size[1]:
+            raise NotImplementedError("non-square patches are not supported by the HIP kernel")
+        K.patch_embed(x, self.proj.weight, self.proj.bias, spos, tpos, out, row0,
+                      out.stride(0))
+
+    def forward(self, x: Tensor) -> Tensor:
+        K.require_gpu(x, what="PatchEmbed")
+        B, _, T, H, W = x.shape
+        P = self.patch_size[0]
+        Tt, Gh, Gw = T // self.tubelet_size, H // P, W // P
+        C = self.proj.out_channels
+        dt = self.proj.weight.dtype
+        out = torch.empty((B, Tt * Gh * Gw, C), dtype=dt, device=x.device)
+        with torch.no_grad():
+            zs = torch.zeros((Gh * Gw, C), dtype=dt, device=x.device)
+            zt = torch.zeros((Tt, C), dtype=dt, device=x.device)
+            self.embed_tokens(x, zs, zt, out, 0)
+        return out.view(B, Tt, Gh, Gw, C).permute(0, 4, 1, 2, 3)
+
+
+# ----------------------------------------------------------------------------- encoder
+class PretrainVideoMamba(nn.Module):
+    streaming_contract_version: str = STREAMING_CONTRACT_VERSION
+
+    def __init__(self, img_size: int = 224, patch_size: int = 16, depth: int = 24,
+                 embed_dim: int = 192, channels: int = 3, drop_path_rate: float = 0.0,
+                 ssm_cfg: Optional[Dict[str, object]] = None, norm_epsilon: float = 1e-5,
+                 initializer_cfg: Optional[Dict[str, object]] = None,
+                 fused_add_norm: bool = True, rms_norm: bool = True,
+                 residual_in_fp32: bool = True, bimamba: bool = True,
+                 pool_type: str = "cls+avg", kernel_size: int = 1, num_frames: int = 8,
+                 device=None, dtype=None, use_checkpoint: bool = False,
+                 checkpoint_num: int = 0, add_pool_norm: bool = True):
+        fk = {k: v for k, v in (("device", device), ("dtype", dtype)) if v is not None}
+        super().__init__()
+        if not bimamba:
+            raise NotImplementedError(
+                "This minimal VideoMamba package only supports bimamba=True.")
+        self.residual_in_fp32 = residual_in_fp32
+        self.fused_add_norm = fused_add_norm
+        self.use_checkpoint = use_checkpoint
+        self.checkpoint_num = checkpoint_num
+        self.depth = depth
+        self.pool_type = pool_type
+        logger.info("Use checkpoint: %s, checkpoint number: %s, pool type: %s",
+                    use_checkpoint, checkpoint_num, pool_type)
+        self.d_model = self.num_features = self.embed_dim = embed_dim
+
+        self.patch_embed = PatchEmbed(img_size=img_size, patch_size=patch_size,
+                                      kernel_size=kernel_size, in_chans=channels,
+                                      embed_dim=embed_dim)
+        num_patches = self.patch_embed.num_patches
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, num_patches + 1, embed_dim))
+        self.temporal_pos_embedding = nn.Parameter(
+            torch.zeros(1, num_frames // kernel_size, embed_dim))
+        dpr = [v.item() for v in torch.linspace(0, drop_path_rate, depth)]
+        inter_dpr = [0.0] + dpr
+        self.drop_path = DropPath(drop_path_rate) if drop_path_rate > 0.0 else nn.Identity()
+        self.layers = nn.ModuleList([
+            create_block(embed_dim, ssm_cfg=ssm_cfg, norm_epsilon=norm_epsilon,
+                         rms_norm=rms_norm, residual_in_fp32=residual_in_fp32,
+                         fused_add_norm=fused_add_norm, layer_idx=i, bimamba=bimamba,
+                         drop_path=inter_dpr[i], **fk)
+            for i in range(depth)])
+        self.norm = (RMSNorm if rms_norm else nn.LayerNorm)(embed_dim, eps=norm_epsilon, **fk)
+        self.add_pool_norm = add_pool_norm
+        if add_pool_norm:
+            self.pool_norm = nn.LayerNorm(embed_dim)
+
+        self.apply(segm_init_weights)
+        trunc_normal_(self.pos_embed, std=0.02)
+        self.apply(partial(_init_weights, n_layer=depth, **(initializer_cfg or {})))
+
+    # ------------------------------------------------------------------ state API
+    def _mixers(self):
+        return [layer.mixer for layer in self.layers]
+
+    def allocate_inference_cache(self, batch_size: int, max_seqlen: int, dtype=None, **kwargs):
+        return {i: layer.allocate_inference_cache(batch_size, max_seqlen, dtype=dtype, **kwargs)
+                for i, layer in enumerate(self.layers)}
+
+    def init_ssm_state(self, batch_size: int, dtype=None, device=None, as_dict: bool = False):
+        states = []
+        for layer in self.layers:
+            _, s = layer.allocate_inference_cache(batch_size, max_seqlen=1, dtype=dtype)
+            states.append(s if device is None else s.to(device=device))
+        return dict(enumerate(states)) if as_dict else states
+
+    def allocate_state(self, batch_size: int, dtype=None, device=None, as_dict: bool = False):
+        """Per-layer zero (conv_state, ssm_state) for chunked execution (contract
+        ``self.streaming_contract_version``)."""
+        states = [m.allocate_state(batch_size, dtype=dtype, device=device) for m in self._mixers()]
+        return dict(enumerate(states)) if as_dict else states
+
+    def init_state(self, batch_size: int, dtype=None, device=None, as_dict: bool = False):
+        """Backward-compatible alias for ``allocate_state``."""
+        return self.allocate_state(batch_size=batch_size, dtype=dtype, device=device,
+                                   as_dict=as_dict)
+
+    def expected_state_shapes(self, batch_size: int) -> Dict[int, StateShape]:
+        if batch_size <= 0:
+            raise ValueError("batch_size must be a positive integer.")
+        return {i: StateShape(conv_state=(batch_size, int(m.d_inner), int(m.d_conv)),
+                              ssm_state=(batch_size, int(m.d_inner), int(m.d_state)))
+                for i, m in enumerate(self._mixers())}
+
+    def forward_return_semantics(self) -> ForwardReturnSemantics:
+        return _return_semantics(self.add_pool_norm)
+
+    @torch.jit.ignore()
+    def no_weight_decay(self):
+        return {"pos_embed", "cls_token", "temporal_pos_embedding"}
+
+    def get_num_layers(self):
+        return len(self.layers)
+
+    @torch.jit.ignore()
+    def load_pretrained(self, checkpoint_path, prefix=""):
+        raise NotImplementedError("ViT .npz weight loading is not part of the VideoMamba "
+                                  "encoder; use load_state_dict(...) with a plain state_dict.")
+
+    # ------------------------------------------------------------------ helpers
+    def _get_layer_state(self, state, layer_idx: int):
+        if state is None:
+            return None
+        if isinstance(state, dict):
+            return state.get(layer_idx)
+        if isinstance(state, (list, tuple)):
+            return state[layer_idx]
+        raise TypeError("state must be a list, tuple, or dict indexed by layer id")
+
+    def _validate_temporal_length(self, frame_count: int) -> int:
+        k = self.patch_embed.tubelet_size
+        if frame_count <= 0:
+            raise ValueError("Input must contain at least one frame.")
+        if frame_count % k:
+            raise ValueError(
+                f"Input frame count ({frame_count}) must be divisible by tubelet size ({k}).")
+        return frame_count // k
+
+    def _spatial_token_grid(self, height: int, width: int) -> Tuple[int, int]:
+        ph, pw = self.patch_embed.patch_size
+        if height < ph or width < pw:
+            raise ValueError("Input spatial size must be at least one patch: "
+                             f"got ({height}, {width}) with patch size ({ph}, {pw}).")
+        return height // ph, width // pw
+
+    def _get_spatial_pos_embedding(self, grid_h: int, grid_w: int, dtype=None, device=None):
+        device = self.pos_embed.device if device is None else device
+        dtype = self.pos_embed.dtype if dtype is None else dtype
+        patch_pos = self.pos_embed[:, 1:]
+        ph, pw = self.patch_embed.patch_size
+        bh, bw = self.patch_embed.img_size[0] // ph, self.patch_embed.img_size[1] // pw
+        if bh * bw != patch_pos.shape[1]:
+            bh, bw = _infer_spatial_grid(patch_pos.shape[1], (bh, bw))
+        if (grid_h, grid_w) == (bh, bw):
+            return patch_pos.to(device=device, dtype=dtype)
+        grid = patch_pos.reshape(1, bh, bw, self.embed_dim).permute(0, 3, 1, 2).float()
+        grid = F.interpolate(grid, size=(grid_h, grid_w), mode="bicubic", align_corners=False)
+        return grid.permute(0, 2, 3, 1).reshape(1, grid_h * grid_w, self.embed_dim).to(
+            device=device, dtype=dtype)
+
+    def _has_cls_token_for_forward(self, ssm_state, temporal_pos_offset: int) -> bool:
+        if ssm_state is None or temporal_pos_offset <= 0:
+            return True
+        first = self._get_layer_state(ssm_state, 0)
+        return not (isinstance(first, (list, tuple)) and len(first) == 2)
+
+    def _get_temporal_pos_embedding(self, seqlen: int, offset: int = 0, dtype=None, device=None):
+        """Temporal embedding slice [offset, offset+seqlen); linearly interpolated to
+        ``offset+seqlen`` entries when that exceeds the table (``videomamba.py:655-675``)."""
+        if offset < 0:
+            raise ValueError("temporal_pos_offset must be non-negative.")
+        device = self.temporal_pos_embedding.device if device is None else device
+        dtype = self.temporal_pos_embedding.dtype if dtype is None else dtype
+        table = self.temporal_pos_embedding.to(device=device, dtype=dtype)
+        end = offset + seqlen
+        if end > table.shape[1]:
+            table = F.interpolate(table.permute(0, 2, 1).float(), size=end, mode="linear",
+                                  align_corners=False).permute(0, 2, 1).to(dtype=dtype)
+        return table[:, offset:end]
+
+    def _normalize_mask(self, mask, batch_size, token_count, device, require_cls_visible):
+        if mask is None:
+            return None
+        if mask.ndim != 2:
+            raise ValueError("mask must be 2D with shape [B, N].")
+        if mask.shape[0] != batch_size:
+            raise ValueError(
+                f"mask batch size mismatch: expected {batch_size}, got {mask.shape[0]}.")
+        mask = mask.to(device=device, dtype=torch.bool)
+        if mask.shape[1] != token_count:
+            raise ValueError(
+                f"mask token length mismatch: expected {token_count}, got {mask.shape[1]}.")
+        if require_cls_visible and token_count > 0 and bool(mask[:, 0].any()):
+            raise ValueError("mask must keep CLS token visible (mask[:, 0] must be False).")
+        return mask
+
+    def _visible_token_positions(self, mask, batch_size, token_count, device,
+                                 require_cls_visible):
+        """(normalized mask, ascending visible positions per sample) or (None, None)."""
+        mask = self._normalize_mask(mask, batch_size, token_count, device, require_cls_visible)
+        if mask is None:
+            return None, None
+        visible = ~mask
+        counts = visible.sum(dim=1)
+        if counts.numel() > 0 and not bool((counts == counts[0]).all()):
+            raise ValueError("mask must keep the same number of visible tokens per sample; "
+                             f"got per-sample counts: {counts.tolist()}.")
+        n_vis = int(counts[0].item()) if counts.numel() > 0 else 0
+        if counts.numel() > 0 and n_vis <= 0:
+            raise ValueError("mask must keep at least one visible token per sample.")
+        pos = torch.arange(token_count, device=device).unsqueeze(0).expand(batch_size, -1)
+        pos = pos.masked_fill(mask, token_count)
+        return mask, torch.sort(pos, dim=1).values[:, :n_vis]
+
+    def _masked_temporal_average(self, patch_tokens, visible_positions, temporal_tokens,
+                                 tokens_per_frame, has_cls_token):
+        """Per-frame mean of the visible patch tokens (``videomamba.py:702-751``)."""
+        if patch_tokens.ndim != 3:
+            raise ValueError("patch_tokens must have shape [B, N, C].")
+        if visible_positions.ndim != 2:
+            raise ValueError("visible_positions must have shape [B, N_total_visible].")
+        if patch_tokens.shape[0] != visible_positions.shape[0]:
+            raise ValueError("Batch size mismatch between patch_tokens and visible_positions.")
+        if visible_positions.shape[1] != patch_tokens.shape[1] + (1 if has_cls_token else 0):
+            raise ValueError("visible_positions and patch_tokens lengths are inconsistent.")
+        if has_cls_token and visible_positions.numel() > 0 and \
+                not bool((visible_positions[:, 0] == 0).all()):
+            raise ValueError("mask must keep CLS token visible for temporal pooling.")
+        ppos = visible_positions[:, 1:] - 1 if has_cls_token else visible_positions
+        frame = torch.div(ppos, tokens_per_frame, rounding_mode="floor").long()
+        Bsz, n, C = patch_tokens.shape
+        sums = patch_tokens.new_zeros(Bsz, temporal_tokens, C)
+        sums.scatter_add_(1, frame.unsqueeze(-1).expand(-1, -1, C), patch_tokens)
+        counts = patch_tokens.new_zeros(Bsz, temporal_tokens, 1)
+        counts.scatter_add_(1, frame.unsqueeze(-1), patch_tokens.new_ones(Bsz, n, 1))
+        if bool((counts == 0).any()):
+            raise ValueError("keep_temporal with masking requires at least one visible patch "
+                             "token for each temporal slice.")
+        return sums / counts
+
+    # ------------------------------------------------------------------ forward
+    def _embed(self, x: Tensor, has_cls: bool, temporal_pos_offset: int):
+        """Patch embed + positional adds (+ CLS row) into a zero-padded (B, Lp, C) buffer."""
+        Bsz, _, T, H, W = x.shape
+        k = self.patch_embed.tubelet_size
+        P = self.patch_embed.patch_size[0]
+        Tt, Gh, Gw = T // k, H // P, W // P
+        dt = self.patch_embed.proj.weight.dtype
+        spos = self._get_spatial_pos_embedding(Gh, Gw, dtype=dt, device=x.device)
+        tpos = self._get_temporal_pos_embedding(Tt, offset=temporal_pos_offset, dtype=dt,
+                                                device=x.device)
+        L = Tt * Gh * Gw + (1 if has_cls else 0)
+        Lp = round_up(L)
+        buf = torch.empty((Bsz, Lp, self.embed_dim), dtype=dt, device=x.device)
+        self.patch_embed.embed_tokens(x, spos[0], tpos[0], buf, 1 if has_cls else 0)
+        if has_cls:
+            buf[:, 0] = (self.cls_token + self.pos_embed[:, :1].to(dtype=dt))[:, 0].to(dt)
+        if Lp > L:
+            buf[:, L:] = 0
+        return buf, L, Tt, Gh * Gw
+
+    def forward_features(self, x: Tensor, mask: Optional[Tensor] = None, use_image: bool = False,
+                         ssm_state: Optional[StateCollection] = None,
+                         temporal_pos_offset: int = 0):
+        """Features (B, N_vis, C) [+ next state] (``videomamba.py:786-941``)."""
+        if x.ndim != 5:
+            raise ValueError("x must have shape [B, C, T, H, W].")
+        self._validate_temporal_length(x.shape[2])
+        K.require_gpu(x, what="VideoMamba")
+        warn_if_grad(x, self.patch_embed.proj.weight)
+        with torch.no_grad():
+            return self._forward_features(x, mask, ssm_state, temporal_pos_offset)
+
+    def _forward_features(self, x, mask, ssm_state, temporal_pos_offset):
+        has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
+        h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset)
+        Bsz = x.shape[0]
+        _, visible = self._visible_token_positions(mask, Bsz, L, x.device,
+                                                   require_cls_visible=has_cls)
+        if visible is not None:
+            gathered = h[:, :L].gather(1, visible.unsqueeze(-1).expand(-1, -1, self.embed_dim))
+            L = gathered.shape[1]
+            h = torch.zeros((Bsz, round_up(L), self.embed_dim), dtype=h.dtype, device=h.device)
+            h[:, :L] = gathered
+
+        residual = None
+        new_states = None
+        tuple_out = False
+        for idx, layer in enumerate(self.layers):
+            layer_state = self._get_layer_state(ssm_state, idx)
+            full = isinstance(layer_state, (list, tuple)) and len(layer_state) == 2
+            if full and new_states is None:
+                if isinstance(ssm_state, dict):
+                    new_states = {}
+                else:
+                    new_states = [None] * len(self.layers)
+                    tuple_out = isinstance(ssm_state, tuple)
+            if full:
+                h, residual, layer_state = layer.forward_padded(
+                    h, residual, L, state=tuple(layer_state), return_state=True)
+            else:
+                h, residual, _ = layer.forward_padded(h, residual, L, ssm_state=layer_state)
+            if new_states is not None:
+                new_states[idx] = layer_state
+
+        nw, nb, eps = self.norm.weight, self.norm.bias, self.norm.eps
+        is_rms = _norm_kind(self.norm)
+        if self.fused_add_norm:
+            out = K._norm(self.drop_path(h), nw, nb, residual, False, self.residual_in_fp32,
+                          eps, is_rms)
+        else:
+            residual = h if residual is None else residual + self.drop_path(h)
+            out = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms)
+        x_vis = out[:, :L].contiguous()
+
+        if new_states is not None and isinstance(new_states, list):
+            if any(s is None for s in new_states):
+                raise ValueError("Expected full state for all layers.")
+            return x_vis, (tuple(new_states) if tuple_out else new_states)
+        if ssm_state is None:
+            return x_vis
+        if new_states is not None:
+            return x_vis, new_states
+        return x_vis, ssm_state
+
+    def forward(self, x: Tensor, mask: Optional[Tensor] = None, use_image: bool = False,
+                keep_temporal: bool = False, ssm_state: Optional[StateCollection] = None,
+                temporal_pos_offset: int = 0):
+        """(x_vis, x_pool[, next_state]) with ``add_pool_norm``, else x_vis[, next_state]
+        (``videomamba.py:943-1067``)."""
+        if x.ndim != 5:
+            raise ValueError("x must have shape [B, C, T, H, W].")
+        gh, gw = self._spatial_token_grid(x.shape[-2], x.shape[-1])
+        per_frame = gh * gw
+        temporal_tokens = self._validate_temporal_length(x.shape[2])
+        has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
+        feats = self.forward_features(x, mask, use_image, ssm_state=ssm_state,
+                                      temporal_pos_offset=temporal_pos_offset)
+        if ssm_state is None:
+            x_vis = feats
+        else:
+            x_vis, ssm_state = feats
+        if not self.add_pool_norm:
+            return x_vis if ssm_state is None else (x_vis, ssm_state)
+        with torch.no_grad():
+            x_vis, x_pool = self._pool(x, x_vis, mask, keep_temporal, has_cls, temporal_tokens,
+                                       per_frame)
+        return (x_vis, x_pool) if ssm_state is None else (x_vis, x_pool, ssm_state)
+
+    def _pool(self, x, x_vis, mask, keep_temporal, has_cls, temporal_tokens, per_frame):
+        cls_tok = x_vis[:, :1] if has_cls else None
+        patch = x_vis[:, 1:] if has_cls else x_vis
+        pool = self.pool_type
+        if pool in {"cls", "cls+avg", "cls_cat_avg"} and cls_tok is None:
+            raise ValueError(
+                f"pool_type='{pool}' requires a CLS token, but continuation "
+                "streaming chunks (temporal_pos_offset > 0 with full state) do not include CLS. "
+                "Use pool_type='avg' for chunked streaming.")
+        if pool != "cls" and patch.shape[1] == 0:
+            raise ValueError("mask must keep at least one patch token visible when using "
+                             f"pool_type='{pool}'.")
+        if pool == "cls":
+            return patch, self.pool_norm(cls_tok)
+        if keep_temporal:
+            Bsz, _, C = patch.shape
+            if mask is None:
+                avg = patch.reshape(Bsz, temporal_tokens, per_frame, C).mean(2)
+            else:
+                full = (1 if has_cls else 0) + temporal_tokens * per_frame
+                _, vis = self._visible_token_positions(mask, Bsz, full, x.device,
+                                                       require_cls_visible=has_cls)
+                avg = self._masked_temporal_average(patch, vis, temporal_tokens, per_frame,
+                                                    has_cls)
+        else:
+            avg = patch.mean(1, keepdim=True)
+        if pool == "cls+avg":
+            pooled = self.pool_norm(cls_tok + avg)
+        elif pool == "cls_cat_avg":
+            pooled = self.pool_norm(torch.cat([cls_tok, avg], dim=1))
+        elif pool == "avg":
+            pooled = self.pool_norm(avg)
+        else:
+            raise ValueError(f"Unsupported pool_type: {pool}")
+        return patch, pooled
+
+
+# ----------------------------------------------------------------------------- loading
+def load_state_dict(pretrained_path, model, ckpt_num_frame, num_frames):
+    """Load a plain state_dict checkpoint with spatial (bicubic) and temporal (linear)
+    positional-embedding interpolation (``videomamba.py:1070-1147``).  Only the
+    ``weights_only=True`` loader is used."""
+    logger.info("Loading pretrained weights from %s", pretrained_path)
+    ckpt = torch.load(pretrained_path, map_location="cpu", weights_only=True)
+    if not isinstance(ckpt, dict):
+        raise TypeError("Expected a plain state_dict (dict) checkpoint.")
+    if "model" in ckpt or "module" in ckpt:
+        raise ValueError("Checkpoint wrapper keys ('model'/'module') are not supported. "
+                         "Pass a plain state_dict checkpoint.")
+    pe = model.patch_embed
+    pos = ckpt["pos_embed"]
+    C = pos.shape[-1]
+    n_extra = model.pos_embed.shape[-2] - pe.num_patches
+    gh, gw = pe.img_size[0] // pe.patch_size[0], pe.img_size[1] // pe.patch_size[1]
+    if gh * gw != pe.num_patches:
+        raise ValueError(f"Model patch grid size mismatch: {gh}x{gw} != num_patches({pe.num_patches}).")
+    oh, ow = _infer_spatial_grid(pos.shape[-2] - n_extra, (gh, gw))
+    if (oh, ow) != (gh, gw):
+        logger.info("Position interpolate from %dx%d to %dx%d", oh, ow, gh, gw)
+        grid = pos[:, n_extra:].reshape(-1, oh, ow, C).permute(0, 3, 1, 2)
+        grid = F.interpolate(grid, size=(gh, gw), mode="bicubic", align_corners=False)
+        grid = grid.permute(0, 2, 3, 1).reshape(-1, gh * gw, C)
+        ckpt["pos_embed"] = torch.cat((pos[:, :n_extra], grid), dim=1)
+    if ckpt_num_frame is None or ckpt_num_frame <= 0:
+        raise ValueError("ckpt_num_frame must be a positive integer when loading pretrained weights.")
+    t_old = ckpt_num_frame // pe.tubelet_size
+    t_new = num_frames // pe.tubelet_size
+    if t_old != t_new:
+        logger.info("Temporal interpolate from %d to %d", t_old, t_new)
+        tpe = ckpt["temporal_pos_embedding"].permute(0, 2, 1)
+        tpe = F.interpolate(tpe, size=(t_new,), mode="linear", align_corners=False)
+        ckpt["temporal_pos_embedding"] = tpe.permute(0, 2, 1)
+    msg = model.load_state_dict(ckpt, strict=True)
+    logger.info(msg)
+
+
+_BUILD_FIELDS = ("channels", "img_size", "patch_size", "depth", "embed_dim", "drop_path_rate",
+                 "ssm_cfg", "norm_epsilon", "fused_add_norm", "rms_norm", "residual_in_fp32",
+                 "bimamba", "pool_type", "kernel_size", "num_frames", "use_checkpoint",
+                 "checkpoint_num")
+
+
+def build_videomamba(config, add_pool_norm=True):
+    """Build from ``config.vision_encoder`` (``videomamba.py:1150-1200``); every field is
+    required (``channels`` first: a config with ``in_chans`` raises AttributeError)."""
+    vc = config.vision_encoder
+    kw = {name: getattr(vc, name) for name in _BUILD_FIELDS}
+    model = PretrainVideoMamba(add_pool_norm=add_pool_norm, **kw)
+    object.__setattr__(model, "default_cfg", {"url": ""})
+    pretrained = vc.pretrained
+    if pretrained is not None:
+        load_state_dict(pretrained_path=pretrained, model=model,
+                        ckpt_num_frame=vc.ckpt_num_frame, num_frames=kw["num_frames"])
+    else:
+        logger.info("No pretrained weights!!!")
+    return model
