@@ -21,6 +21,8 @@
 // Per (element, state) the VALU cost is 2 exp-equivalents + ~6 FMA-class ops; the
 // scan adds ~(4*steps+3)/K per element-state.
 
+#include <stdlib.h>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -259,6 +261,385 @@ __global__ __launch_bounds__(64 * NW) void scan_fwd_kernel(const ScanParams p) {
   }
 }
 
+// --------------------------------------------------------------------- scan v3
+// Throughput path.  One wave = one channel row (b, d); lanes over time, K steps per lane,
+// blocks of 64*K steps; a workgroup = NW channels of one batch row sharing the B/C
+// staging.  Per block the per-lane delta sums and their 64-lane prefix structure are
+// computed once; per state the Hillis-Steele (a, b) scan then needs only
+//     b += exp2(A * S_range) * dpp_shift(b)
+// where S_range (sum of delta over the lanes the current pair already covers) is
+// state-independent, so the exps sit off the serial DPP chain and invalid DPP sources
+// read 0 (bound_ctrl) with no "old"-value moves.  G states are interleaved per pass
+// (G independent fold / scan / sweep chains).  B/C are staged per block in LDS as fp32
+// in a [state][K/4][lane][4] layout: every ds_read_b128 is 64 consecutive 16-byte words.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dppz(float v) {  // invalid source lanes read 0
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, true));
+}
+
+template <typename T, int K, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
+  constexpr int TB = 64 * K;
+  constexpr int KQ = K / 4;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sB = smem;                  // [kMaxN][KQ][64][4]
+  float* sC = smem + kMaxN * TB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.y;
+  const int d_raw = blockIdx.x * NW + wave;
+  const bool active = d_raw < p.dim;
+  const int d = active ? d_raw : p.dim - 1;
+  const int N = p.dstate;
+  const int L = p.seqlen;
+  const int LO = p.out_len;
+  const bool vx = p.vec_x != 0;
+
+  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
+  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
+  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
+  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
+  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
+
+  float A2[kMaxN], carry[kMaxN];  // wave-uniform
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) {
+    A2[n] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
+    carry[n] = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
+  }
+  const float Dv = p.D ? p.D[d] : 0.0f;
+  const float bias = p.dbias ? p.dbias[d] : 0.0f;
+
+  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
+    // ---- stage B/C (fp32, lane-interleaved) ----
+    __syncthreads();
+    const int chunks = 2 * N * (TB / 8);
+    for (int idx = tid; idx < chunks; idx += 64 * NW) {
+      const int row = idx / (TB / 8);
+      const int c8 = idx - row * (TB / 8);
+      const bool isC = row >= N;
+      const int n = isC ? row - N : row;
+      const T* src = isC ? Cb + n * p.c_sn : Bb + n * p.b_sn;
+      const int t = t_blk + c8 * 8;
+      float w[8];
+      if (p.vec_bc && t + 8 <= L) {
+        load8(src + t, w);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
+      }
+      // block-relative step r = c8*8 + j -> lane r/K, k = r%K
+      float* base = (isC ? sC : sB) + n * TB;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int r = c8 * 8 + 4 * q;
+        const int ln = r / K, k = r - ln * K;
+        *reinterpret_cast<float4*>(base + ((k >> 2) * 64 + ln) * 4) =
+            make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      }
+    }
+    __syncthreads();
+
+    // ---- per-lane prologue ----
+    const int t0 = t_blk + lane * K;
+    float dl[K], du[K], y[K];
+    {
+      float uv[K], dv[K];
+      load_k<T, K>(urow, t0, L, vx, uv);
+      load_k<T, K>(drow, t0, L, vx, dv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dd = dv[k] + bias;
+        if (p.softplus) dd = softplus(dd);
+        dd = (t0 + k < L) ? dd : 0.0f;
+        dl[k] = dd;
+        du[k] = dd * uv[k];
+        y[k] = Dv * uv[k];
+      }
+    }
+    // delta range sums for the scan steps (state independent)
+    float sd = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) sd += dl[k];
+    float prow = sd;
+    float s1, s2, s4, s8;
+    {
+      float t = dppz<0x111>(prow); s1 = prow;            prow += t;
+      t = dppz<0x112>(prow);       s2 = prow;            prow += t;
+      t = dppz<0x114>(prow);       s4 = prow;            prow += t;
+      t = dppz<0x118>(prow);       s8 = prow;            prow += t;
+    }
+    // s1 = sd, s2 = sum of lanes (i-1, i], s4 = (i-3, i], s8 = (i-7, i] within the row
+    const float srow = prow;                 // row-inclusive prefix: range before bcast15
+    const float shalf = prow + dppz<0x142, 0xa>(prow);  // half-inclusive: range before bcast31
+
+    // ---- states, G at a time ----
+#pragma unroll
+    for (int n0 = 0; n0 < kMaxN; n0 += G) {
+      if (n0 < N) {
+        float a[G][K], bb[G][K], fold[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int n = n0 + g;
+          const float* bs = sB + n * TB + lane * 4;
+          fold[g] = 0.0f;
+#pragma unroll
+          for (int kq = 0; kq < KQ; ++kq) {
+            const float4 q = *reinterpret_cast<const float4*>(bs + kq * 256);
+            const float bv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int k = kq * 4 + i;
+              a[g][k] = __builtin_amdgcn_exp2f(dl[k] * A2[n]);
+              bb[g][k] = du[k] * bv[i];
+              fold[g] = fmaf(a[g][k], fold[g], bb[g][k]);
+            }
+          }
+        }
+        // carry enters the wave at lane 0
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int n = n0 + g;
+          const float aa = __builtin_amdgcn_exp2f(sd * A2[n]);
+          if (lane == 0) fold[g] = fmaf(aa, carry[n], fold[g]);
+        }
+        // 64-lane inclusive scan of b; a-products from the delta range sums
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int n = n0 + g;
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(s1 * A2[n]), dppz<0x111>(fold[g]), fold[g]);
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(s2 * A2[n]), dppz<0x112>(fold[g]), fold[g]);
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(s4 * A2[n]), dppz<0x114>(fold[g]), fold[g]);
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(s8 * A2[n]), dppz<0x118>(fold[g]), fold[g]);
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(srow * A2[n]), dppz<0x142, 0xa>(fold[g]), fold[g]);
+          fold[g] = fmaf(__builtin_amdgcn_exp2f(shalf * A2[n]), dppz<0x143, 0xc>(fold[g]), fold[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int n = n0 + g;
+          float h = dppz<0x138>(fold[g]);  // wave_shr:1: exclusive prefix (lane 0 reads 0)
+          if (lane == 0) h = carry[n];
+          carry[n] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[g]), 63));
+          const float* cs = sC + n * TB + lane * 4;
+#pragma unroll
+          for (int kq = 0; kq < KQ; ++kq) {
+            const float4 q = *reinterpret_cast<const float4*>(cs + kq * 256);
+            const float cv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int k = kq * 4 + i;
+              h = fmaf(a[g][k], h, bb[g][k]);
+              y[k] = fmaf(h, cv[i], y[k]);
+            }
+          }
+        }
+      }
+    }
+
+    if (zrow) {
+      float zv[K];
+      load_k<T, K>(zrow, t0, L, vx, zv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) y[k] *= silu(zv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
+    if (active && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y);
+  }
+
+  if (p.hl && active && lane == 0) {
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n)
+      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[n]);
+  }
+}
+
+template <typename T, int K, int G, int NW>
+static void launch_v3(const ScanParams& p, hipStream_t s) {
+  const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
+  dim3 grid((p.dim + NW - 1) / NW, p.batch);
+  hipLaunchKernelGGL((scan_v3_kernel<T, K, G, NW>), grid, dim3(64 * NW), lds, s, p);
+}
+
+// --------------------------------------------------------------------- time-split scan
+// Scan v2 (the production path).  A workgroup owns NC channels of one batch row and the
+// WHOLE sequence: S waves (S <= 8) each cover 64*K consecutive timesteps, K per lane.
+// Per state n:
+//   1. each lane folds its K steps of every channel into (a, b) pairs (zero carry),
+//      a 64-lane DPP scan gives the in-wave inclusive b, and lane 63 publishes the wave
+//      total b to LDS (double-buffered by state parity);
+//   2. one workgroup barrier;
+//   3. each wave composes the totals of the waves before it onto the block carry (the
+//      wave products are exp2(A*sum(delta)), from per-wave delta sums published once per
+//      super-block), gets its lanes' carry-in as exp2(A*prefix_delta)*carry + b_excl,
+//      and re-sweeps its K steps emitting y += C*h.
+// B_t / C_t rows are read straight from L2 with 16-byte loads and shared by the NC
+// channels of the wave.  Sequences longer than 8*64*K run as super-blocks with the
+// block carry composed through all S waves.
+template <typename T, int K>
+__device__ __forceinline__ void load_row_k(const T* row, int t0, int L, bool vec, float (&v)[K]) {
+  load_k<T, K>(row, t0, L, vec, v);
+}
+
+__device__ __forceinline__ float wave_incl_sum(float v) {
+  v += dpp_f<0x111>(0.0f, v);
+  v += dpp_f<0x112>(0.0f, v);
+  v += dpp_f<0x114>(0.0f, v);
+  v += dpp_f<0x118>(0.0f, v);
+  v += dpp_f<0x142, 0xa>(0.0f, v);
+  v += dpp_f<0x143, 0xc>(0.0f, v);
+  return v;
+}
+
+template <typename T, int K, int NC>
+__global__ __launch_bounds__(512) void scan_tw_kernel(const ScanParams p, const int S) {
+  constexpr int TW = 64 * K;
+  __shared__ float s_sdw[NC][8];
+  __shared__ float s_bt[2][NC][8];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  const int N = p.dstate;
+  const int L = p.seqlen;
+  const int LO = p.out_len;
+  const int SB = S * TW;
+  const bool vx = p.vec_x != 0;
+  const bool vbc = p.vec_bc != 0;
+
+  int dch[NC];
+  bool act[NC];
+  float A2[NC][kMaxN], carry[NC][kMaxN], Dv[NC], bias[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int dr = blockIdx.x * NC + c;
+    act[c] = dr < p.dim;
+    dch[c] = act[c] ? dr : p.dim - 1;
+    Dv[c] = p.D ? p.D[dch[c]] : 0.0f;
+    bias[c] = p.dbias ? p.dbias[dch[c]] : 0.0f;
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) {
+      A2[c][n] = (n < N) ? p.A[dch[c] * N + n] * kLog2e : 0.0f;
+      carry[c][n] = (n < N && p.h0)
+          ? load_dyn(p.h0, b * p.h0_sb + dch[c] * p.h0_sd + n, p.h0_dtype) : 0.0f;
+    }
+  }
+  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
+
+  for (int t_sb = 0; t_sb < LO; t_sb += SB) {
+    const int t0 = t_sb + wave * TW + lane * K;
+    const bool more = t_sb + SB < L;  // another super-block follows: keep the block carry
+    float dl[NC][K], du[NC][K], y[NC][K], sd[NC], psd_ex[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + dch[c] * p.u_sd;
+      const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + dch[c] * p.dl_sd;
+      float uv[K], dv[K];
+      load_k<T, K>(urow, t0, L, vx, uv);
+      load_k<T, K>(drow, t0, L, vx, dv);
+      sd[c] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dd = dv[k] + bias[c];
+        if (p.softplus) dd = softplus(dd);
+        dd = (t0 + k < L) ? dd : 0.0f;
+        dl[c][k] = dd;
+        du[c][k] = dd * uv[k];
+        y[c][k] = Dv[c] * uv[k];
+        sd[c] += dd;
+      }
+      const float incl = wave_incl_sum(sd[c]);
+      psd_ex[c] = incl - sd[c];
+      if (lane == 63) s_sdw[c][wave] = incl;
+    }
+
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) {
+      if (n < N) {
+        float bv[K];
+        load_k<T, K>(Bb + n * p.b_sn, t0, L, vbc, bv);
+        float a[NC][K], bb[NC][K], fold[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          fold[c] = 0.0f;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            a[c][k] = __builtin_amdgcn_exp2f(dl[c][k] * A2[c][n]);
+            bb[c][k] = du[c][k] * bv[k];
+            fold[c] = fmaf(a[c][k], fold[c], bb[c][k]);
+          }
+          const float aa = __builtin_amdgcn_exp2f(sd[c] * A2[c][n]);
+          pair_scan<64>(aa, fold[c]);
+          if (lane == 63) s_bt[n & 1][c][wave] = fold[c];
+        }
+        __syncthreads();
+        float cv[K];
+        load_k<T, K>(Cb + n * p.c_sn, t0, L, vbc, cv);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          // carry entering this wave: compose the totals of the earlier waves
+          float hc = carry[c][n];
+          float nxt = 0.0f;
+          const int upto = more ? S : wave;
+          for (int w = 0; w < upto; ++w) {
+            const float e = __builtin_amdgcn_exp2f(A2[c][n] * s_sdw[c][w]);
+            const float v = fmaf(e, hc, s_bt[n & 1][c][w]);
+            hc = (w < wave) ? v : hc;
+            nxt = v;
+          }
+          if (more) carry[c][n] = nxt;
+          const float bex = dpp_f<0x138>(0.0f, fold[c]);  // wave_shr:1 -> exclusive b
+          float h = fmaf(__builtin_amdgcn_exp2f(A2[c][n] * psd_ex[c]), hc, bex);
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            h = fmaf(a[c][k], h, bb[c][k]);
+            y[c][k] = fmaf(h, cv[k], y[c][k]);
+          }
+          // the final state is the last wave's last lane after the sweep
+          if (!more && p.hl && act[c] && wave == S - 1 && lane == 63)
+            store_dyn(p.hl, b * p.hl_sb + dch[c] * p.hl_sd + n, p.hl_dtype, h);
+        }
+      }
+    }
+
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (p.z) {
+        const T* zrow = static_cast<const T*>(p.z) + b * p.z_sb + dch[c] * p.z_sd;
+        float zv[K];
+        load_k<T, K>(zrow, t0, L, vx, zv);
+#pragma unroll
+        for (int k = 0; k < K; ++k) y[c][k] *= silu(zv[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) y[c][k] = (t0 + k < L) ? y[c][k] : 0.0f;
+      T* orow = static_cast<T*>(p.out) + b * p.o_sb + dch[c] * p.o_sd;
+      if (act[c] && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y[c]);
+    }
+    __syncthreads();  // s_sdw is rewritten by the next super-block
+  }
+  if (L == 0 && p.hl && wave == 0 && lane == 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (act[c])
+        for (int n = 0; n < N; ++n)
+          store_dyn(p.hl, b * p.hl_sb + dch[c] * p.hl_sd + n, p.hl_dtype, carry[c][n]);
+  }
+}
+
+template <typename T, int K, int NC>
+static void launch_tw(const ScanParams& p, hipStream_t s) {
+  constexpr int TW = 64 * K;
+  int S = (p.out_len + TW - 1) / TW;
+  S = S < 1 ? 1 : (S > 8 ? 8 : S);
+  dim3 grid((p.dim + NC - 1) / NC, p.batch);
+  hipLaunchKernelGGL((scan_tw_kernel<T, K, NC>), grid, dim3(64 * S), 0, s, p, S);
+}
+
 // --------------------------------------------------------------------- one-token step
 struct StepParams {
   void* state; const void* x; const void* dt; const float* A; const void* B; const void* C;
@@ -299,13 +680,26 @@ static void launch_scan(const ScanParams& p, hipStream_t s) {
   hipLaunchKernelGGL((scan_fwd_kernel<T, K, LPC, NW>), grid, dim3(64 * NW), 0, s, p);
 }
 
+// VM_SCAN_VARIANT selects an alternative kernel for A/B timing and cross-checks
+// (read per call so tests can sweep it); 0 = production choice.
+static int scan_variant() {
+  const char* e = getenv("VM_SCAN_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
 template <typename T>
 static void dispatch_scan(const ScanParams& p, hipStream_t s) {
-  // Channel-parallel work is B*D channels; when it is small, give each channel a full
-  // 64-lane row so more waves exist to hide latency.
-  const long long chans = 1LL * p.batch * p.dim;
-  if (chans >= 4096) launch_scan<T, 16, 16, 4>(p, s);
-  else launch_scan<T, 8, 64, 4>(p, s);
+  switch (scan_variant()) {
+    case 1: launch_scan<T, 8, 64, 4>(p, s); break;     // v1: channel-serial blocks
+    case 2: launch_scan<T, 16, 16, 4>(p, s); break;
+    case 3: launch_tw<T, 16, 1>(p, s); break;          // time-split, 1 channel x K=16
+    case 4: launch_tw<T, 8, 1>(p, s); break;
+    case 5: launch_tw<T, 8, 2>(p, s); break;           // time-split, 2 channels x K=8
+    case 6: launch_v3<T, 8, 1, 8>(p, s); break;
+    case 7: launch_v3<T, 8, 2, 4>(p, s); break;
+    case 8: launch_v3<T, 16, 2, 4>(p, s); break;
+    default: launch_v3<T, 8, 2, 8>(p, s); break;       // v3: 8 channels x K=8, 2 states
+  }
 }
 
 }  // namespace vm
