@@ -277,8 +277,9 @@ __device__ __forceinline__ float dppz(float v) {  // invalid source lanes read 0
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, true));
 }
 
-template <typename T, int K, int G, int NW>
+template <typename T, int K, int G, int NW, int ABL = 0>
 __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
+  // ABL (timing-only ablations): 1 no DPP scan, 2 no exp, 4 no B/C staging, 8 no x loads
   constexpr int TB = 64 * K;
   constexpr int KQ = K / 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
   for (int t_blk = 0; t_blk < LO; t_blk += TB) {
     // ---- stage B/C (fp32, lane-interleaved) ----
     __syncthreads();
-    const int chunks = 2 * N * (TB / 8);
+    const int chunks = (ABL & 4) ? 0 : 2 * N * (TB / 8);
     for (int idx = tid; idx < chunks; idx += 64 * NW) {
       const int row = idx / (TB / 8);
       const int c8 = idx - row * (TB / 8);
@@ -341,15 +342,20 @@ __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
             make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
       }
     }
-    __syncthreads();
+    if (!(ABL & 4)) __syncthreads();
 
     // ---- per-lane prologue ----
     const int t0 = t_blk + lane * K;
     float dl[K], du[K], y[K];
     {
       float uv[K], dv[K];
-      load_k<T, K>(urow, t0, L, vx, uv);
-      load_k<T, K>(drow, t0, L, vx, dv);
+      if (ABL & 8) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) { uv[k] = 0.001f * (t0 + k); dv[k] = -4.0f + 0.0001f * k; }
+      } else {
+        load_k<T, K>(urow, t0, L, vx, uv);
+        load_k<T, K>(drow, t0, L, vx, dv);
+      }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         float dd = dv[k] + bias;
@@ -393,7 +399,7 @@ __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int k = kq * 4 + i;
-              a[g][k] = __builtin_amdgcn_exp2f(dl[k] * A2[n]);
+              a[g][k] = (ABL & 2) ? fmaf(dl[k], A2[n], 1.0f) : __builtin_amdgcn_exp2f(dl[k] * A2[n]);
               bb[g][k] = du[k] * bv[i];
               fold[g] = fmaf(a[g][k], fold[g], bb[g][k]);
             }
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
         }
         // 64-lane inclusive scan of b; a-products from the delta range sums
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < (ABL & 1 ? 0 : G); ++g) {
           const int n = n0 + g;
           fold[g] = fmaf(__builtin_amdgcn_exp2f(s1 * A2[n]), dppz<0x111>(fold[g]), fold[g]);
           fold[g] = fmaf(__builtin_amdgcn_exp2f(s2 * A2[n]), dppz<0x112>(fold[g]), fold[g]);
@@ -457,11 +463,471 @@ __global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
   }
 }
 
-template <typename T, int K, int G, int NW>
+template <typename T, int K, int G, int NW, int ABL = 0>
 static void launch_v3(const ScanParams& p, hipStream_t s) {
   const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
   dim3 grid((p.dim + NW - 1) / NW, p.batch);
-  hipLaunchKernelGGL((scan_v3_kernel<T, K, G, NW>), grid, dim3(64 * NW), lds, s, p);
+  hipLaunchKernelGGL((scan_v3_kernel<T, K, G, NW, ABL>), grid, dim3(64 * NW), lds, s, p);
+}
+
+// --------------------------------------------------------------------- scan v4
+// Production throughput path.  gfx950 issues a wave64 fp32 VALU op in ~4 cycles, so the
+// fp32 peak needs packed math: the states are processed in pairs held in float2
+// (v_pk_mul_f32 / v_pk_fma_f32), two independent pair-chains per pass (P).  The rest is
+// v3's structure: one wave per channel row, lanes over time (K steps per lane), blocks
+// of 64*K steps, B/C staged per block in LDS as fp32 laid out [pair][K/2][lane][4]
+// (4 = two steps x two states: one conflict-free ds_read_b128 per two steps), 64-lane
+// DPP scan of b with the range products E_o built recursively from the neighbours'
+// products (E_2o = E_o * shift_o(E_o)) plus two exps for the row/half spans.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 exp2v(f2 x) {
+  return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+}
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ f2 dppz2(f2 v) { return f2{dppz<CTRL, ROWMASK>(v.x), dppz<CTRL, ROWMASK>(v.y)}; }
+
+// softplus / silu from the hardware exp2 / log2 / rcp (a few ulp; fp32 reference 1e-6)
+__device__ __forceinline__ float softplus_fast(float x) {
+  if (x > 20.0f) return x;
+  const float u = __builtin_amdgcn_exp2f(x * kLog2e);
+  const float w = 1.0f + u;
+  // log1p(u) = log(w) * u / (w - 1), exact-ish even when w rounds near 1
+  return (w == 1.0f) ? u : __builtin_amdgcn_logf(w) * 0.6931471805599453f * u *
+                                __builtin_amdgcn_rcpf(w - 1.0f);
+}
+__device__ __forceinline__ float silu_fast(float z) {
+  return z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * kLog2e));
+}
+
+template <typename T, int K, int P, int NW>
+__global__ __launch_bounds__(64 * NW) void scan_v4_kernel(const ScanParams p) {
+  constexpr int TB = 64 * K;
+  constexpr int K2 = K / 2;
+  constexpr int NP = kMaxN / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sB = smem;                 // [NP][K2][64][4]
+  float* sC = smem + kMaxN * TB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.y;
+  const int d_raw = blockIdx.x * NW + wave;
+  const bool active = d_raw < p.dim;
+  const int d = active ? d_raw : p.dim - 1;
+  const int N = p.dstate;
+  const int NPr = (N + 1) >> 1;
+  const int L = p.seqlen;
+  const int LO = p.out_len;
+  const bool vx = p.vec_x != 0;
+
+  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
+  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
+  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
+  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
+  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
+
+  f2 A2[NP], carry[NP];  // wave-uniform
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int n0 = 2 * q, n1 = 2 * q + 1;
+    A2[q] = f2{n0 < N ? p.A[d * N + n0] * kLog2e : 0.0f, n1 < N ? p.A[d * N + n1] * kLog2e : 0.0f};
+    const long long hb = b * p.h0_sb + d * p.h0_sd;
+    carry[q] = f2{(n0 < N && p.h0) ? load_dyn(p.h0, hb + n0, p.h0_dtype) : 0.0f,
+                  (n1 < N && p.h0) ? load_dyn(p.h0, hb + n1, p.h0_dtype) : 0.0f};
+  }
+  const float Dv = p.D ? p.D[d] : 0.0f;
+  const float bias = p.dbias ? p.dbias[d] : 0.0f;
+
+  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
+    // ---- stage B/C: thread = (B|C, state pair, 8-step chunk) ----
+    __syncthreads();
+    const int chunks = 2 * NPr * (TB / 8);
+    for (int idx = tid; idx < chunks; idx += 64 * NW) {
+      const int row = idx / (TB / 8);
+      const int c8 = idx - row * (TB / 8);
+      const bool isC = row >= NPr;
+      const int q = isC ? row - NPr : row;
+      const T* src = isC ? Cb : Bb;
+      const long long sn = isC ? p.c_sn : p.b_sn;
+      const int t = t_blk + c8 * 8;
+      float w0[8], w1[8];
+      const bool has1 = 2 * q + 1 < N;
+      if (p.vec_bc && t + 8 <= L) {
+        load8(src + (2 * q) * sn + t, w0);
+        if (has1) load8(src + (2 * q + 1) * sn + t, w1);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          w0[j] = (t + j < L) ? to_f32(src[(2 * q) * sn + t + j]) : 0.0f;
+          w1[j] = (has1 && t + j < L) ? to_f32(src[(2 * q + 1) * sn + t + j]) : 0.0f;
+        }
+      }
+      if (!has1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w1[j] = 0.0f;
+      }
+      const int r = c8 * 8;           // block-relative first step of the chunk
+      const int ln = r / K, kb = r - ln * K;
+      float* base = (isC ? sC : sB) + q * K2 * 256;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const int k2 = (kb + j) >> 1;
+        *reinterpret_cast<float4*>(base + (k2 * 64 + ln) * 4) =
+            make_float4(w0[j], w1[j], w0[j + 1], w1[j + 1]);
+      }
+    }
+    __syncthreads();
+
+    // ---- per-lane prologue ----
+    const int t0 = t_blk + lane * K;
+    float dl[K], du[K];
+    f2 y2[K];
+    {
+      float uv[K], dv[K];
+      load_k<T, K>(urow, t0, L, vx, uv);
+      load_k<T, K>(drow, t0, L, vx, dv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dd = dv[k] + bias;
+        if (p.softplus) dd = softplus_fast(dd);
+        dd = (t0 + k < L) ? dd : 0.0f;
+        dl[k] = dd;
+        du[k] = dd * uv[k];
+        y2[k] = f2{Dv * uv[k], 0.0f};
+      }
+    }
+    float sd = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) sd += dl[k];
+    float srow = sd;
+    srow += dppz<0x111>(srow);
+    srow += dppz<0x112>(srow);
+    srow += dppz<0x114>(srow);
+    srow += dppz<0x118>(srow);                         // row-inclusive delta sum
+    const float shalf = srow + dppz<0x142, 0xa>(srow);  // half-inclusive delta sum
+
+    // ---- state pairs, P per pass ----
+#pragma unroll
+    for (int q0 = 0; q0 < NP; q0 += P) {
+      if (q0 < NPr) {
+        f2 a[P][K], bb[P][K], fold[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int q = q0 + j;
+          const float* bs = sB + q * K2 * 256 + lane * 4;
+          fold[j] = f2{0.0f, 0.0f};
+#pragma unroll
+          for (int k2 = 0; k2 < K2; ++k2) {
+            const float4 v = *reinterpret_cast<const float4*>(bs + k2 * 256);
+            const f2 bv[2] = {f2{v.x, v.y}, f2{v.z, v.w}};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int k = 2 * k2 + i;
+              a[j][k] = exp2v(A2[q] * dl[k]);
+              bb[j][k] = bv[i] * du[k];
+              fold[j] = fma2(a[j][k], fold[j], bb[j][k]);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int q = q0 + j;
+          const f2 e1 = exp2v(A2[q] * sd);  // product over the lane's own steps
+          if (lane == 0) fold[j] = fma2(e1, carry[q], fold[j]);
+          const f2 e2 = e1 * dppz2<0x111>(e1);
+          const f2 e4 = e2 * dppz2<0x112>(e2);
+          const f2 e8 = e4 * dppz2<0x114>(e4);
+          fold[j] = fma2(e1, dppz2<0x111>(fold[j]), fold[j]);
+          fold[j] = fma2(e2, dppz2<0x112>(fold[j]), fold[j]);
+          fold[j] = fma2(e4, dppz2<0x114>(fold[j]), fold[j]);
+          fold[j] = fma2(e8, dppz2<0x118>(fold[j]), fold[j]);
+          fold[j] = fma2(exp2v(A2[q] * srow), dppz2<0x142, 0xa>(fold[j]), fold[j]);
+          fold[j] = fma2(exp2v(A2[q] * shalf), dppz2<0x143, 0xc>(fold[j]), fold[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int q = q0 + j;
+          f2 h = dppz2<0x138>(fold[j]);  // exclusive prefix
+          if (lane == 0) h = carry[q];
+          carry[q] = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[j].x), 63)),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[j].y), 63))};
+          const float* cs = sC + q * K2 * 256 + lane * 4;
+#pragma unroll
+          for (int k2 = 0; k2 < K2; ++k2) {
+            const float4 v = *reinterpret_cast<const float4*>(cs + k2 * 256);
+            const f2 cv[2] = {f2{v.x, v.y}, f2{v.z, v.w}};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int k = 2 * k2 + i;
+              h = fma2(a[j][k], h, bb[j][k]);
+              y2[k] = fma2(h, cv[i], y2[k]);
+            }
+          }
+        }
+      }
+    }
+
+    float y[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = y2[k].x + y2[k].y;
+    if (zrow) {
+      float zv[K];
+      load_k<T, K>(zrow, t0, L, vx, zv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) y[k] *= silu_fast(zv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
+    if (active && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y);
+  }
+
+  if (p.hl && active && lane == 0) {
+    const long long hb = b * p.hl_sb + d * p.hl_sd;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (2 * q < N) store_dyn(p.hl, hb + 2 * q, p.hl_dtype, carry[q].x);
+      if (2 * q + 1 < N) store_dyn(p.hl, hb + 2 * q + 1, p.hl_dtype, carry[q].y);
+    }
+  }
+}
+
+template <typename T, int K, int P, int NW>
+static void launch_v4(const ScanParams& p, hipStream_t s) {
+  const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
+  dim3 grid((p.dim + NW - 1) / NW, p.batch);
+  hipLaunchKernelGGL((scan_v4_kernel<T, K, P, NW>), grid, dim3(64 * NW), lds, s, p);
+}
+
+// --------------------------------------------------------------------- scan v5
+// Scalar-math successor of v4 (measured on gfx950: v_pk_fma_f32 costs ~2x v_fma_f32 per
+// wave instruction, so packing buys nothing; v_exp_f32 ~3x).  One state per pass, K
+// steps per lane with any even K (K=10 covers L=3137 in 5 blocks of 640 at 98% lane
+// use), B/C staged as fp32 in a [state][K/2][lane][2] layout (ds_read_b64, 512
+// contiguous bytes per wave), u/delta/z read with 4-byte (bf16 pair) or 16-byte loads.
+template <typename T, int K>
+__device__ __forceinline__ void load_even(const T* row, int t0, int L, bool vec, float (&v)[K]) {
+  if (vec && t0 + K <= L) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(row + t0 + j);
+        v[j] = __uint_as_float(w << 16);
+        v[j + 1] = __uint_as_float(w & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        const float2 w = *reinterpret_cast<const float2*>(row + t0 + j);
+        v[j] = w.x;
+        v[j + 1] = w.y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (t0 + k < L) ? to_f32(row[t0 + k]) : 0.0f;
+  }
+}
+
+template <typename T, int K>
+__device__ __forceinline__ void store_even(T* row, int t0, int LO, bool vec, const float (&v)[K]) {
+  if (vec && t0 + K <= LO) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int j = 0; j < K; j += 2)
+        *reinterpret_cast<uint32_t*>(row + t0 + j) =
+            static_cast<uint32_t>(from_f32<bf16_t>(v[j])) |
+            (static_cast<uint32_t>(from_f32<bf16_t>(v[j + 1])) << 16);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; j += 2)
+        *reinterpret_cast<float2*>(row + t0 + j) = make_float2(v[j], v[j + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (t0 + k < LO) row[t0 + k] = from_f32<T>(v[k]);
+  }
+}
+
+template <typename T, int K, int NW>
+__global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
+  static_assert(K % 2 == 0, "K must be even");
+  constexpr int TB = 64 * K;
+  constexpr int K2 = K / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sB = smem;                 // [N][K2][64][2]
+  float* sC = smem + kMaxN * TB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.y;
+  const int d_raw = blockIdx.x * NW + wave;
+  const bool active = d_raw < p.dim;
+  const int d = active ? d_raw : p.dim - 1;
+  const int N = p.dstate;
+  const int L = p.seqlen;
+  const int LO = p.out_len;
+  const bool vx = p.vec_x != 0;
+
+  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
+  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
+  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
+  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
+  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
+
+  float A2[kMaxN], carry[kMaxN];  // wave-uniform (SGPRs)
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) {
+    A2[n] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
+    carry[n] = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
+  }
+  const float Dv = p.D ? p.D[d] : 0.0f;
+  const float bias = p.dbias ? p.dbias[d] : 0.0f;
+
+  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
+    // ---- stage B/C: thread = (B|C, state, 8-step chunk) -> four float2 writes ----
+    __syncthreads();
+    const int chunks = 2 * N * (TB / 8);
+    for (int idx = tid; idx < chunks; idx += 64 * NW) {
+      const int row = idx / (TB / 8);
+      const int c8 = idx - row * (TB / 8);
+      const bool isC = row >= N;
+      const int n = isC ? row - N : row;
+      const T* src = (isC ? Cb + n * p.c_sn : Bb + n * p.b_sn);
+      const int t = t_blk + c8 * 8;
+      float w[8];
+      if (p.vec_bc && t + 8 <= L) {
+        load8(src + t, w);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
+      }
+      float* base = (isC ? sC : sB) + n * TB;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const int r = c8 * 8 + j;       // block-relative step (even)
+        const int ln = r / K, k = r - ln * K;
+        *reinterpret_cast<float2*>(base + ((k >> 1) * 64 + ln) * 2) = make_float2(w[j], w[j + 1]);
+      }
+    }
+    __syncthreads();
+
+    // ---- per-lane prologue ----
+    const int t0 = t_blk + lane * K;
+    float dl[K], du[K], y[K];
+    {
+      float uv[K], dv[K];
+      load_even<T, K>(urow, t0, L, vx, uv);
+      load_even<T, K>(drow, t0, L, vx, dv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float dd = dv[k] + bias;
+        if (p.softplus) dd = softplus_fast(dd);
+        dd = (t0 + k < L) ? dd : 0.0f;
+        dl[k] = dd;
+        du[k] = dd * uv[k];
+        y[k] = Dv * uv[k];
+      }
+    }
+    float sd = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) sd += dl[k];
+    float srow = sd;
+    srow += dppz<0x111>(srow);
+    srow += dppz<0x112>(srow);
+    srow += dppz<0x114>(srow);
+    srow += dppz<0x118>(srow);
+    const float shalf = srow + dppz<0x142, 0xa>(srow);
+
+    // ---- states ----
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) {
+      if (n < N) {
+        const float* bs = sB + n * TB + lane * 2;
+        float a[K], bb[K];
+        float fold = 0.0f;
+#pragma unroll
+        for (int k2 = 0; k2 < K2; ++k2) {
+          const float2 v = *reinterpret_cast<const float2*>(bs + k2 * 128);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int k = 2 * k2 + i;
+            a[k] = __builtin_amdgcn_exp2f(dl[k] * A2[n]);
+            bb[k] = du[k] * (i ? v.y : v.x);
+            fold = fmaf(a[k], fold, bb[k]);
+          }
+        }
+        const float e1 = __builtin_amdgcn_exp2f(sd * A2[n]);
+        if (lane == 0) fold = fmaf(e1, carry[n], fold);
+        const float e2 = e1 * dppz<0x111>(e1);
+        const float e4 = e2 * dppz<0x112>(e2);
+        const float e8 = e4 * dppz<0x114>(e4);
+        fold = fmaf(e1, dppz<0x111>(fold), fold);
+        fold = fmaf(e2, dppz<0x112>(fold), fold);
+        fold = fmaf(e4, dppz<0x114>(fold), fold);
+        fold = fmaf(e8, dppz<0x118>(fold), fold);
+        fold = fmaf(__builtin_amdgcn_exp2f(srow * A2[n]), dppz<0x142, 0xa>(fold), fold);
+        fold = fmaf(__builtin_amdgcn_exp2f(shalf * A2[n]), dppz<0x143, 0xc>(fold), fold);
+        float h = dppz<0x138>(fold);
+        if (lane == 0) h = carry[n];
+        carry[n] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold), 63));
+        const float* cs = sC + n * TB + lane * 2;
+#pragma unroll
+        for (int k2 = 0; k2 < K2; ++k2) {
+          const float2 v = *reinterpret_cast<const float2*>(cs + k2 * 128);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int k = 2 * k2 + i;
+            h = fmaf(a[k], h, bb[k]);
+            y[k] = fmaf(h, i ? v.y : v.x, y[k]);
+          }
+        }
+      }
+    }
+
+    if (zrow) {
+      float zv[K];
+      load_even<T, K>(zrow, t0, L, vx, zv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) y[k] *= silu_fast(zv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
+    if (active && t0 < LO) store_even<T, K>(orow, t0, LO, vx, y);
+  }
+
+  if (p.hl && active && lane == 0) {
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n)
+      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[n]);
+  }
+}
+
+template <typename T, int K, int NW>
+static void launch_v5(const ScanParams& p, hipStream_t s) {
+  const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
+  dim3 grid((p.dim + NW - 1) / NW, p.batch);
+  hipLaunchKernelGGL((scan_v5_kernel<T, K, NW>), grid, dim3(64 * NW), lds, s, p);
+}
+
+// Pick the steps-per-lane K that covers out_len with the least padded work; per block
+// the scan costs about as much as 8/K of a step, so ties go to the larger K.  The LDS
+// staging is 2*16*64*K fp32 (80 KB at K=10): with 8-wave workgroups two fit per CU
+// (4 waves/SIMD), which caps K at 10.
+template <typename T>
+static void launch_v5_auto(const ScanParams& p, hipStream_t s) {
+  auto cost = [&](int k) {
+    const double tb = 64.0 * k;
+    return ((p.out_len + tb - 1) / tb) * tb * (1.0 + 4.0 / k);
+  };
+  if (cost(10) <= cost(8)) launch_v5<T, 10, 8>(p, s);
+  else launch_v5<T, 8, 8>(p, s);
 }
 
 // --------------------------------------------------------------------- time-split scan
@@ -698,7 +1164,22 @@ static void dispatch_scan(const ScanParams& p, hipStream_t s) {
     case 6: launch_v3<T, 8, 1, 8>(p, s); break;
     case 7: launch_v3<T, 8, 2, 4>(p, s); break;
     case 8: launch_v3<T, 16, 2, 4>(p, s); break;
-    default: launch_v3<T, 8, 2, 8>(p, s); break;       // v3: 8 channels x K=8, 2 states
+    case 21: launch_v3<T, 8, 1, 8, 1>(p, s); break;   // ablations (timing only, wrong output)
+    case 22: launch_v3<T, 8, 1, 8, 2>(p, s); break;
+    case 24: launch_v3<T, 8, 1, 8, 4>(p, s); break;
+    case 28: launch_v3<T, 8, 1, 8, 8>(p, s); break;
+    case 29: launch_v3<T, 8, 1, 8, 15>(p, s); break;
+    case 23: launch_v3<T, 8, 1, 8, 3>(p, s); break;
+    case 9: launch_v3<T, 8, 2, 8>(p, s); break;
+    case 10: launch_v4<T, 8, 2, 8>(p, s); break;
+    case 11: launch_v4<T, 8, 1, 4>(p, s); break;
+    case 12: launch_v4<T, 16, 1, 4>(p, s); break;
+    case 13: launch_v4<T, 8, 1, 8>(p, s); break;      // v4: packed state pairs
+    case 14: launch_v5<T, 10, 8>(p, s); break;
+    case 15: launch_v5<T, 8, 4>(p, s); break;
+    case 16: launch_v5<T, 16, 4>(p, s); break;
+    case 17: launch_v5<T, 8, 8>(p, s); break;
+    default: launch_v5_auto<T>(p, s); break;          // v5: scalar, K chosen per L
   }
 }
 
