@@ -64,6 +64,21 @@ def f32c(t: Optional[Tensor]) -> Optional[Tensor]:
     return t.contiguous()
 
 
+def f32_cached(owner, t: Optional[Tensor], slot: str) -> Optional[Tensor]:
+    """fp32 contiguous copy of a small parameter cached on ``owner`` (a module) and
+    refreshed when the parameter changes (data pointer, version, dtype or device)."""
+    if t is None:
+        return None
+    key = (t.data_ptr(), t._version, t.dtype, t.device)
+    cache = owner.__dict__.setdefault("_vm_f32_cache", {})
+    hit = cache.get(slot)
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            hit = (key, f32c(t))
+        cache[slot] = hit
+    return hit[1]
+
+
 def _lastdim_contig(t: Optional[Tensor]) -> Optional[Tensor]:
     if t is None:
         return None
@@ -247,7 +262,7 @@ def causal_conv1d_update(x: Tensor, conv_state: Tensor, weight: Tensor,
 
 # --------------------------------------------------------------------------- norms
 def _norm(x, weight, bias, residual, prenorm, residual_in_fp32, eps, is_rms, out=None,
-          residual_out=None):
+          residual_out=None, owner=None):
     require_gpu(x, weight, bias, residual, what="rms_norm_fn/layer_norm_fn")
     shape = x.shape
     cols = shape[-1]
@@ -269,7 +284,11 @@ def _norm(x, weight, bias, residual, prenorm, residual_in_fp32, eps, is_rms, out
             rdt = residual.dtype if residual is not None else (
                 torch.float32 if residual_in_fp32 else x.dtype)
             ro = torch.empty(shape, dtype=rdt, device=x.device)
-    add_norm_raw(x2, r2, f32c(weight), f32c(bias), y, ro, rows, cols, eps, is_rms, _stream(x))
+    if owner is not None:
+        w32, b32 = f32_cached(owner, weight, "w"), f32_cached(owner, bias, "b")
+    else:
+        w32, b32 = f32c(weight), f32c(bias)
+    add_norm_raw(x2, r2, w32, b32, y, ro, rows, cols, eps, is_rms, _stream(x))
     return (y, ro) if prenorm else y
 
 

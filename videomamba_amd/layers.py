@@ -30,8 +30,8 @@ class RMSNorm(nn.Module):
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, prenorm: bool = False,
                 residual_in_fp32: bool = False):
-        return K.rms_norm_fn(x, self.weight, self.bias, residual=residual, prenorm=prenorm,
-                             residual_in_fp32=residual_in_fp32, eps=self.eps)
+        return K._norm(x, self.weight, self.bias, residual, prenorm, residual_in_fp32, self.eps,
+                       True, owner=self)
 
 
 class DropPath(nn.Module):

@@ -88,9 +88,11 @@ class Block(nn.Module):
             h = hidden_states if residual is None else self.drop_path(hidden_states)
             # internal residual buffers are updated in place; a caller's tensor never is
             return K._norm(h, nw, nb, residual, True, self.residual_in_fp32, eps, is_rms,
-                           residual_out=residual if inplace and residual is not None else None)
+                           residual_out=residual if inplace and residual is not None else None,
+                           owner=self.norm)
         residual = hidden_states if residual is None else residual + self.drop_path(hidden_states)
-        hidden = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms)
+        hidden = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms,
+                         owner=self.norm)
         if self.residual_in_fp32:
             residual = residual.to(torch.float32)
         return hidden, residual
@@ -502,10 +504,11 @@ class PretrainVideoMamba(nn.Module):
         is_rms = _norm_kind(self.norm)
         if self.fused_add_norm:
             out = K._norm(self.drop_path(h), nw, nb, residual, False, self.residual_in_fp32,
-                          eps, is_rms)
+                          eps, is_rms, owner=self.norm)
         else:
             residual = h if residual is None else residual + self.drop_path(h)
-            out = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms)
+            out = K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms,
+                          owner=self.norm)
         x_vis = out[:, :L].contiguous()
 
         if new_states is not None and isinstance(new_states, list):
