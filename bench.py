@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Measured gfx950 issue costs (tools/probes/valu_rate.hip, >=2 waves/SIMD): cycles per
 # wave64 instruction per SIMD.  The scan's irreducible work per (element, state) is one
-# v_exp_f32 plus five fp32 mul/fma (delta*A, delta*u*B, fold, h, y*C).
+# v_exp_f32 plus four fp32 mul/fma (delta*A, (delta*u)*B, h update, y += h*C).
 CYC_EXP, CYC_FMA, SIMDS, CLOCK_HZ = 8.2, 2.8, 1024, 2.4e9
 
 CONFIGS = {
@@ -64,7 +64,7 @@ def _sync_barrier(world):
     torch.cuda.synchronize()
 
 
-def _pmc_traffic(shape):
+def _pmc_traffic(shape, kernel):
     """HBM bytes per scan launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
     (profiles/scan_traffic_*.json, gfx950 read correction applied) when they were taken
     at this shape; None otherwise.  PMC collection needs its own profiler run, so it is
@@ -73,37 +73,49 @@ def _pmc_traffic(shape):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "scan_traffic_*.json")))[::-1]:
         with open(path) as f:
             rec = json.load(f)
-        if rec.get("shape") == shape:
+        if rec.get("shape") == shape and rec.get("kernel", "").startswith(kernel):
             return int(rec["hbm_bytes_per_launch"])
     return None
 
 
-def scan_roofline(batch, reps, device):
+def scan_roofline(batch, reps, device, layout="tm"):
     """Time the scan kernel at the bench shape (layer-0 geometry, padded layout) with HIP
-    events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d)."""
+    events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d).
+    layout "tm": the model's token-major buffers (u, dt: (B*Lp, D); z inside xz (B*Lp, 2D);
+    B/C inside x_dbl (B*Lp, R+2N)); "cm": channel-major (D, B*Lp) buffers."""
     from videomamba_amd import kernels as K
     from videomamba_amd.layers import round_up
 
-    D, N, L = 1152, 16, 3137
+    D, N, L, R = 1152, 16, 3137, 36
     Lp = round_up(L)
     n = batch * Lp
     g = torch.Generator(device=device).manual_seed(1)
     bf = torch.bfloat16
-    u = torch.randn(D, n, device=device, generator=g).to(bf)
-    dt = (0.5 * torch.randn(D, n, device=device, generator=g) - 4.0).to(bf)
-    z = torch.randn(D, n, device=device, generator=g).to(bf)
-    bc = torch.randn(2 * N, n, device=device, generator=g).to(bf)
     A = -torch.arange(1, N + 1, device=device, dtype=torch.float32).repeat(D, 1).contiguous()
     Dv = torch.ones(D, device=device)
     bias = torch.full((D,), -4.0, device=device)
     h = torch.zeros(batch, D, N, device=device, dtype=bf)
-    y = torch.empty_like(u)
-    rows = (Lp, n)
+    if layout == "tm":
+        u = torch.randn(n, D, device=device, generator=g).to(bf)
+        dt = (0.5 * torch.randn(n, D, device=device, generator=g) - 4.0).to(bf)
+        xz = torch.randn(n, 2 * D, device=device, generator=g).to(bf)
+        xdbl = torch.randn(n, R + 2 * N, device=device, generator=g).to(bf)
+        z, Bm, Cm = xz[:, D:], xdbl[:, R:], xdbl[:, R + N:]
+        y = torch.empty_like(u)
+        s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * (R + 2 * N), 1, R + 2 * N)
+    else:
+        u = torch.randn(D, n, device=device, generator=g).to(bf)
+        dt = (0.5 * torch.randn(D, n, device=device, generator=g) - 4.0).to(bf)
+        z = torch.randn(D, n, device=device, generator=g).to(bf)
+        bc = torch.randn(2 * N, n, device=device, generator=g).to(bf)
+        Bm, Cm = bc[:N], bc[N:]
+        y = torch.empty_like(u)
+        s_u = s_z = s_bc = (Lp, n, 1)
     stream = torch.cuda.current_stream(device).cuda_stream
 
     def launch():
-        K.scan_raw(u, rows, dt, rows, A, bc[:N], rows, bc[N:], rows, Dv, z, rows, bias, True,
-                   h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, rows, Lp,
+        K.scan_raw(u, s_u, dt, s_u, A, Bm, s_bc, Cm, s_bc, Dv, z, s_z, bias, True,
+                   h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, s_u, Lp,
                    batch, D, L, N, 1, stream)
 
     for _ in range(5):
@@ -119,15 +131,16 @@ def scan_roofline(batch, reps, device):
     e = 2
     algo = batch * D * L * 4 * e + 2 * batch * N * L * e + 4 * D * N + 8 * D + 2 * batch * D * N * e
     achieved = algo / avg_s / 1e9
-    floor_s = batch * D * L * N / 64 * (CYC_EXP + 5 * CYC_FMA) / SIMDS / CLOCK_HZ
+    floor_s = batch * D * L * N / 64 * (CYC_EXP + 4 * CYC_FMA) / SIMDS / CLOCK_HZ
     shape = f"B={batch} D={D} L={L} N={N} bf16, stateful"
-    return {"bound": "hbm", "kernel": "vm::scan_v5_kernel", "achieved": round(achieved, 1),
+    kname = "vm::scan_seq_kernel" if layout == "tm" else "vm::scan_v5_kernel"
+    return {"bound": "hbm", "kernel": kname, "layout": layout, "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": _pmc_traffic(shape), "avg_us": round(avg_s * 1e6, 2),
+            "traffic": _pmc_traffic(shape, kname), "avg_us": round(avg_s * 1e6, 2),
             "bytes_per_launch": algo, "shape": shape,
             "valu_model": {"floor_us": round(floor_s * 1e6, 2),
                            "frac_of_valu_floor": round(floor_s / avg_s, 4),
-                           "note": "1 exp + 5 fma per (element, state) at measured gfx950 "
+                           "note": "1 exp + 4 fma-class per (element, state) at measured gfx950 "
                                    "issue costs, 2.4 GHz; the HBM floor is below it"}}
 
 
@@ -210,7 +223,9 @@ def main():
             torch.cuda.synchronize()
             if i >= 3:
                 lat.append((time.perf_counter() - t1) * 1e3)
-        roof = scan_roofline(B, args.scan_reps, device)
+        from videomamba_amd.mamba_simple import mixer_layout
+        roof = scan_roofline(B, args.scan_reps, device,
+                             mixer_layout(B, cfg["embed_dim"] * 2, device))
 
     if rank == 0:
         line = {

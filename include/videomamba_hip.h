@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 1
+#define VM_ABI_VERSION 2
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -55,25 +55,36 @@ const char* vm_last_error(void);
  *   delta' = softplus?(delta + delta_bias)
  *   h_t    = exp(delta'_t * A) * h_{t-1} + delta'_t * u_t * B_t      (h_{-1} = h0 or 0)
  *   y_t    = <h_t, C_t> + D * u_t;   out = y * silu(z)   (z, D optional)
- * u, delta, z, out: (batch, dim, seqlen) with strides (*_sb, *_sd, 1), dtype `dtype`.
- * B, C: (batch, dstate, seqlen) with strides (*_sb, *_sn, 1), dtype `dtype`.
+ * u, delta, z, out: (batch, dim, seqlen) with element strides (*_sb, *_sd, *_sl).
+ * B, C: (batch, dstate, seqlen) with strides (*_sb, *_sn, *_sl).  All in `dtype`.
+ * Two layouts are accepted:
+ *   token-major   — unit channel stride (u/delta/z/out *_sd == 1; B/C any strides):
+ *                   channel-per-lane sequential kernels (vm_scan_seq.hip);
+ *   channel-major — unit step stride for every operand (*_sl == 1): time-parallel
+ *                   kernels (vm_scan.hip).
  * A: (dim, dstate) fp32 contiguous.  D, delta_bias: (dim) fp32, nullable.
  * h0 (nullable) / h_last (nullable): (batch, dim, dstate) with strides (sb, sd, 1) in
  * their own dtype; h_last may alias h0 (in-place state update).  dstate <= 16.
- * Columns [seqlen, out_len) of every out row are written as 0 (padded token layouts).
+ * Steps [seqlen, out_len) of every out row are written as 0 (padded token layouts).
+ * workspace: scratch for the time-segmented token-major form (small batches), at least
+ * vm_selective_scan_workspace_bytes() bytes; with less (or NULL) a single-pass kernel
+ * runs instead — same result, less parallelism.
  */
-int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd,
-                          const void* delta, long long dl_sb, long long dl_sd,
+int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd, long long u_sl,
+                          const void* delta, long long dl_sb, long long dl_sd, long long dl_sl,
                           const float* A,
-                          const void* B, long long b_sb, long long b_sn,
-                          const void* C, long long c_sb, long long c_sn,
+                          const void* B, long long b_sb, long long b_sn, long long b_sl,
+                          const void* C, long long c_sb, long long c_sn, long long c_sl,
                           const float* D, const void* z, long long z_sb, long long z_sd,
-                          const float* delta_bias, int delta_softplus,
+                          long long z_sl, const float* delta_bias, int delta_softplus,
                           const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
                           void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
-                          void* out, long long o_sb, long long o_sd, int out_len,
-                          int batch, int dim, int seqlen, int dstate, int dtype,
-                          vm_stream_t stream);
+                          void* out, long long o_sb, long long o_sd, long long o_sl,
+                          int out_len, int batch, int dim, int seqlen, int dstate, int dtype,
+                          void* workspace, long long workspace_bytes, vm_stream_t stream);
+
+/* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape. */
+long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int dstate);
 
 /*
  * One-token scan step on `state` (updated in place, own dtype; fp32 math).
@@ -91,17 +102,18 @@ int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long
 /*
  * Depthwise causal conv1d (+bias, optional SiLU) over the virtual sequence
  * [conv_state_in (width values) | x], keeping the last `seqlen` outputs.
- * x: (batch, dim, seqlen) strides (x_sb, x_sd, 1); out: strides (o_sb, o_sd, 1), columns
- * [seqlen, out_len) of every out row are written as 0.  weight: (dim, width) fp32;
- * bias: (dim) fp32 nullable.  conv_state_in / conv_state_out: (batch, dim, width)
- * strides (sb, sd, 1), own dtype, nullable; out state = last `width` raw inputs.
- * conv_state_out must not alias conv_state_in.  width <= 8.
+ * x, out: (batch, dim, seqlen) with element strides (*_sb, *_sd, *_sl): either unit step
+ * stride (channel-major rows) or unit channel stride (token-major rows).  Steps
+ * [seqlen, out_len) of out are written as 0.  weight: (dim, width) fp32; bias: (dim) fp32
+ * nullable.  conv_state_in / conv_state_out: (batch, dim, width) strides (sb, sd, 1), own
+ * dtype, nullable; out state = last `width` raw inputs.  conv_state_out must not alias
+ * conv_state_in.  width <= 8.
  */
-int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd,
+int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long long x_sl,
                          const float* weight, const float* bias,
                          const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
                          void* cs_out, int cs_out_dtype, long long cso_sb, long long cso_sd,
-                         void* out, long long o_sb, long long o_sd, int out_len,
+                         void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
                          int batch, int dim, int seqlen, int width, int silu, int dtype,
                          vm_stream_t stream);
 

@@ -244,7 +244,7 @@ def test_library_loads_and_exports_every_header_symbol():
     lib = _lib.load()
     assert lib.vm_abi_version() == _lib.ABI_VERSION
     header = open(os.path.join(ROOT, "include", "videomamba_hip.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(vm_\w+)\(", header, re.M))
+    declared = set(re.findall(r"^\s*(?:int|long long|const char\*)\s+(vm_\w+)\(", header, re.M))
     assert declared == set(_lib.EXPORTED)
     raw = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
@@ -253,10 +253,19 @@ def test_library_loads_and_exports_every_header_symbol():
 
 def test_abi_rejects_bad_arguments_without_gpu():
     lib = _lib.load()
-    rc = lib.vm_selective_scan_fwd(*([None, 0, 0] * 2), None, *([None, 0, 0] * 2),
-                                   None, None, 0, 0, None, 0, None, 0, 0, 0, None, 0, 0, 0,
-                                   None, 0, 0, 0, 1, 1, 1, 16, 0, None)
+    rc = lib.vm_selective_scan_fwd(*([None, 0, 0, 0] * 2), None, *([None, 0, 0, 0] * 2),
+                                   None, None, 0, 0, 0, None, 0, None, 0, 0, 0, None, 0, 0, 0,
+                                   None, 0, 0, 0, 0, 1, 1, 1, 16, 0, None, 0, None)
     assert rc == -1
     assert b"null required pointer" in lib.vm_last_error()
     rc = lib.vm_add_norm_fwd(None, 0, None, 0, None, None, None, 0, None, 0, 1, 8, 1e-5, 1, None)
     assert rc == -1
+
+
+def test_scan_workspace_query_without_gpu():
+    lib = _lib.load()
+    # small batch, long sequence: the segmented token-major form wants scratch
+    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 16) > 0
+    # a chip-filling batch runs single-pass
+    assert lib.vm_selective_scan_workspace_bytes(64, 1152, 3137, 16) == 0
+    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 17) == 0

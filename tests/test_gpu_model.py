@@ -31,6 +31,14 @@ def _close(a, b, tol):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=tol, atol=tol)
 
 
+@pytest.fixture(params=["cm", "tm"])
+def layout(request, monkeypatch):
+    """Both mixer layouts (channel-major + time-parallel scan, token-major +
+    channel-per-lane scan) must match the same fixtures; VM_MIXER_LAYOUT forces one."""
+    monkeypatch.setenv("VM_MIXER_LAYOUT", request.param)
+    return request.param
+
+
 def _load(module, npz, name, dt):
     sd = {k: v.to(dt) for k, v in orc.params_from_npz(npz, name + "/").items()}
     module.load_state_dict(sd, strict=True)
@@ -41,7 +49,7 @@ MIX, MIX_META = load_golden("mixer_cases.npz")
 
 
 @pytest.mark.parametrize("name", sorted(MIX_META))
-def test_mixer_matches_reference_fixture(name):
+def test_mixer_matches_reference_fixture(name, layout):
     meta = MIX_META[name]
     dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
     tol = 1e-4 if dt == torch.float32 else 3e-2
@@ -80,7 +88,7 @@ def _model_from_meta(meta):
 
 
 @pytest.mark.parametrize("name", sorted(MOD_META))
-def test_encoder_matches_reference_fixture(name):
+def test_encoder_matches_reference_fixture(name, layout):
     meta = MOD_META[name]
     dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
     tol = 1e-4 if dt == torch.float32 else 5e-2
@@ -252,7 +260,7 @@ def test_streaming_rejects_cls_pooling_after_first_chunk(pool_type):
         model(x, keep_temporal=True, ssm_state=state, temporal_pos_offset=1)
 
 
-def test_inference_cache_resizes_and_decode_matches_full():
+def test_inference_cache_resizes_and_decode_matches_full(layout):
     model = Mamba(d_model=8, d_state=4, d_conv=2, expand=2, use_fast_path=False,
                   layer_idx=0).cuda().eval()
     cache = SimpleNamespace(seqlen_offset=0, key_value_memory_dict={})
@@ -295,7 +303,7 @@ def test_refiner_block_runs_and_reverses_time():
     assert out.shape == x.shape and st[0].shape == (2, 32, 4) and st[1].shape == (2, 32, 16)
 
 
-def test_streaming_chunked_full_state_matches_full_sequence_features():
+def test_streaming_chunked_full_state_matches_full_sequence_features(layout):
     model = _small_model(add_pool_norm=False).cuda().eval()
     x = torch.randn(1, 3, 8, 8, 8, device=DEV)
     with torch.no_grad():
@@ -307,19 +315,29 @@ def test_streaming_chunked_full_state_matches_full_sequence_features():
 
 
 # ------------------------------------------------------------------ full-size configs
-def test_ti_8f_fp32_matches_oracle():
+_TI_CACHE = {}
+
+
+def _ti_8f_case():
+    if not _TI_CACHE:
+        torch.manual_seed(0)
+        model = PretrainVideoMamba(depth=24, embed_dim=192, num_frames=8).eval()
+        with torch.no_grad():
+            model.temporal_pos_embedding.normal_(0, 0.02)
+        p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        x = torch.randn(1, 3, 8, 224, 224)
+        cfg = dict(img_size=224, patch_size=16, depth=24, kernel_size=1, num_frames=8,
+                   fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+                   pool_type="cls+avg", norm_epsilon=1e-5, d_state=16, d_conv=4)
+        torch.set_num_threads(16)
+        ref_v, ref_p, _ = orc.encoder_forward(p, cfg, x)
+        _TI_CACHE["v"] = (model, x, ref_v, ref_p)
+    return _TI_CACHE["v"]
+
+
+def test_ti_8f_fp32_matches_oracle(layout):
     """C1/C2 geometry (VideoMamba-Ti, d192, depth 24, 8x224^2) in fp32: HIP vs oracle."""
-    torch.manual_seed(0)
-    model = PretrainVideoMamba(depth=24, embed_dim=192, num_frames=8).eval()
-    with torch.no_grad():
-        model.temporal_pos_embedding.normal_(0, 0.02)
-    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    x = torch.randn(1, 3, 8, 224, 224)
-    cfg = dict(img_size=224, patch_size=16, depth=24, kernel_size=1, num_frames=8,
-               fused_add_norm=True, rms_norm=True, residual_in_fp32=True, pool_type="cls+avg",
-               norm_epsilon=1e-5, d_state=16, d_conv=4)
-    torch.set_num_threads(16)
-    ref_v, ref_p, _ = orc.encoder_forward(p, cfg, x)
+    model, x, ref_v, ref_p = _ti_8f_case()
     model = model.to(DEV)
     with torch.no_grad():
         xv, xp = model(x.to(DEV))
@@ -327,7 +345,7 @@ def test_ti_8f_fp32_matches_oracle():
     _close(xp, ref_p, 1e-3)
 
 
-def test_m_16f_bf16_streaming_chunks_match_full_and_fp32():
+def test_m_16f_bf16_streaming_chunks_match_full_and_fp32(layout):
     """VideoMamba-M (d576, depth 32) 16x224^2 bf16: 2 chunks of 8 frames with carried
     fp32 state == one full pass; and the bf16 pass tracks an fp32 pass of the same weights."""
     torch.manual_seed(0)
@@ -348,3 +366,23 @@ def test_m_16f_bf16_streaming_chunks_match_full_and_fp32():
     rel32 = ((full.float() - full32).norm() / full32.norm()).item()
     assert rel32 < 5e-2, rel32
     assert torch.isfinite(full.float()).all()
+
+
+def test_large_batch_selects_token_major_and_matches_channel_major(monkeypatch):
+    """The automatic layout choice: a chip-filling batch runs token-major; its output
+    equals the channel-major run of the same model (bf16, M geometry, 2 frames)."""
+    from videomamba_amd.mamba_simple import mixer_layout
+    simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    assert mixer_layout(1, 1152, torch.device(DEV)) == "cm"
+    big = -(-int(1.25 * simds) // 18)
+    assert mixer_layout(big, 1152, torch.device(DEV)) == "tm"
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=2, embed_dim=576, num_frames=2, add_pool_norm=False)
+    model = model.to(DEV).to(torch.bfloat16).eval()
+    x = torch.randn(big, 3, 2, 224, 224, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        auto = model(x)
+        monkeypatch.setenv("VM_MIXER_LAYOUT", "cm")
+        cm = model(x)
+    rel = ((auto.float() - cm.float()).norm() / cm.float().norm()).item()
+    assert rel < 1e-2, rel

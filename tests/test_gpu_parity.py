@@ -129,6 +129,74 @@ def test_scan_full_size_chunked_equals_full(dt, scan_variant):
     assert torch.isfinite(y_full.float()).all()
 
 
+def _tm(t):
+    """Same (b, d, l) values stored token-major (unit channel stride)."""
+    return None if t is None else t.transpose(1, 2).contiguous().transpose(1, 2)
+
+
+@pytest.mark.parametrize("segments", ["0", "1", "3", "64"])
+@pytest.mark.parametrize("Bz,D,L,N", [(1, 40, 3137, 16),    # ragged channel group
+                                      (64, 72, 300, 16),    # many rows
+                                      (2, 24, 777, 8), (3, 20, 100, 4), (1, 8, 0, 16),
+                                      (1, 130, 9000, 16), (2, 64, 31, 16)])
+def test_scan_token_major_matches_oracle(Bz, D, L, N, segments, monkeypatch):
+    """Token-major operands take the channel-per-lane kernels: single pass, and the
+    segmented summary/carry/final form (VM_SCAN_SEGMENTS forces the segment count;
+    "0" = the cost model's choice)."""
+    monkeypatch.setenv("VM_SCAN_SEGMENTS", segments)
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(Bz, D, L, N, torch.float32, 11 + L)
+    ref_y, ref_h = _oracle_scan(Bz, D, L, N)
+    cu = lambda t: None if t is None else _tm(t.to(DEV))  # noqa: E731
+    y, h = K.selective_scan_fn(cu(u), cu(delta), A.to(DEV), cu(Bm), cu(Cm), Dv.to(DEV), cu(z),
+                               bias.to(DEV), True, True, init.to(DEV))
+    assert y.stride(1) == 1 or D == 1
+    _close(y, ref_y, 1e-4)
+    _close(h, ref_h, 1e-4)
+
+
+@pytest.mark.parametrize("segments", ["0", "1", "16"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_scan_token_major_full_size_chunked_equals_full(dt, segments, monkeypatch):
+    """North-star size (D_inner=1152, L=3137), token-major: split scan with the carried
+    fp32 state == full scan; and == the channel-major kernels."""
+    monkeypatch.setenv("VM_SCAN_SEGMENTS", segments)
+    u, delta, A, Bm, Cm, Dv, z, bias, _ = _rand_scan(2, 1152, 3137, 16, dt, 5, h0=False)
+    cm = [t.to(DEV) for t in (u, delta, A, Bm, Cm, Dv, z, bias)]
+    tm = [_tm(t) if t.dim() == 3 else t for t in cm]
+    y_full, h_full = K.selective_scan_fn(*tm[:6], z=tm[6], delta_bias=tm[7],
+                                         delta_softplus=True, return_last_state=True)
+    y_cm, h_cm = K.selective_scan_fn(*cm[:6], z=cm[6], delta_bias=cm[7],
+                                     delta_softplus=True, return_last_state=True)
+    tol = 1e-5 if dt == torch.float32 else 1e-3
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(y_full, y_cm) < tol and rel(h_full, h_cm) < 1e-5
+    s = 1000
+    sl = lambda t, a, b: _tm(t[..., a:b])  # noqa: E731
+    y1, h1 = K.selective_scan_fn(sl(cm[0], 0, s), sl(cm[1], 0, s), cm[2], sl(cm[3], 0, s),
+                                 sl(cm[4], 0, s), cm[5], z=sl(cm[6], 0, s), delta_bias=cm[7],
+                                 delta_softplus=True, return_last_state=True)
+    y2, h2 = K.selective_scan_fn(sl(cm[0], s, None), sl(cm[1], s, None), cm[2],
+                                 sl(cm[3], s, None), sl(cm[4], s, None), cm[5],
+                                 z=sl(cm[6], s, None), delta_bias=cm[7], delta_softplus=True,
+                                 return_last_state=True, initial_state=h1)
+    assert rel(torch.cat([y1, y2], dim=-1), y_full) < tol
+    assert rel(h2, h_full) < 1e-5
+    assert torch.isfinite(y_full.float()).all()
+
+
+def test_scan_token_major_inplace_bf16_state():
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(2, 16, 50, 16, torch.float32, 3)
+    st = init.to(DEV).to(torch.bfloat16)
+    ref = init.to(torch.bfloat16).float()
+    ref_y, ref_h = orc.selective_scan(u, delta, A, Bm, Cm, Dv, z, bias, True, ref, True)
+    cu = lambda t: _tm(t.to(DEV))  # noqa: E731
+    y, h = K.selective_scan_fn(cu(u), cu(delta), A.to(DEV), cu(Bm), cu(Cm), Dv.to(DEV), cu(z),
+                               bias.to(DEV), True, True, st, last_state_out=st)
+    assert h is st and h.dtype == torch.bfloat16
+    _close(y, ref_y, 1e-4)
+    _close(h, ref_h, 1e-2)
+
+
 def test_scan_inplace_state_alias_and_bf16_state():
     u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(2, 16, 50, 16, torch.float32, 3)
     cu = lambda t: t.to(DEV)  # noqa: E731

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _P = c_void_p
 _LL = c_longlong
@@ -30,23 +30,25 @@ _SIGNATURES = {
     "vm_abi_version": ([], _I),
     "vm_last_error": ([], ctypes.c_char_p),
     "vm_selective_scan_fwd": (
-        [_P, _LL, _LL,            # u
-         _P, _LL, _LL,            # delta
+        [_P, _LL, _LL, _LL,       # u (sb, sd, sl)
+         _P, _LL, _LL, _LL,       # delta
          _P,                      # A
-         _P, _LL, _LL,            # B
-         _P, _LL, _LL,            # C
-         _P, _P, _LL, _LL,        # D, z
+         _P, _LL, _LL, _LL,       # B (sb, sn, sl)
+         _P, _LL, _LL, _LL,       # C
+         _P, _P, _LL, _LL, _LL,   # D, z
          _P, _I,                  # delta_bias, softplus
          _P, _I, _LL, _LL,        # h0
          _P, _I, _LL, _LL,        # h_last
-         _P, _LL, _LL, _I,        # out, out_len
+         _P, _LL, _LL, _LL, _I,   # out, out_len
          _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
+         _P, _LL,                 # workspace, workspace_bytes
          _P], _I),
+    "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I], _LL),
     "vm_selective_state_update": (
         [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
          _P, _LL, _I, _I, _I, _I, _P], _I),
     "vm_causal_conv1d_fwd": (
-        [_P, _LL, _LL, _P, _P, _P, _I, _LL, _LL, _P, _I, _LL, _LL, _P, _LL, _LL, _I,
+        [_P, _LL, _LL, _LL, _P, _P, _P, _I, _LL, _LL, _P, _I, _LL, _LL, _P, _LL, _LL, _LL, _I,
          _I, _I, _I, _I, _I, _I, _P], _I),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),

@@ -23,22 +23,9 @@
 
 #include <stdlib.h>
 
-#include "vm_common.h"
+#include "vm_scan.h"
 
 namespace vm {
-
-constexpr int kMaxN = 16;
-
-struct ScanParams {
-  const void* u; const void* delta; const float* A; const void* B; const void* C;
-  const float* D; const void* z; const float* dbias;
-  const void* h0; void* hl; void* out;
-  long long u_sb, u_sd, dl_sb, dl_sd, b_sb, b_sn, c_sb, c_sn, z_sb, z_sd, o_sb, o_sd;
-  long long h0_sb, h0_sd, hl_sb, hl_sd;
-  int batch, dim, seqlen, out_len, dstate, softplus, h0_dtype, hl_dtype;
-  int vec_x;   // u/delta/z/out rows allow 8-element vector access
-  int vec_bc;  // B/C rows allow 8-element vector access
-};
 
 template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ float dpp_f(float old, float v) {
@@ -487,18 +474,6 @@ __device__ __forceinline__ f2 exp2v(f2 x) {
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ f2 dppz2(f2 v) { return f2{dppz<CTRL, ROWMASK>(v.x), dppz<CTRL, ROWMASK>(v.y)}; }
-
-// softplus / silu from the hardware exp2 / log2 / rcp.  softplus = ln2*log2(1 + 2^(x/ln2))
-// is within ~1.2e-7 absolute of log1p(exp(x)) (the relative error grows only where the
-// step itself is < 1e-4 and contributes nothing measurable); threshold 20 as torch.
-__device__ __forceinline__ float softplus_fast(float x) {
-  return x > 20.0f ? x
-                   : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x * kLog2e)) *
-                         0.6931471805599453f;
-}
-__device__ __forceinline__ float silu_fast(float z) {
-  return z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * kLog2e));
-}
 
 template <typename T, int K, int P, int NW>
 __global__ __launch_bounds__(64 * NW) void scan_v4_kernel(const ScanParams p) {
@@ -1186,18 +1161,19 @@ static void dispatch_scan(const ScanParams& p, hipStream_t s) {
 
 using namespace vm;
 
-extern "C" int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd,
-                                     const void* delta, long long dl_sb, long long dl_sd,
-                                     const float* A,
-                                     const void* B, long long b_sb, long long b_sn,
-                                     const void* C, long long c_sb, long long c_sn,
-                                     const float* D, const void* z, long long z_sb, long long z_sd,
-                                     const float* delta_bias, int delta_softplus,
-                                     const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
-                                     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
-                                     void* out, long long o_sb, long long o_sd, int out_len,
-                                     int batch, int dim, int seqlen, int dstate, int dtype,
-                                     vm_stream_t stream) {
+extern "C" int vm_selective_scan_fwd(
+    const void* u, long long u_sb, long long u_sd, long long u_sl,
+    const void* delta, long long dl_sb, long long dl_sd, long long dl_sl,
+    const float* A,
+    const void* B, long long b_sb, long long b_sn, long long b_sl,
+    const void* C, long long c_sb, long long c_sn, long long c_sl,
+    const float* D, const void* z, long long z_sb, long long z_sd, long long z_sl,
+    const float* delta_bias, int delta_softplus,
+    const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
+    void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
+    void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
+    int batch, int dim, int seqlen, int dstate, int dtype,
+    void* workspace, long long workspace_bytes, vm_stream_t stream) {
   if (!u || !delta || !A || !B || !C || !out) {
     vmhost::set_error("vm_selective_scan_fwd: null required pointer");
     return VM_E_INVALID;
@@ -1219,9 +1195,23 @@ extern "C" int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_
   p.u_sb = u_sb; p.u_sd = u_sd; p.dl_sb = dl_sb; p.dl_sd = dl_sd;
   p.b_sb = b_sb; p.b_sn = b_sn; p.c_sb = c_sb; p.c_sn = c_sn;
   p.z_sb = z_sb; p.z_sd = z_sd; p.o_sb = o_sb; p.o_sd = o_sd;
+  p.u_sl = u_sl; p.dl_sl = dl_sl; p.b_sl = b_sl; p.c_sl = c_sl; p.z_sl = z_sl; p.o_sl = o_sl;
   p.h0_sb = h0_sb; p.h0_sd = h0_sd; p.hl_sb = hl_sb; p.hl_sd = hl_sd;
   p.batch = batch; p.dim = dim; p.seqlen = seqlen; p.out_len = out_len; p.dstate = dstate;
   p.softplus = delta_softplus; p.h0_dtype = h0_dtype; p.hl_dtype = hl_dtype;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // Token-major operands (channel stride 1): channel-per-lane sequential kernels.
+  if (seq_supported(p, dtype) && scan_variant() == 0) {
+    seq_launch(p, dtype, workspace, workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0,
+               s);
+    return vmhost::launch_status("vm_selective_scan_fwd");
+  }
+  // Channel-major operands (step stride 1): time-parallel kernels.
+  if (u_sl != 1 || dl_sl != 1 || b_sl != 1 || c_sl != 1 || o_sl != 1 || (z && z_sl != 1)) {
+    vmhost::set_error("vm_selective_scan_fwd: operands must have a unit channel stride "
+                      "(u/delta/z/out) or a unit step stride (all operands)");
+    return VM_E_INVALID;
+  }
   const long long m = dtype == VM_DTYPE_BF16 ? 8 : 4;  // elements per 16 bytes
   auto rows_ok = [&](const void* ptr, long long s1, long long s2) {
     return ptr == nullptr || (vmhost::aligned16(ptr) && s1 % m == 0 && s2 % m == 0);
@@ -1229,11 +1219,16 @@ extern "C" int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_
   p.vec_x = rows_ok(u, u_sb, u_sd) && rows_ok(delta, dl_sb, dl_sd) && rows_ok(z, z_sb, z_sd) &&
             rows_ok(out, o_sb, o_sd);
   p.vec_bc = rows_ok(B, b_sb, b_sn) && rows_ok(C, c_sb, c_sn);
-  hipStream_t s = static_cast<hipStream_t>(stream);
   // seqlen == 0 still launches: the block loop is empty and h_last receives h0 (or 0).
   if (dtype == VM_DTYPE_BF16) dispatch_scan<bf16_t>(p, s);
   else dispatch_scan<float>(p, s);
   return vmhost::launch_status("vm_selective_scan_fwd");
+}
+
+extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen,
+                                                       int dstate) {
+  if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN) return 0;
+  return static_cast<long long>(seq_workspace_bytes(batch, dim, seqlen, nullptr));
 }
 
 extern "C" int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long long s_sd,

@@ -1,0 +1,389 @@
+// Token-major selective scan for gfx950: one lane per channel, sequential in time.
+//
+// Same math as vm_scan.hip (_selective_scan_ref, models/videomamba/mamba_simple.py:30-106)
+// on the token-major layout the mixer uses for large batches: u / delta / z / out rows are
+// (batch, step, channel) with channel stride 1, so one wave reads one 128-byte line per
+// operand per step.  A lane owns one channel and keeps its 16 states in registers; per
+// (step, state) the work is the irreducible  a = exp2(delta*A*log2e),  h = a*h + (delta*u)*B,
+// y += h*C  — 4 VALU + 1 transcendental, no cross-lane scan and no re-sweep.  B_t / C_t
+// (shared by every channel of a batch row) are staged per 32-step block in LDS as fp32 and
+// read back as uniform-address (broadcast) ds_read_b128; u / delta / z are prefetched 8
+// steps ahead in registers.
+//
+// Parallelism is batch x channel-groups.  When that is too small to fill the chip (small
+// batch, e.g. the B=1 streaming-chunk latency case) the sequence is cut into S segments:
+//   pass 1 (MODE 1): each segment from a zero state -> end state and sum(delta);
+//   carry          : per (b, d, n) the entry state of every segment, sequentially over S;
+//   pass 2 (MODE 2): each segment from its entry state, emitting y (and h_last).
+
+#include <stdlib.h>
+
+#include "vm_scan.h"
+
+namespace vm {
+
+struct SeqWork {
+  float* hend;  // [B][S][D][kMaxN]  segment end states from a zero entry state (pass 1)
+  float* sdel;  // [B][S][D]         segment delta sums (pass 1)
+  float* hin;   // [B][S][D][kMaxN]  segment entry states (carry)
+  int S, seg_len;
+};
+
+constexpr int kTS = 32;       // steps per LDS block
+constexpr int kPF = 8;        // u / delta / z prefetch distance in steps
+constexpr int kMaxSeg = 64;   // segments per sequence (carry kernel keeps them in registers)
+constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
+
+// Buffer descriptor over a wave-uniform base: per-step byte offsets go in soffset (SGPR),
+// the lane's channel offset in voffset, so no per-lane 64-bit address math runs per step.
+// Host guarantees every in-range byte offset is < kSeqRange; kSeqDead (>= the records
+// count) makes a store a hardware no-op, so stores need no branch.
+constexpr int kSeqRange = 1 << 30;
+constexpr int kSeqDead = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  void* ub = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, 0, kSeqRange, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (sizeof(T) == 2)
+    return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+  else
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+template <typename T>
+__device__ __forceinline__ void bstore(T v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (sizeof(T) == 2)
+    __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+template <typename T>
+__device__ __forceinline__ float raw_f32(uint32_t r) {
+  if constexpr (sizeof(T) == 2) return __uint_as_float(r << 16);
+  else return __uint_as_float(r);
+}
+
+// MODE 0: single pass (entry state h0), MODE 1: summary, MODE 2: final with entry states.
+template <typename T, int NW, int MODE, bool SP, bool HZ>
+__global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, const SeqWork w) {
+  static_assert(NW * 64 >= 4 * kTS, "B/C staging needs 4 threads per block step");
+  __shared__ __attribute__((aligned(16))) float sbc[2][kTS][2 * kMaxN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int seg = blockIdx.y;
+  const int b = blockIdx.z;
+  const int d_raw = (blockIdx.x * NW + wave) * 64 + lane;
+  const bool active = d_raw < p.dim;
+  const int d = active ? d_raw : p.dim - 1;
+  const int N = p.dstate;
+  const int L = p.seqlen;
+  const int t_beg = seg * w.seg_len;
+  const int t_end = min(L, t_beg + w.seg_len);
+  const long long ws_row = (static_cast<long long>(b) * w.S + seg) * p.dim + d;
+
+  float A2[kMaxN], h[kMaxN];
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) {
+    A2[n] = n < N ? p.A[d * N + n] * kLog2e : 0.0f;
+    float h_init = 0.0f;
+    if constexpr (MODE == 0) {
+      if (n < N && p.h0) h_init = load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype);
+    }
+    if constexpr (MODE == 2) h_init = w.hin[ws_row * kMaxN + n];
+    h[n] = h_init;
+  }
+  const float Dv = p.D ? p.D[d] : 0.0f;
+  const float bias = p.dbias ? p.dbias[d] : 0.0f;
+  // Wave-uniform row bases (buffer descriptors) + the lane's channel byte offset.
+  const int d0 = __builtin_amdgcn_readfirstlane((blockIdx.x * NW + wave) * 64 < p.dim
+                                                    ? (blockIdx.x * NW + wave) * 64
+                                                    : p.dim - 1);
+  constexpr int ES = sizeof(T);
+  const int voff = (d - d0) * ES;
+  const int voff_st = active ? voff : kSeqDead;
+  const auto ur = uniform_rsrc(static_cast<const T*>(p.u) + b * p.u_sb + d0);
+  const auto dr_ = uniform_rsrc(static_cast<const T*>(p.delta) + b * p.dl_sb + d0);
+  const auto zr = uniform_rsrc(HZ ? static_cast<const T*>(p.z) + b * p.z_sb + d0
+                                  : static_cast<const T*>(p.u));
+  const auto orr = uniform_rsrc(static_cast<T*>(p.out) + b * p.o_sb + d0);
+  const int us = static_cast<int>(p.u_sl) * ES, ds = static_cast<int>(p.dl_sl) * ES;
+  const int zs = static_cast<int>(p.z_sl) * ES, os = static_cast<int>(p.o_sl) * ES;
+
+  // B/C staging role: thread -> (block step sr, operand B|C, states sn0..sn0+7)
+  const int sr = tid >> 2;
+  const int sq = tid & 3;
+  const bool stager = tid < 4 * kTS;
+  const bool isC = (sq >> 1) != 0;
+  const T* ssrc = static_cast<const T*>(isC ? p.C : p.B) + b * (isC ? p.c_sb : p.b_sb);
+  const long long ssl = isC ? p.c_sl : p.b_sl;
+  const long long ssn = isC ? p.c_sn : p.b_sn;
+  const int sn0 = (sq & 1) * 8;
+  auto stage_load = [&](int tb, float (&v)[8]) {
+    const int t = tb + sr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = sn0 + j;
+      v[j] = (stager && t < L && n < N) ? to_f32(ssrc[t * ssl + n * ssn]) : 0.0f;
+    }
+  };
+  auto stage_store = [&](int buf, const float (&v)[8]) {
+    if (stager) {
+      float* dst = &sbc[buf][sr][(isC ? kMaxN : 0) + sn0];
+      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  };
+
+  const int nblk = t_end > t_beg ? (t_end - t_beg + kTS - 1) / kTS : 0;
+  float stg[8];
+  if (nblk > 0) {
+    stage_load(t_beg, stg);
+    stage_store(0, stg);
+  }
+  __syncthreads();
+
+  // Drain the parameter loads (A, D, bias, entry state) here: left pending they merge into
+  // the step loop's header and force a conservative vmcnt wait on every iteration.
+  __builtin_amdgcn_s_waitcnt(0);
+  uint32_t ru[kPF], rd[kPF], rz[kPF];
+  const int tlast = L > 0 ? L - 1 : 0;
+  if (nblk > 0) {
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) {
+      const int t = min(t_beg + j, tlast);
+      ru[j] = bload<T>(ur, voff, t * us);
+      rd[j] = bload<T>(dr_, voff, t * ds);
+      rz[j] = HZ && MODE != 1 ? bload<T>(zr, voff, t * zs) : 0u;
+    }
+  }
+
+  float sdel = 0.0f;
+  for (int k = 0; k < nblk; ++k) {
+    const int tb = t_beg + k * kTS;
+    const bool more = k + 1 < nblk;
+    if (more) stage_load(tb + kTS, stg);
+    const float* blk = &sbc[k & 1][0][0];
+    for (int g = 0; g < kTS; g += kPF) {
+#pragma unroll
+      for (int j = 0; j < kPF; ++j) {
+        const int t = tb + g + j;
+        const float uu = raw_f32<T>(ru[j]);
+        const float dr = raw_f32<T>(rd[j]);
+        const float zz = raw_f32<T>(rz[j]);
+        {
+          const int tn = min(t + kPF, tlast);
+          ru[j] = bload<T>(ur, voff, tn * us);
+          rd[j] = bload<T>(dr_, voff, tn * ds);
+          if (HZ && MODE != 1) rz[j] = bload<T>(zr, voff, tn * zs);
+        }
+        // keep each step's refill loads at the step head: the scheduler would otherwise
+        // sink them below all eight steps, collapsing the prefetch distance to zero
+        // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
+        __builtin_amdgcn_sched_barrier(0);
+        const bool live = t < t_end;
+        float dl = dr + bias;
+        if (SP) dl = softplus_fast(dl);
+        dl = live ? dl : 0.0f;
+        const float du = dl * uu;
+        const float4* row = reinterpret_cast<const float4*>(blk + (g + j) * 2 * kMaxN);
+        float Bv[kMaxN], Cv[kMaxN];
+#pragma unroll
+        for (int q = 0; q < kMaxN / 4; ++q) {
+          const float4 bq = row[q];
+          Bv[4 * q] = bq.x; Bv[4 * q + 1] = bq.y; Bv[4 * q + 2] = bq.z; Bv[4 * q + 3] = bq.w;
+          if constexpr (MODE != 1) {
+            const float4 cq = row[kMaxN / 4 + q];
+            Cv[4 * q] = cq.x; Cv[4 * q + 1] = cq.y; Cv[4 * q + 2] = cq.z; Cv[4 * q + 3] = cq.w;
+          }
+        }
+        if constexpr (MODE == 1) {
+          sdel += dl;
+#pragma unroll
+          for (int n = 0; n < kMaxN; ++n)
+            h[n] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n]), h[n], du * Bv[n]);
+        } else {
+          float y0 = Dv * uu, y1 = 0.0f;  // two chains: ILP for the 16-term dot product
+#pragma unroll
+          for (int n = 0; n < kMaxN; n += 2) {
+            h[n] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n]), h[n], du * Bv[n]);
+            h[n + 1] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n + 1]), h[n + 1], du * Bv[n + 1]);
+            y0 = fmaf(h[n], Cv[n], y0);
+            y1 = fmaf(h[n + 1], Cv[n + 1], y1);
+          }
+          float y = y0 + y1;
+          if (HZ) y *= silu_fast(zz);
+          // unconditional store (a branch here makes the loop-carried vmcnt accounting
+          // conservative): dead lanes / steps get an out-of-range voffset instead
+          bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+        }
+      }
+    }
+    if (more) stage_store((k + 1) & 1, stg);
+    __syncthreads();
+  }
+
+  if constexpr (MODE == 1) {
+    if (active) {
+#pragma unroll
+      for (int n = 0; n < kMaxN; ++n) w.hend[ws_row * kMaxN + n] = h[n];
+      w.sdel[ws_row] = sdel;
+    }
+  } else {
+    if (t_end >= L && active) {  // the segment that ends the sequence
+      if (p.hl) {
+#pragma unroll
+        for (int n = 0; n < kMaxN; ++n)
+          if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, h[n]);
+      }
+      for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
+    }
+  }
+}
+
+// Entry state of every segment: h_in[0] = h0, h_in[s+1] = exp2(A*log2e*sum_delta[s]) *
+// h_in[s] + h_end[s].  One thread per (b, d, n); the S summaries are loaded up front.
+__global__ __launch_bounds__(256) void scan_seq_carry_kernel(const ScanParams p, const SeqWork w) {
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
+  if (i >= total) return;
+  const int n = static_cast<int>(i % kMaxN);
+  const int d = static_cast<int>((i / kMaxN) % p.dim);
+  const int b = static_cast<int>(i / (static_cast<long long>(kMaxN) * p.dim));
+  const int N = p.dstate;
+  const float A2 = n < N ? p.A[d * N + n] * kLog2e : 0.0f;
+  const long long stride = static_cast<long long>(p.dim);
+  const long long row0 = static_cast<long long>(b) * w.S * stride + d;
+  const float* __restrict__ sdel = w.sdel;
+  const float* __restrict__ hend = w.hend;
+  float* __restrict__ hin = w.hin;
+  float sd[kMaxSeg], he[kMaxSeg];
+#pragma unroll
+  for (int s = 0; s < kMaxSeg; ++s) {
+    if (s + 1 < w.S) {
+      const long long row = row0 + s * stride;
+      sd[s] = sdel[row];
+      he[s] = hend[row * kMaxN + n];
+    }
+  }
+  float h = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
+#pragma unroll
+  for (int s = 0; s < kMaxSeg; ++s) {
+    if (s < w.S) {
+      hin[(row0 + s * stride) * kMaxN + n] = h;
+      if (s + 1 < w.S) h = fmaf(__builtin_amdgcn_exp2f(A2 * sd[s]), h, he[s]);
+    }
+  }
+}
+
+template <typename T, int MODE, bool SP, bool HZ>
+static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hipStream_t s) {
+  const int groups = (p.dim + 63) / 64;
+  dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
+  hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ>), grid, dim3(64 * kSeqNW), 0, s,
+                     p, w);
+}
+
+template <typename T, bool SP, bool HZ>
+static void launch_seq_t(const ScanParams& p, const SeqWork& w, hipStream_t s) {
+  if (w.S <= 1) {
+    launch_seq_mode<T, 0, SP, HZ>(p, w, 1, s);
+    return;
+  }
+  launch_seq_mode<T, 1, SP, HZ>(p, w, w.S - 1, s);  // the last segment's summary is unused
+  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
+  hipLaunchKernelGGL(scan_seq_carry_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                     dim3(256), 0, s, p, w);
+  launch_seq_mode<T, 2, SP, HZ>(p, w, w.S, s);
+}
+
+template <typename T>
+static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
+  const bool hz = p.z != nullptr;
+  if (p.softplus) {
+    if (hz) launch_seq_t<T, true, true>(p, w, s);
+    else launch_seq_t<T, true, false>(p, w, s);
+  } else {
+    if (hz) launch_seq_t<T, false, true>(p, w, s);
+    else launch_seq_t<T, false, false>(p, w, s);
+  }
+}
+
+// Segment count: minimise the busiest SIMD's cycles.  Per wave-step ~470 cycles for a
+// wave alone on its SIMD, ~380 per wave when two or more share it (gfx950 issue costs);
+// segmenting costs ~1.8x the work (summary + final pass) plus two launches.
+static int choose_segments(int batch, int dim, int seqlen) {
+  if (seqlen < 64) return 1;
+  const double groups = (dim + 63) / 64;
+  int best = 1;
+  double best_cost = 0.0;
+  for (int S = 1; S <= kMaxSeg; S *= 2) {
+    const int seg = (seqlen + S - 1) / S;
+    if (S > 1 && seg < 16) break;
+    const int s_eff = (seqlen + seg - 1) / seg;
+    const double waves = batch * groups * s_eff;
+    const double per_simd = waves / 1024.0 > 1.0 ? waves / 1024.0 : 1.0;
+    const double step = per_simd <= 1.0 ? 470.0 : 380.0 * per_simd;
+    const double cost = step * seg * (s_eff > 1 ? 1.8 : 1.0) + (s_eff > 1 ? 20000.0 : 0.0);
+    if (S == 1 || cost < best_cost) {
+      best = s_eff;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+// VM_SCAN_SEGMENTS (read per call) forces the segment count — tests and sweeps.
+static int segments_for(int batch, int dim, int seqlen) {
+  const char* e = getenv("VM_SCAN_SEGMENTS");
+  if (e && atoi(e) > 0) {
+    int S = atoi(e) < kMaxSeg ? atoi(e) : kMaxSeg;
+    if (S > seqlen) S = seqlen > 0 ? seqlen : 1;
+    return S;
+  }
+  return choose_segments(batch, dim, seqlen);
+}
+
+size_t seq_workspace_bytes(int batch, int dim, int seqlen, int* segments) {
+  const int S = segments_for(batch, dim, seqlen);
+  if (segments) *segments = S;
+  if (S <= 1) return 0;
+  return static_cast<size_t>(batch) * S * dim * (2 * kMaxN + 1) * sizeof(float);
+}
+
+bool seq_supported(const ScanParams& p, int dtype) {
+  // buffer offsets are 31-bit byte offsets from each batch row's base
+  const long long es = dtype == VM_DTYPE_BF16 ? 2 : 4;
+  const long long span = static_cast<long long>(p.out_len > p.seqlen ? p.out_len : p.seqlen) + 1;
+  auto fits = [&](long long sl) { return sl >= 0 && (span * sl + p.dim) * es < (1ll << 30); };
+  return p.u_sd == 1 && p.dl_sd == 1 && p.o_sd == 1 && (p.z == nullptr || p.z_sd == 1) &&
+         p.dstate <= kMaxN && fits(p.u_sl) && fits(p.dl_sl) && fits(p.o_sl) &&
+         (p.z == nullptr || fits(p.z_sl));
+}
+
+void seq_launch(const ScanParams& p, int dtype, void* workspace, size_t workspace_bytes,
+                hipStream_t s) {
+  int S = 1;
+  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, &S);
+  SeqWork w{};
+  if (S > 1 && workspace && workspace_bytes >= need) {
+    const size_t states = static_cast<size_t>(p.batch) * S * p.dim * kMaxN;
+    w.hend = static_cast<float*>(workspace);
+    w.hin = w.hend + states;
+    w.sdel = w.hin + states;
+    w.seg_len = (p.seqlen + S - 1) / S;
+    w.S = (p.seqlen + w.seg_len - 1) / w.seg_len;  // every segment non-empty
+  } else {
+    w.S = 1;
+    w.seg_len = p.seqlen;
+  }
+  if (dtype == VM_DTYPE_BF16) launch_seq<bf16_t>(p, w, s);
+  else launch_seq<float>(p, w, s);
+}
+
+}  // namespace vm

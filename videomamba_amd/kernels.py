@@ -85,29 +85,63 @@ def _lastdim_contig(t: Optional[Tensor]) -> Optional[Tensor]:
     return t if (t.stride(-1) == 1 or t.shape[-1] <= 1) else t.contiguous()
 
 
+def _channel_contig(t: Optional[Tensor]) -> Optional[Tensor]:
+    """(b, d, l) view with unit stride on d (token-major storage)."""
+    if t is None:
+        return None
+    if t.stride(1) == 1 or t.shape[1] <= 1:
+        return t
+    return t.transpose(1, 2).contiguous().transpose(1, 2)
+
+
 # --------------------------------------------------------------------------- raw launchers
+_WORKSPACE = {}
+
+
+def scan_workspace(device: torch.device, nbytes: int) -> Optional[Tensor]:
+    """Per-device scratch for the time-segmented token-major scan (grown, never shrunk)."""
+    if nbytes <= 0:
+        return None
+    key = (device.type, device.index)
+    buf = _WORKSPACE.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WORKSPACE[key] = buf
+    return buf
+
+
 def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, softplus,
              h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen, dstate, dtype,
              stream):
+    """Strides are (batch, channel|state, step) element strides; either every
+    u/delta/z/out channel stride is 1 (token-major) or every step stride is 1."""
     lib = _lib.load()
+    ws_bytes = 0
+    ws = None
+    if u_s[1] == 1:
+        ws_bytes = int(lib.vm_selective_scan_workspace_bytes(batch, dim, seqlen, dstate))
+        ws = scan_workspace(u.device, ws_bytes)
     rc = lib.vm_selective_scan_fwd(
-        _p(u), u_s[0], u_s[1], _p(delta), dl_s[0], dl_s[1], _p(A32),
-        _p(B), b_s[0], b_s[1], _p(C), c_s[0], c_s[1],
-        _p(D32), _p(z), z_s[0], z_s[1], _p(bias32), int(softplus),
+        _p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
+        _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
+        _p(D32), _p(z), z_s[0], z_s[1], z_s[2], _p(bias32), int(softplus),
         _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
         _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
-        _p(out), o_s[0], o_s[1], out_len, batch, dim, seqlen, dstate, dtype, stream)
+        _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate, dtype,
+        _p(ws), ws_bytes, stream)
     _lib.check(rc, "vm_selective_scan_fwd")
 
 
 def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, batch, dim,
              seqlen, width, silu, dtype, stream):
+    """x_s / o_s: (batch, channel, step) element strides (unit step or unit channel)."""
     lib = _lib.load()
     rc = lib.vm_causal_conv1d_fwd(
-        _p(x), x_s[0], x_s[1], _p(w32), _p(b32),
+        _p(x), x_s[0], x_s[1], x_s[2], _p(w32), _p(b32),
         _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
         _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
-        _p(out), o_s[0], o_s[1], out_len, batch, dim, seqlen, width, int(silu), dtype, stream)
+        _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, width, int(silu), dtype,
+        stream)
     _lib.check(rc, "vm_causal_conv1d_fwd")
 
 
@@ -155,12 +189,23 @@ def selective_scan_fn(u: Tensor, delta: Tensor, A: Tensor, B: Tensor, C: Tensor,
             last_state_out.copy_(h)
             h = last_state_out
         return out, h
-    u = _lastdim_contig(u)
-    delta = _lastdim_contig(delta.to(u.dtype))
-    z = _lastdim_contig(None if z is None else z.to(u.dtype))
-    B = _lastdim_contig(B.to(u.dtype))
-    C = _lastdim_contig(C.to(u.dtype))
-    out = torch.empty((batch, dim, seqlen), dtype=u.dtype, device=u.device)
+    # Layout follows u: token-major views (unit channel stride, e.g. a transposed
+    # (b, l, d) tensor) take the channel-per-lane kernels, anything else is made
+    # step-contiguous for the time-parallel kernels.
+    tm = dim > 1 and u.stride(1) == 1
+    conv = _channel_contig if tm else _lastdim_contig
+    u = conv(u)
+    delta = conv(delta.to(u.dtype))
+    z = conv(None if z is None else z.to(u.dtype))
+    B = B.to(u.dtype)
+    C = C.to(u.dtype)
+    if not tm:
+        B = _lastdim_contig(B)
+        C = _lastdim_contig(C)
+    if tm:
+        out = torch.empty((batch, seqlen, dim), dtype=u.dtype, device=u.device).transpose(1, 2)
+    else:
+        out = torch.empty((batch, dim, seqlen), dtype=u.dtype, device=u.device)
     h0 = None
     if initial_state is not None:
         h0 = _lastdim_contig(initial_state)
@@ -170,14 +215,13 @@ def selective_scan_fn(u: Tensor, delta: Tensor, A: Tensor, B: Tensor, C: Tensor,
             (batch, dim, dstate), dtype=torch.float32, device=u.device)
         if hl.stride(-1) != 1:
             raise ValueError("last_state_out must have unit stride on the state axis")
-    scan_raw(u, (u.stride(0), u.stride(1)), delta, (delta.stride(0), delta.stride(1)),
-             f32c(A), B, (B.stride(0), B.stride(1)), C, (C.stride(0), C.stride(1)),
-             f32c(D), z, (z.stride(0), z.stride(1)) if z is not None else (0, 0),
+    s3 = lambda t: (t.stride(0), t.stride(1), t.stride(2))  # noqa: E731
+    scan_raw(u, s3(u), delta, s3(delta), f32c(A), B, s3(B), C, s3(C),
+             f32c(D), z, s3(z) if z is not None else (0, 0, 0),
              f32c(delta_bias), delta_softplus,
              h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
              hl, (hl.stride(0), hl.stride(1)) if hl is not None else (0, 0),
-             out, (out.stride(0), out.stride(1)), seqlen, batch, dim, seqlen, dstate, dt,
-             _stream(u))
+             out, s3(out), seqlen, batch, dim, seqlen, dstate, dt, _stream(u))
     return (out, hl) if return_last_state else out
 
 
@@ -223,17 +267,21 @@ def causal_conv1d_fn(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None,
         weight = weight.reshape(weight.shape[0], weight.shape[-1])
     batch, dim, seqlen = x.shape
     width = weight.shape[1]
-    x = _lastdim_contig(x)
-    out = torch.empty((batch, dim, seqlen), dtype=x.dtype, device=x.device)
+    tm = dim > 1 and x.stride(1) == 1  # token-major view: keep the layout
+    if tm:
+        out = torch.empty((batch, seqlen, dim), dtype=x.dtype, device=x.device).transpose(1, 2)
+    else:
+        x = _lastdim_contig(x)
+        out = torch.empty((batch, dim, seqlen), dtype=x.dtype, device=x.device)
     cs_in = _lastdim_contig(conv_state)
     cs_out = None
     if return_conv_state:
         cs_dtype = conv_state.dtype if conv_state is not None else x.dtype
         cs_out = torch.empty((batch, dim, width), dtype=cs_dtype, device=x.device)
-    conv_raw(x, (x.stride(0), x.stride(1)), f32c(weight), f32c(bias),
+    conv_raw(x, (x.stride(0), x.stride(1), x.stride(2)), f32c(weight), f32c(bias),
              cs_in, (cs_in.stride(0), cs_in.stride(1)) if cs_in is not None else (0, 0),
              cs_out, (cs_out.stride(0), cs_out.stride(1)) if cs_out is not None else (0, 0),
-             out, (out.stride(0), out.stride(1)), seqlen, batch, dim, seqlen, width,
+             out, (out.stride(0), out.stride(1), out.stride(2)), seqlen, batch, dim, seqlen, width,
              activation is not None, dtype_code(x.dtype), _stream(x))
     return (out, cs_out) if return_conv_state else out
 

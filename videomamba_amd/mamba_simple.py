@@ -13,6 +13,13 @@ chosen for them:
     y  = selective_scan(u, dt, A, B, C, D, z, dt_bias, softplus)  HIP, fp32 state
     out = y^T @ W_out^T         -> (B*Lp, C)
 
+For batches that fill the chip (>= ~1.25 channel-group waves per SIMD) the mixer runs
+token-major instead — every buffer (B*Lp, channels), every projection a plain
+``F.linear`` — so the scan can take the channel-per-lane kernel (vm_scan_seq.hip):
+
+    xz = hn @ W_in^T (B*Lp, 2D);  u = conv(x) (B*Lp, D);  x_dbl = u @ W_x^T (B*Lp, R+2N)
+    dt = x_dbl[:, :R] @ W_dt^T (B*Lp, D);  y = scan(...) (B*Lp, D);  out = y @ W_out^T
+
 Rounding points match the reference slow path (xz, u, x_dbl, dt, y, out in the model
 dtype).  The GEMMs are plain library GEMMs (hipBLASLt via torch.matmul) on this layout;
 no transpose copies are materialised.  The scan runs once per chunk — never per token —
@@ -41,6 +48,20 @@ from .layers import round_up, warn_if_grad
 
 _CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP "
                "kernels (libvideomamba_hip, gfx950) are GPU-only.")
+
+
+def mixer_layout(batch: int, d_inner: int, device: torch.device) -> str:
+    """"tm" (token-major, channel-per-lane scan) when batch x 64-channel groups gives at
+    least ~1.25 waves per SIMD, else "cm" (channel-major, time-parallel scan).  Measured
+    at D=1152, L=3137 (profiles/): the time-parallel kernel costs ~24 us per clip-layer at
+    any batch, the channel-per-lane one ~1.6 ms flat up to 2 waves/SIMD (15 us per
+    clip-layer at B=112).  VM_MIXER_LAYOUT=tm|cm overrides."""
+    forced = os.getenv("VM_MIXER_LAYOUT", "").lower()
+    if forced in ("tm", "cm"):
+        return forced
+    simds = 4 * torch.cuda.get_device_properties(device).multi_processor_count
+    waves = batch * ((d_inner + 63) // 64)
+    return "tm" if waves >= 1.25 * simds else "cm"
 
 
 class InferenceParamsLike(Protocol):
@@ -126,6 +147,8 @@ class Mamba(nn.Module):
                         h_last: Optional[Tensor] = None) -> Tensor:
         """hn: (B, Lp, C) contiguous, rows >= seqlen zero.  Returns (B, Lp, C) with rows
         >= seqlen zero.  States are read/written by the kernels (see module doc)."""
+        if mixer_layout(hn.shape[0], self.d_inner, hn.device) == "tm":
+            return self._forward_padded_tm(hn, seqlen, conv_state_in, conv_state_out, h0, h_last)
         Bsz, Lp, C = hn.shape
         Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
         n = Bsz * Lp
@@ -133,29 +156,60 @@ class Mamba(nn.Module):
         stream = torch.cuda.current_stream(hn.device).cuda_stream
         A, Dv, dbias, cw, cb = self._fp32_params()
         rows = (Lp, n)  # (batch stride, channel stride) of a (ch, B*Lp) buffer
+        rows3 = (Lp, n, 1)  # + step stride
 
         xz = torch.matmul(self.in_proj.weight, hn.view(n, C).t())  # (2D, B*Lp)
         if self.in_proj.bias is not None:
             xz += self.in_proj.bias.to(xz.dtype)[:, None]
         x, z = xz[:Dm], xz[Dm:]
         u = torch.empty((Dm, n), dtype=hn.dtype, device=hn.device)
-        K.conv_raw(x, rows, cw, cb,
+        K.conv_raw(x, rows3, cw, cb,
                    conv_state_in, (conv_state_in.stride(0), conv_state_in.stride(1))
                    if conv_state_in is not None else (0, 0),
                    conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
                    if conv_state_out is not None else (0, 0),
-                   u, rows, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
+                   u, rows3, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
         x_dbl = torch.matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
         dt = torch.matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
         y = torch.empty_like(u)
-        K.scan_raw(u, rows, dt, rows, A, x_dbl[R:R + N], rows, x_dbl[R + N:], rows, Dv,
-                   z, rows, dbias, True,
+        K.scan_raw(u, rows3, dt, rows3, A, x_dbl[R:R + N], rows3, x_dbl[R + N:], rows3, Dv,
+                   z, rows3, dbias, True,
                    h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
                    h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
-                   y, rows, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+                   y, rows3, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
         out = torch.matmul(y.t(), self.out_proj.weight.t())  # (B*Lp, C)
         if self.out_proj.bias is not None:
             out += self.out_proj.bias.to(out.dtype)
+        return out.view(Bsz, Lp, C)
+
+    def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last):
+        """Token-major form of :meth:`_forward_padded` (same math, same rounding points)."""
+        Bsz, Lp, C = hn.shape
+        Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
+        n = Bsz * Lp
+        E = R + 2 * N
+        dt_code = K.dtype_code(hn.dtype)
+        stream = torch.cuda.current_stream(hn.device).cuda_stream
+        A, Dv, dbias, cw, cb = self._fp32_params()
+        s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
+
+        xz = F.linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
+        u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+        K.conv_raw(xz, s_xz, cw, cb,
+                   conv_state_in, (conv_state_in.stride(0), conv_state_in.stride(1))
+                   if conv_state_in is not None else (0, 0),
+                   conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
+                   if conv_state_out is not None else (0, 0),
+                   u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
+        x_dbl = F.linear(u, self.x_proj.weight)  # (n, R+2N)
+        dt = F.linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
+        y = torch.empty_like(u)
+        K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
+                   xz[:, Dm:], s_xz, dbias, True,
+                   h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
+                   h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
+                   y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+        out = F.linear(y, self.out_proj.weight, self.out_proj.bias)  # (n, C)
         return out.view(Bsz, Lp, C)
 
     def _check_state(self, t: Tensor, last: int, what: str, batch: int) -> Tensor:
