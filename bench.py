@@ -170,9 +170,9 @@ def cpu_baseline(cfg, threads):
 
 def main():
     args = _args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from videomamba_amd.sharding import dist_env, max_over_ranks
+
+    rank, local, world = dist_env()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
@@ -203,10 +203,7 @@ def main():
         _sync_barrier(world)
         elapsed = time.perf_counter() - t0
     assert torch.isfinite(out[1].float()).all()
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+    elapsed = max_over_ranks(elapsed, device)  # the slowest rank's clock
     ms_per_step = elapsed / args.steps * 1e3
     tokens = world * B * T * 196 * args.steps
     value = tokens / elapsed
