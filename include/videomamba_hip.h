@@ -13,6 +13,8 @@
  *   vm_causal_conv1d_fwd       <- causal_conv1d_fn (+ conv_state prepend)
  *                                 (mamba_simple.py:381-404)
  *   vm_causal_conv1d_update    <- causal_conv1d_update  (mamba_simple.py:468-474)
+ *   vm_conv_proj_fwd           <- causal_conv1d_fn + x_proj + dt_proj, fused, token-major
+ *                                 (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
@@ -116,6 +118,28 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
                          void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
                          int batch, int dim, int seqlen, int width, int silu, int dtype,
                          vm_stream_t stream);
+
+/*
+ * Fused token-major mixer middle (bf16): per token row of the flattened (batch, out_len)
+ * axis,  u = silu(conv1d([conv_state_in | x]))  ->  x_dbl = u @ W_x^T  ->
+ * dt = x_dbl[:, :r] @ W_dt^T, rounded to bf16 at each of the three (the reference's
+ * rounding points).  x: the first `dim` columns of xz rows (strides xz_sb, xz_sl; unit
+ * channel stride).  u, dt: (rows, dim), x_dbl: (rows, e), all batch-contiguous
+ * (sb == out_len * sl).  wx_pad: (e_pad, dim) with rows >= e zero (e_pad % 16 == 0,
+ * e_pad <= 128); wdt_pad: (dim, r_pad) with columns >= r zero (r_pad 32 or 64).  Rows
+ * with step >= seqlen are written as 0.  conv state as vm_causal_conv1d_fwd (width <= 4).
+ * dim % 64 == 0, seqlen >= 1.
+ */
+int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
+                     const float* conv_weight, const float* conv_bias,
+                     const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
+                     void* cs_out, int cs_out_dtype, long long cso_sb, long long cso_sd,
+                     const void* wx_pad, int e, int e_pad, const void* wdt_pad, int r, int r_pad,
+                     void* u, long long u_sb, long long u_sl,
+                     void* xdbl, long long xd_sb, long long xd_sl,
+                     void* dt, long long dt_sb, long long dt_sl,
+                     int out_len, int batch, int dim, int seqlen, int width, int dtype,
+                     vm_stream_t stream);
 
 /*
  * One-token conv step: shift conv_state left by one, append x, dot with weight (+bias),

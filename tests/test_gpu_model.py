@@ -386,3 +386,36 @@ def test_large_batch_selects_token_major_and_matches_channel_major(monkeypatch):
         cm = model(x)
     rel = ((auto.float() - cm.float()).norm() / cm.float().norm()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("d_model,L,split", [(96, 301, 130), (64, 70, 3), (288, 1000, 999)])
+def test_fused_conv_proj_mixer_bf16_matches_oracle_and_unfused(d_model, L, split, monkeypatch):
+    """Token-major bf16 mixer with the fused conv+x_proj+dt_proj kernel (D % 64 == 0):
+    vs the oracle's bf16 restatement and vs the unfused token-major path, full and two
+    chunks with carried (conv_state, ssm_state) — including a 3-token first chunk (the conv
+    halo reaches into the state) and a 1-token second chunk."""
+    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
+    torch.manual_seed(d_model)
+    m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.add_(0.02 * torch.randn_like(prm))
+    m = m.to(torch.bfloat16).to(DEV).eval()
+    p = {k: v.detach().float().cpu().to(torch.bfloat16) for k, v in m.state_dict().items()}
+    x = torch.randn(3, L, d_model).to(torch.bfloat16)
+    ref = orc.mamba_mixer(p, "", x, d_state=16, d_conv=4)
+    xd = x.to(DEV)
+    with torch.no_grad():
+        full = m(xd)
+        o1, (c1, s1) = m(xd[:, :split], return_state=True)
+        o2, (c2, s2) = m(xd[:, split:], state=(c1, s1), return_state=True)
+        monkeypatch.setenv("VM_FUSED_CONV_PROJ", "0")
+        unfused = m(xd)
+    _close(full, ref, 5e-2)
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(full, unfused) < 1e-2
+    assert rel(torch.cat([o1, o2], 1), full) < 1e-2
+    r1, (rc1, rs1) = orc.mamba_mixer(p, "", x[:, :split], d_state=16, d_conv=4,
+                                     return_state=True)
+    _close(c1, rc1, 2e-2)
+    _close(s1, rs1, 5e-2)

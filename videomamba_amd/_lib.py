@@ -50,6 +50,12 @@ _SIGNATURES = {
     "vm_causal_conv1d_fwd": (
         [_P, _LL, _LL, _LL, _P, _P, _P, _I, _LL, _LL, _P, _I, _LL, _LL, _P, _LL, _LL, _LL, _I,
          _I, _I, _I, _I, _I, _I, _P], _I),
+    "vm_conv_proj_fwd": (
+        [_P, _LL, _LL, _P, _P,                    # xz, conv weight / bias
+         _P, _I, _LL, _LL, _P, _I, _LL, _LL,      # conv state in / out
+         _P, _I, _I, _P, _I, _I,                  # W_x pad, e, e_pad, W_dt pad, r, r_pad
+         _P, _LL, _LL, _P, _LL, _LL, _P, _LL, _LL,  # u, x_dbl, dt
+         _I, _I, _I, _I, _I, _I, _P], _I),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_add_norm_fwd": (

@@ -145,6 +145,22 @@ def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, b
     _lib.check(rc, "vm_causal_conv1d_fwd")
 
 
+def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, wdt_pad, r,
+                  u, u_s, xdbl, xd_s, dt, dt_s, out_len, batch, dim, seqlen, width, stream):
+    """Fused token-major conv1d + SiLU -> x_proj -> dt_proj (bf16).  *_s = (batch, step)
+    element strides of the token-major buffers; wx_pad (e_pad, D) / wdt_pad (D, r_pad) are
+    zero-padded copies of the projection weights."""
+    lib = _lib.load()
+    rc = lib.vm_conv_proj_fwd(
+        _p(xz), xz_s[0], xz_s[1], _p(cw32), _p(cb32),
+        _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
+        _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
+        _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad), r, wdt_pad.shape[1],
+        _p(u), u_s[0], u_s[1], _p(xdbl), xd_s[0], xd_s[1], _p(dt), dt_s[0], dt_s[1],
+        out_len, batch, dim, seqlen, width, dtype_code(u.dtype), stream)
+    _lib.check(rc, "vm_conv_proj_fwd")
+
+
 def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_rms, stream):
     lib = _lib.load()
     rc = lib.vm_add_norm_fwd(

@@ -141,6 +141,30 @@ class Mamba(nn.Module):
             self._pcache_key = key
         return self._pcache
 
+    def _padded_proj_weights(self):
+        """x_proj / dt_proj weights zero-padded for the fused conv_proj kernel:
+        W_x -> (round_up(R+2N, 16), D), W_dt -> (D, 32 or 64); cached per version."""
+        srcs = (self.x_proj.weight, self.dt_proj.weight)
+        key = tuple((p.data_ptr(), p._version, p.dtype, p.device) for p in srcs)
+        if key != getattr(self, "_wpad_key", None):
+            with torch.no_grad():
+                wx, wdt = self.x_proj.weight, self.dt_proj.weight
+                e, r = wx.shape[0], wdt.shape[1]
+                wx_pad = wx.new_zeros(((e + 15) // 16 * 16, wx.shape[1]))
+                wx_pad[:e] = wx
+                wdt_pad = wdt.new_zeros((wdt.shape[0], 32 if r <= 32 else 64))
+                wdt_pad[:, :r] = wdt
+            self._wpad = (wx_pad.contiguous(), wdt_pad.contiguous())
+            self._wpad_key = key
+        return self._wpad
+
+    def _fused_conv_proj_ok(self, hn: Tensor, seqlen: int) -> bool:
+        E = self.dt_rank + 2 * self.d_state
+        return (hn.dtype == torch.bfloat16 and seqlen >= 1 and self.d_inner % 64 == 0
+                and self.d_conv <= 4 and E <= 128 and self.dt_rank <= 64
+                and self.x_proj.bias is None and self.dt_proj.weight.dtype == torch.bfloat16
+                and os.getenv("VM_FUSED_CONV_PROJ", "1") != "0")
+
     # ------------------------------------------------------------------ core
     def _forward_padded(self, hn: Tensor, seqlen: int, *, conv_state_in: Optional[Tensor] = None,
                         conv_state_out: Optional[Tensor] = None, h0: Optional[Tensor] = None,
@@ -195,14 +219,23 @@ class Mamba(nn.Module):
 
         xz = F.linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
         u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
-        K.conv_raw(xz, s_xz, cw, cb,
-                   conv_state_in, (conv_state_in.stride(0), conv_state_in.stride(1))
-                   if conv_state_in is not None else (0, 0),
-                   conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
-                   if conv_state_out is not None else (0, 0),
-                   u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
-        x_dbl = F.linear(u, self.x_proj.weight)  # (n, R+2N)
-        dt = F.linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
+        csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
+                 if conv_state_in is not None else (0, 0))
+        cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
+                 if conv_state_out is not None else (0, 0))
+        if self._fused_conv_proj_ok(hn, seqlen):
+            # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip)
+            wx_pad, wdt_pad = self._padded_proj_weights()
+            x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
+            dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            K.conv_proj_raw(xz, s_xz[::2], cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
+                            wx_pad, E, wdt_pad, R, u, s_u[::2], x_dbl, (Lp * E, E), dt,
+                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream)
+        else:
+            K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
+                       u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
+            x_dbl = F.linear(u, self.x_proj.weight)  # (n, R+2N)
+            dt = F.linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
         y = torch.empty_like(u)
         K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                    xz[:, Dm:], s_xz, dbias, True,
