@@ -244,6 +244,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         print(json.dumps(line), flush=True)
+    if torch.cuda.tunable.is_enabled() and torch.cuda.tunable.tuning_is_enabled():
+        torch.cuda.tunable.write_file()  # VM_GEMM_TUNING=tune: persist new GEMM results
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

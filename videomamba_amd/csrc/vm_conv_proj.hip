@@ -19,6 +19,8 @@
 // W_dt fragments straight from L2 (each read by one wave of the workgroup).
 // HBM traffic per token: x row in, u / dt rows out (+ x_dbl): 3 * D * 2 + 2 * (R + 2N) B.
 
+#include <stdlib.h>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -50,104 +52,132 @@ __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return static_cast<uint32_t>(from_f32<bf16_t>(a)) | (static_cast<uint32_t>(from_f32<bf16_t>(b)) << 16);
+}
+__device__ __forceinline__ float silu_f(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2e));
+}
 
+__device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
+                                         int row0, int lane, int wave);
+
+// LDS: sA [64][72] bf16 (u chunk, then x_dbl[:, :R]);  sU [4 waves][64][72] bf16 (W_x
+// chunk during the sweep, then per-wave output staging);  dynamic: conv weights (D, 4)
+// and bias (D) as fp32.
+template <bool DT, int NB>  // DT: also run dt_proj here; NB = e_pad / 16 x_proj blocks
 __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
-  __shared__ __attribute__((aligned(16))) bf16_t sB[kCPMaxNB * 16 * kCPPad];
+  __shared__ __attribute__((aligned(16))) bf16_t sU[4 * kCPTok * kCPPad];
+  extern __shared__ __attribute__((aligned(16))) float sW[];  // [D][4] taps, then [D] bias
+  bf16_t* sB = sU;  // W_x chunk: e_pad (<= 128) rows of kCPPad
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int row0 = blockIdx.x * kCPTok;
-  const int nb = p.e_pad / 16;
+  const int D = p.dim;
 
-  // conv role: 8 channels x 2 token rows
+  // conv weights, right-aligned into 4 taps, and bias -> LDS
+  for (int i = tid; i < D * 4; i += 256) {
+    const int ch = i >> 2, tap = (i & 3) - (4 - p.width);
+    sW[i] = tap >= 0 ? p.cw[ch * p.width + tap] : 0.0f;
+  }
+  for (int i = tid; i < D; i += 256) sW[4 * D + i] = p.cb ? p.cb[i] : 0.0f;
+
+  // conv role: 8 channels x 2 adjacent token rows (same sequence: rows 2k, 2k+1 never
+  // straddle a batch boundary because out_len is even)
   const int cg = tid & 7;
   const int tg = tid >> 3;
-  int tb[2], tt[2];
-  bool rv[2];
+  const int rowa = row0 + 2 * tg;
+  const bool rva = rowa < p.rows, rvb = rowa + 1 < p.rows;
+  const int rr = rva ? rowa : p.rows - 1;
+  const int b = rr / p.lp;
+  const int ta = rr - b * p.lp;  // step of the first row; window rows ta-3 .. ta+1
+  const bf16_t* xrow = p.xz + b * p.xz_sb;
+  auto load_win = [&](int c, uint4 (&w)[5]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = row0 + 2 * tg + i;
-    rv[i] = row < p.rows;
-    const int rr = rv[i] ? row : p.rows - 1;
-    tb[i] = rr / p.lp;
-    tt[i] = rr - tb[i] * p.lp;
-  }
+    for (int j = 0; j < 5; ++j) {
+      const int te = ta - 3 + j;
+      w[j] = (te >= 0 && te < p.seqlen)
+                 ? *reinterpret_cast<const uint4*>(xrow + te * p.xz_sl + c)
+                 : make_uint4(0, 0, 0, 0);
+    }
+  };
 
-  f32x4 acc[kCPMaxNB];
+  f32x4 acc[NB];
 #pragma unroll
-  for (int j = 0; j < kCPMaxNB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c0 = 0; c0 < p.dim; c0 += kCPCh) {
-    // ---- stage W_x[:, c0:c0+64] (e_pad rows x 128 B) ----
+  uint4 cur[5], nxt[5];
+  load_win(cg * 8, cur);
+  __syncthreads();  // sW ready
+  for (int c0 = 0; c0 < D; c0 += kCPCh) {
+    const int c = c0 + cg * 8;
+    if (c0 + kCPCh < D) load_win(c + kCPCh, nxt);  // prefetch the next chunk's window
+    // ---- stage W_x[:, c0:c0+64] ----
     for (int idx = tid; idx < p.e_pad * 8; idx += 256) {
       const int n = idx >> 3, q = idx & 7;
       *reinterpret_cast<uint4*>(&sB[n * kCPPad + q * 8]) =
-          *reinterpret_cast<const uint4*>(p.wx + (long long)n * p.dim + c0 + q * 8);
+          *reinterpret_cast<const uint4*>(p.wx + (long long)n * D + c0 + q * 8);
     }
-    // ---- conv + silu for (2 tokens) x (8 channels) ----
-    const int c = c0 + cg * 8;
-    float w[4][8], bias[8];
+    // ---- conv + silu, one channel pair (one packed word of each window row) at a time ----
+    if (ta < 3 && p.csi) {  // window reaches before the sequence start: conv state
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int ch = c + k;
+      for (int j = 0; j < 3; ++j) {
+        const int te = ta - 3 + j;
+        const int sj = p.width + te;
+        if (te < 0 && sj >= 0) {
+          uint32_t w4[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int tap = i - (4 - p.width);  // right-aligned taps
-        w[i][k] = tap >= 0 ? p.cw[ch * p.width + tap] : 0.0f;
-      }
-      bias[k] = p.cb ? p.cb[ch] : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int b = tb[i], t = tt[i];
-      float o[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = bias[k];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int te = t - 3 + j;
-        float v[8];
-        if (te >= 0 && te < p.seqlen) {
-          const uint4 q = *reinterpret_cast<const uint4*>(p.xz + b * p.xz_sb + te * p.xz_sl + c);
-          unpack8(q, v);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int sj = p.width + te;  // state column of virtual step te < 0
-            v[k] = (te < 0 && p.csi && sj >= 0)
-                       ? load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd + sj,
-                                  p.csi_dtype)
-                       : 0.0f;
-          }
+          for (int k = 0; k < 8; k += 2)
+            w4[k / 2] = pack2(
+                load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd + sj, p.csi_dtype),
+                load_dyn(p.csi, b * p.csi_sb + (long long)(c + k + 1) * p.csi_sd + sj,
+                         p.csi_dtype));
+          cur[j] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = fmaf(w[j][k], v[k], o[k]);
       }
-      const bool live = rv[i] && t < p.seqlen;
-      uint32_t packed[4];
+    }
+    const bool la = rva && ta < p.seqlen, lb = rvb && ta + 1 < p.seqlen;
+    uint32_t pa[4], pb[4];
 #pragma unroll
-      for (int k = 0; k < 8; k += 2) {
-        const float a0 = live ? silu(o[k]) : 0.0f;
-        const float a1 = live ? silu(o[k + 1]) : 0.0f;
-        packed[k / 2] = static_cast<uint32_t>(from_f32<bf16_t>(a0)) |
-                        (static_cast<uint32_t>(from_f32<bf16_t>(a1)) << 16);
+    for (int q = 0; q < 4; ++q) {
+      float lo[5], hi[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const uint32_t wd = q == 0 ? cur[j].x : q == 1 ? cur[j].y : q == 2 ? cur[j].z : cur[j].w;
+        lo[j] = __uint_as_float(wd << 16);
+        hi[j] = __uint_as_float(wd & 0xffff0000u);
       }
-      const uint4 pq = make_uint4(packed[0], packed[1], packed[2], packed[3]);
-      if (rv[i]) *reinterpret_cast<uint4*>(p.u + (long long)(row0 + 2 * tg + i) * p.u_sl + c) = pq;
-      *reinterpret_cast<uint4*>(&sA[(2 * tg + i) * kCPPad + cg * 8]) = pq;
-      // new conv state: the last `width` raw inputs, from the row holding step L-1
-      if (p.cso && live && t == p.seqlen - 1) {  // one row per sequence: reload
-        for (int k = 0; k < 8; ++k)
-          for (int s = 0; s < p.width; ++s) {
-            const int te = t - p.width + 1 + s;
-            float v = 0.0f;
-            if (te >= 0) v = to_f32(p.xz[b * p.xz_sb + te * p.xz_sl + c + k]);
-            else if (p.csi) v = load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd +
+      const int ch = c + 2 * q;
+      const float4 wl = *reinterpret_cast<const float4*>(&sW[ch * 4]);
+      const float4 wh = *reinterpret_cast<const float4*>(&sW[(ch + 1) * 4]);
+      const float bl = sW[4 * D + ch], bh = sW[4 * D + ch + 1];
+      const float a0 = fmaf(wl.w, lo[3], fmaf(wl.z, lo[2], fmaf(wl.y, lo[1], fmaf(wl.x, lo[0], bl))));
+      const float a1 = fmaf(wh.w, hi[3], fmaf(wh.z, hi[2], fmaf(wh.y, hi[1], fmaf(wh.x, hi[0], bh))));
+      const float b0 = fmaf(wl.w, lo[4], fmaf(wl.z, lo[3], fmaf(wl.y, lo[2], fmaf(wl.x, lo[1], bl))));
+      const float b1 = fmaf(wh.w, hi[4], fmaf(wh.z, hi[3], fmaf(wh.y, hi[2], fmaf(wh.x, hi[1], bh))));
+      pa[q] = pack2(la ? silu_f(a0) : 0.f, la ? silu_f(a1) : 0.f);
+      pb[q] = pack2(lb ? silu_f(b0) : 0.f, lb ? silu_f(b1) : 0.f);
+    }
+    const uint4 qa = make_uint4(pa[0], pa[1], pa[2], pa[3]);
+    const uint4 qb = make_uint4(pb[0], pb[1], pb[2], pb[3]);
+    if (rva) *reinterpret_cast<uint4*>(p.u + (long long)rowa * p.u_sl + c) = qa;
+    if (rvb) *reinterpret_cast<uint4*>(p.u + (long long)(rowa + 1) * p.u_sl + c) = qb;
+    *reinterpret_cast<uint4*>(&sA[(2 * tg) * kCPPad + cg * 8]) = qa;
+    *reinterpret_cast<uint4*>(&sA[(2 * tg + 1) * kCPPad + cg * 8]) = qb;
+    // new conv state: the last `width` raw inputs, from the row holding step L-1
+    if (p.cso && ((la && ta == p.seqlen - 1) || (lb && ta + 1 == p.seqlen - 1))) {
+      const int t = p.seqlen - 1;
+      for (int k = 0; k < 8; ++k)
+        for (int s = 0; s < p.width; ++s) {
+          const int te = t - p.width + 1 + s;
+          float val = 0.0f;
+          if (te >= 0) val = to_f32(xrow[te * p.xz_sl + c + k]);
+          else if (p.csi) val = load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd +
                                                     p.width + te, p.csi_dtype);
-            store_dyn(p.cso, b * p.cso_sb + (long long)(c + k) * p.cso_sd + s, p.cso_dtype, v);
-          }
-      }
+          store_dyn(p.cso, b * p.cso_sb + (long long)(c + k) * p.cso_sd + s, p.cso_dtype, val);
+        }
     }
     __syncthreads();
     // ---- x_proj MFMA: wave's 16 tokens x all e_pad outputs, K = 64 ----
@@ -156,38 +186,57 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(
           &sA[(wave * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
 #pragma unroll
-      for (int j = 0; j < kCPMaxNB; ++j) {
-        if (j < nb) {
-          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
-              &sB[(j * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, acc[j], 0, 0, 0);
-        }
+      for (int j = 0; j < NB; ++j) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+            &sB[(j * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, acc[j], 0, 0, 0);
       }
     }
     __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 5; ++j) cur[j] = nxt[j];
   }
 
-  // ---- x_dbl: round to bf16, store, and stage x_dbl[:, :R] (zero-padded) as dt's A ----
+  // ---- x_dbl: bf16 tile [64][e_pad] in sU (stride kCPPad*2), x_dbl[:, :R] -> sA ----
+  bf16_t* sX = sU;  // [64][2 * kCPPad] (e_pad <= 128 < 144)
   for (int idx = tid; idx < kCPTok * kCPPad / 8; idx += 256)
     *reinterpret_cast<uint4*>(&sA[idx * 8]) = make_uint4(0, 0, 0, 0);
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kCPMaxNB; ++j) {
-    if (j < nb) {
-      const int n = j * 16 + (lane & 15);
+  for (int j = 0; j < NB; ++j) {
+    const int n = j * 16 + (lane & 15);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int lr = wave * 16 + (lane >> 4) * 4 + e;
-        const int row = row0 + lr;
-        const bf16_t v = from_f32<bf16_t>(acc[j][e]);
-        if (n < p.e && row < p.rows) p.xdbl[(long long)row * p.xd_sl + n] = v;
-        if (n < p.r) sA[lr * kCPPad + n] = v;
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int lr = wave * 16 + (lane >> 4) * 4 + e;
+      const bf16_t v = from_f32<bf16_t>(acc[j][e]);
+      sX[lr * 2 * kCPPad + n] = v;
+      if (n < p.r) sA[lr * kCPPad + n] = v;
     }
   }
   __syncthreads();
+  // coalesced x_dbl rows: e (even) bf16 per row, 4-byte pieces
+  {
+    const int pieces = p.e / 2;
+    for (int idx = tid; idx < kCPTok * pieces; idx += 256) {
+      const int lr = idx / pieces, q = idx - lr * pieces;
+      const int row = row0 + lr;
+      if (row < p.rows)
+        *reinterpret_cast<uint32_t*>(p.xdbl + (long long)row * p.xd_sl + 2 * q) =
+            *reinterpret_cast<const uint32_t*>(&sX[lr * 2 * kCPPad + 2 * q]);
+    }
+  }
+  if constexpr (DT) {
+    __syncthreads();  // sU is reused below as per-wave output staging
+    dt_phase(p, sA, sU, row0, lane, wave);
+  }
+}
 
-  // ---- dt_proj MFMA: wave = column blocks wave, wave+4, ...; all 64 tokens ----
+// dt_proj for one 64-token tile: A = x_dbl[:, :R] (zero-padded to r_pad) in sA,
+// wave = 64-column blocks wave, wave+4, ...; outputs staged per wave in sU and stored as
+// 128-byte row segments.
+__device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
+                                         int row0, int lane, int wave) {
+  const int D = p.dim;
   const int ksteps = p.r_pad / 32;
   bf16x8 af[4][2];
 #pragma unroll
@@ -196,28 +245,64 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
     for (int ks = 0; ks < 2; ++ks)
       af[i][ks] = *reinterpret_cast<const bf16x8*>(
           &sA[(i * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
-  const int rbase = row0 + (lane >> 4) * 4;  // + i * 16 + e
-  bf16_t* __restrict__ dtp = p.dt + (long long)rbase * p.dt_sl;
-  for (int nblk = wave; nblk * 16 < p.dim; nblk += 4) {
-    const int n = nblk * 16 + (lane & 15);
-    bf16x8 bf[2];
+  bf16_t* stg = sU + wave * kCPTok * kCPPad;
+  for (int cb = wave; cb * 64 < D; cb += 4) {
+    f32x4 d[4][4];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      bf[ks] = ks < ksteps ? *reinterpret_cast<const bf16x8*>(
-                                 p.wdt + (long long)n * p.r_pad + ks * 32 + (lane >> 4) * 8)
-                           : bf16x8{};
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) d[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        if (ks < ksteps) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[ks], d, 0, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int n = cb * 64 + j * 16 + (lane & 15);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (rbase + i * 16 + e < p.rows)
-          dtp[(long long)(i * 16 + e) * p.dt_sl + n] = from_f32<bf16_t>(d[e]);
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks < ksteps) {
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+              p.wdt + (long long)n * p.r_pad + ks * 32 + (lane >> 4) * 8);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            d[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bv, d[i][j], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
+              from_f32<bf16_t>(d[i][j][e]);
+    // the wave reads back its own staging tile: 64 rows x 128 B, 16 B per lane-store
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + (lane >> 3), q = lane & 7;
+      const int row = row0 + lr;
+      const uint4 val = *reinterpret_cast<const uint4*>(&stg[lr * kCPPad + q * 8]);
+      if (row < p.rows)
+        *reinterpret_cast<uint4*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 8) = val;
     }
   }
+}
+
+
+// dt = x_dbl[:, :R] @ W_dt^T for 64-token tiles (the split form of conv_proj_kernel<true>).
+__global__ __launch_bounds__(256) void dt_proj_kernel(const ConvProjParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
+  __shared__ __attribute__((aligned(16))) bf16_t sU[4 * kCPTok * kCPPad];
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.x * kCPTok;
+  for (int idx = tid; idx < kCPTok * kCPPad / 8; idx += 256)
+    *reinterpret_cast<uint4*>(&sA[idx * 8]) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  for (int idx = tid; idx < kCPTok * p.r; idx += 256) {
+    const int lr = idx / p.r, k = idx - lr * p.r;
+    const int row = row0 + lr;
+    sA[lr * kCPPad + k] = row < p.rows ? p.xdbl[(long long)row * p.xd_sl + k] : bf16_t(0);
+  }
+  __syncthreads();
+  dt_phase(p, sA, sU, row0, tid & 63, tid >> 6);
 }
 
 }  // namespace vm
@@ -248,8 +333,11 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     return VM_E_INVALID;
   }
   if (!vmhost::aligned16(xz) || !vmhost::aligned16(u) || !vmhost::aligned16(wx_pad) ||
-      !vmhost::aligned16(wdt_pad) || xz_sb % 8 || xz_sl % 8 || u_sb % 8 || u_sl % 8) {
-    vmhost::set_error("vm_conv_proj_fwd: xz / u / weights need 16-byte aligned rows");
+      !vmhost::aligned16(wdt_pad) || !vmhost::aligned16(dt) || xz_sb % 8 || xz_sl % 8 ||
+      u_sb % 8 || u_sl % 8 || dt_sl % 8 || out_len % 2 || e % 2 || xd_sl % 2 ||
+      (reinterpret_cast<uintptr_t>(xdbl) & 3) || dim > 8192) {
+    vmhost::set_error("vm_conv_proj_fwd: xz / u / dt / weights need 16-byte aligned rows, "
+                      "x_dbl 4-byte aligned, even out_len and e, dim <= 8192");
     return VM_E_INVALID;
   }
   if (u_sb != out_len * u_sl || xd_sb != out_len * xd_sl || dt_sb != out_len * dt_sl) {
@@ -275,6 +363,22 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   p.rows = batch * out_len; p.e = e; p.e_pad = e_pad; p.r = r; p.r_pad = r_pad;
   p.width = width; p.csi_dtype = cs_in_dtype; p.cso_dtype = cs_out_dtype;
   dim3 grid((p.rows + kCPTok - 1) / kCPTok);
-  hipLaunchKernelGGL(conv_proj_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream), p);
+  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const char* split = getenv("VM_CONV_PROJ_SPLIT");
+  const bool fused_dt = split && atoi(split) == 0;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
+  switch (e_pad / 16) {  // x_proj output blocks
+#define VM_CP_CASE(NBV)                                              \
+    case NBV:                                                        \
+      if (fused_dt) go(conv_proj_kernel<true, NBV>);                 \
+      else go(conv_proj_kernel<false, NBV>);                         \
+      break;
+    VM_CP_CASE(1) VM_CP_CASE(2) VM_CP_CASE(3) VM_CP_CASE(4)
+    VM_CP_CASE(5) VM_CP_CASE(6) VM_CP_CASE(7) VM_CP_CASE(8)
+#undef VM_CP_CASE
+  }
+  // conv + x_proj at lower register pressure, then dt_proj from x_dbl
+  if (!fused_dt) hipLaunchKernelGGL(dt_proj_kernel, grid, dim3(256), 0, st, p);
   return vmhost::launch_status("vm_conv_proj_fwd");
 }

@@ -44,6 +44,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from . import kernels as K
+from .gemm_tuning import enable_tuned_gemms
 from .layers import round_up, warn_if_grad
 
 _CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP "
@@ -171,6 +172,7 @@ class Mamba(nn.Module):
                         h_last: Optional[Tensor] = None) -> Tensor:
         """hn: (B, Lp, C) contiguous, rows >= seqlen zero.  Returns (B, Lp, C) with rows
         >= seqlen zero.  States are read/written by the kernels (see module doc)."""
+        enable_tuned_gemms()
         if mixer_layout(hn.shape[0], self.d_inner, hn.device) == "tm":
             return self._forward_padded_tm(hn, seqlen, conv_state_in, conv_state_out, h0, h_last)
         Bsz, Lp, C = hn.shape
