@@ -68,9 +68,14 @@ __device__ __forceinline__ float raw_f32(uint32_t r) {
 }
 
 // MODE 0: single pass (entry state h0), MODE 1: summary, MODE 2: final with entry states.
-template <typename T, int NW, int MODE, bool SP, bool HZ>
+// SB: B_t / C_t (16 states, unit state stride, 4-byte aligned rows) come in as scalar
+// loads — wave-uniform SGPR operands of the VALU ops, one step ahead — instead of the LDS
+// staging + broadcast reads.
+template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB>
 __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, const SeqWork w) {
   static_assert(NW * 64 >= 4 * kTS, "B/C staging needs 4 threads per block step");
+  typedef __attribute__((address_space(4))) const uint32_t* cptr;
+  constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
   __shared__ __attribute__((aligned(16))) float sbc[2][kTS][2 * kMaxN];
 
   const int tid = threadIdx.x;
@@ -142,17 +147,34 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
 
   const int nblk = t_end > t_beg ? (t_end - t_beg + kTS - 1) / kTS : 0;
   float stg[8];
-  if (nblk > 0) {
-    stage_load(t_beg, stg);
-    stage_store(0, stg);
+  if constexpr (!SB) {
+    if (nblk > 0) {
+      stage_load(t_beg, stg);
+      stage_store(0, stg);
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  const T* Bq = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cq = static_cast<const T*>(p.C) + b * p.c_sb;
+  uint32_t bcw[2][2 * NWD];  // [step parity][B words | C words]
+  auto bc_load = [&](int t, uint32_t (&dst)[2 * NWD]) {
+    const cptr bp = (cptr)(Bq + static_cast<long long>(t) * p.b_sl);  // generic -> constant AS
+    const cptr cp = (cptr)(Cq + static_cast<long long>(t) * p.c_sl);
+#pragma unroll
+    for (int i = 0; i < NWD; ++i) {
+      dst[i] = bp[i];
+      if constexpr (MODE != 1) dst[NWD + i] = cp[i];
+    }
+  };
 
   // Drain the parameter loads (A, D, bias, entry state) here: left pending they merge into
   // the step loop's header and force a conservative vmcnt wait on every iteration.
   __builtin_amdgcn_s_waitcnt(0);
   uint32_t ru[kPF], rd[kPF], rz[kPF];
   const int tlast = L > 0 ? L - 1 : 0;
+  if constexpr (SB) {
+    if (nblk > 0) bc_load(t_beg, bcw[0]);
+  }
   if (nblk > 0) {
 #pragma unroll
     for (int j = 0; j < kPF; ++j) {
@@ -167,7 +189,9 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   for (int k = 0; k < nblk; ++k) {
     const int tb = t_beg + k * kTS;
     const bool more = k + 1 < nblk;
-    if (more) stage_load(tb + kTS, stg);
+    if constexpr (!SB) {
+      if (more) stage_load(tb + kTS, stg);
+    }
     const float* blk = &sbc[k & 1][0][0];
     for (int g = 0; g < kTS; g += kPF) {
 #pragma unroll
@@ -182,6 +206,12 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
           rd[j] = bload<T>(dr_, voff, tn * ds);
           if (HZ && MODE != 1) rz[j] = bload<T>(zr, voff, tn * zs);
         }
+        if constexpr (SB) {
+          // this step's B/C rows (issued one step ago) have landed — explicit lgkmcnt(0),
+          // scalar loads return out of order — then fetch the next step's rows
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+        }
         // keep each step's refill loads at the step head: the scheduler would otherwise
         // sink them below all eight steps, collapsing the prefetch distance to zero
         // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
@@ -191,15 +221,30 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         if (SP) dl = softplus_fast(dl);
         dl = live ? dl : 0.0f;
         const float du = dl * uu;
-        const float4* row = reinterpret_cast<const float4*>(blk + (g + j) * 2 * kMaxN);
         float Bv[kMaxN], Cv[kMaxN];
+        if constexpr (SB) {
+          const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
 #pragma unroll
-        for (int q = 0; q < kMaxN / 4; ++q) {
-          const float4 bq = row[q];
-          Bv[4 * q] = bq.x; Bv[4 * q + 1] = bq.y; Bv[4 * q + 2] = bq.z; Bv[4 * q + 3] = bq.w;
-          if constexpr (MODE != 1) {
-            const float4 cq = row[kMaxN / 4 + q];
-            Cv[4 * q] = cq.x; Cv[4 * q + 1] = cq.y; Cv[4 * q + 2] = cq.z; Cv[4 * q + 3] = cq.w;
+          for (int n = 0; n < kMaxN; ++n) {
+            if constexpr (sizeof(T) == 2) {
+              const uint32_t wb = cw[n >> 1], wc = cw[NWD + (n >> 1)];
+              Bv[n] = __uint_as_float((n & 1) ? (wb & 0xffff0000u) : (wb << 16));
+              Cv[n] = __uint_as_float((n & 1) ? (wc & 0xffff0000u) : (wc << 16));
+            } else {
+              Bv[n] = __uint_as_float(cw[n]);
+              Cv[n] = __uint_as_float(cw[NWD + n]);
+            }
+          }
+        } else {
+          const float4* row = reinterpret_cast<const float4*>(blk + (g + j) * 2 * kMaxN);
+#pragma unroll
+          for (int q = 0; q < kMaxN / 4; ++q) {
+            const float4 bq = row[q];
+            Bv[4 * q] = bq.x; Bv[4 * q + 1] = bq.y; Bv[4 * q + 2] = bq.z; Bv[4 * q + 3] = bq.w;
+            if constexpr (MODE != 1) {
+              const float4 cq = row[kMaxN / 4 + q];
+              Cv[4 * q] = cq.x; Cv[4 * q + 1] = cq.y; Cv[4 * q + 2] = cq.z; Cv[4 * q + 3] = cq.w;
+            }
           }
         }
         if constexpr (MODE == 1) {
@@ -224,8 +269,10 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         }
       }
     }
-    if (more) stage_store((k + 1) & 1, stg);
-    __syncthreads();
+    if constexpr (!SB) {
+      if (more) stage_store((k + 1) & 1, stg);
+      __syncthreads();
+    }
   }
 
   if constexpr (MODE == 1) {
@@ -281,12 +328,27 @@ __global__ __launch_bounds__(256) void scan_seq_carry_kernel(const ScanParams p,
   }
 }
 
+// B/C as scalar loads: 16 states, unit state stride, every row 4-byte aligned.
+static bool seq_sgpr_bc(const ScanParams& p, int es) {
+  const char* e = getenv("VM_SCAN_SGPR");
+  if (e && atoi(e) == 0) return false;
+  auto ok = [&](const void* ptr, long long sb, long long sn, long long sl) {
+    return sn == 1 && (reinterpret_cast<uintptr_t>(ptr) & 3) == 0 && (sb * es) % 4 == 0 &&
+           (sl * es) % 4 == 0;
+  };
+  return p.dstate == kMaxN && ok(p.B, p.b_sb, p.b_sn, p.b_sl) && ok(p.C, p.c_sb, p.c_sn, p.c_sl);
+}
+
 template <typename T, int MODE, bool SP, bool HZ>
 static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hipStream_t s) {
   const int groups = (p.dim + 63) / 64;
   dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
-  hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ>), grid, dim3(64 * kSeqNW), 0, s,
-                     p, w);
+  if (seq_sgpr_bc(p, sizeof(T)))
+    hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true>), grid, dim3(64 * kSeqNW),
+                       0, s, p, w);
+  else
+    hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, false>), grid,
+                       dim3(64 * kSeqNW), 0, s, p, w);
 }
 
 template <typename T, bool SP, bool HZ>
