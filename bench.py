@@ -244,8 +244,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         print(json.dumps(line), flush=True)
-    if torch.cuda.tunable.is_enabled() and torch.cuda.tunable.tuning_is_enabled():
-        torch.cuda.tunable.write_file()  # VM_GEMM_TUNING=tune: persist new GEMM results
+    # (VM_GEMM_TUNING=tune: TunableOp writes its results file at process exit)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

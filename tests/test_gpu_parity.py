@@ -184,6 +184,30 @@ def test_scan_token_major_full_size_chunked_equals_full(dt, segments, monkeypatc
     assert torch.isfinite(y_full.float()).all()
 
 
+@pytest.mark.parametrize("cpl", ["1", "2"])
+@pytest.mark.parametrize("segments", ["1", "5"])
+@pytest.mark.parametrize("Bz,D,L", [(2, 128, 777), (3, 200, 64), (1, 1152, 3137), (2, 64, 9)])
+def test_scan_token_major_bf16_channel_pairs(Bz, D, L, segments, cpl, monkeypatch):
+    """bf16 token-major scan with B/C as scalar loads: one channel per lane (cpl=1) and the
+    two-adjacent-channels-per-lane kernel (cpl=2, forced), single pass and segmented, vs the
+    oracle on the same bf16 inputs (one bf16 rounding of the output) and vs the
+    channel-major kernel."""
+    monkeypatch.setenv("VM_SCAN_SEGMENTS", segments)
+    monkeypatch.setenv("VM_SCAN_CPL", cpl)
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(Bz, D, L, 16, torch.bfloat16, 7 + L)
+    ref_y, ref_h = orc.selective_scan(u.float(), delta.float(), A, Bm.float(), Cm.float(), Dv,
+                                      z.float(), bias, True, init, True)
+    cm = [t.to(DEV) if t is not None else None for t in (u, delta, A, Bm, Cm, Dv, z, bias, init)]
+    y, h = K.selective_scan_fn(_tm(cm[0]), _tm(cm[1]), cm[2], _tm(cm[3]), _tm(cm[4]), cm[5],
+                               _tm(cm[6]), cm[7], True, True, cm[8])
+    _close(y, ref_y, 2e-2)
+    _close(h, ref_h, 1e-4)
+    y_cm, h_cm = K.selective_scan_fn(*cm[:7], cm[7], True, True, cm[8])
+    rel = ((y.float() - y_cm.float()).norm() / y_cm.float().norm()).item()
+    assert rel < 5e-3, rel
+    assert ((h - h_cm).norm() / h_cm.norm()).item() < 1e-5
+
+
 def test_scan_token_major_inplace_bf16_state():
     u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(2, 16, 50, 16, torch.float32, 3)
     st = init.to(DEV).to(torch.bfloat16)

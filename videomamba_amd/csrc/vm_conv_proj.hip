@@ -67,8 +67,11 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
 // and bias (D) as fp32.
 template <bool DT, int NB>  // DT: also run dt_proj here; NB = e_pad / 16 x_proj blocks
 __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
+  // sU: W_x chunk (<= 128 rows x kCPPad) / x_dbl tile (64 x 2*kCPPad); with DT also the
+  // per-wave dt staging (4 x 64 x kCPPad)
+  constexpr int kSU = DT ? 4 * kCPTok * kCPPad : 2 * kCPTok * kCPPad;
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
-  __shared__ __attribute__((aligned(16))) bf16_t sU[4 * kCPTok * kCPPad];
+  __shared__ __attribute__((aligned(16))) bf16_t sU[kSU];
   extern __shared__ __attribute__((aligned(16))) float sW[];  // [D][4] taps, then [D] bias
   bf16_t* sB = sU;  // W_x chunk: e_pad (<= 128) rows of kCPPad
   const int tid = threadIdx.x;
