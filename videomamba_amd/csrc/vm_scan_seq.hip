@@ -293,7 +293,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 }
 
-// Two adjacent channels per lane (bf16, 16 states, B/C as scalar loads): one 4-byte load
+// Two adjacent channels per lane (bf16, 16 states, B/C as scalar loads; opt-in, see
+// seq_two_channels for the measurement): one 4-byte load
 // or store moves both channels' u / delta / z / y, and the per-step fixed work (B/C unpack
 // on the scalar unit, waits, loop) is shared by two recurrences whose exp / FMA chains
 // interleave.  Same math and segment modes as scan_seq_kernel.
@@ -499,14 +500,13 @@ static bool seq_sgpr_bc(const ScanParams& p, int es) {
   return p.dstate == kMaxN && ok(p.B, p.b_sb, p.b_sn, p.b_sl) && ok(p.C, p.c_sb, p.c_sn, p.c_sl);
 }
 
-// Two channels per lane halves the wave count: only when >= ~1.5 waves per SIMD remain
-// (MI355X: 1024 SIMDs), unless VM_SCAN_CPL forces it (2) or forbids it (1).
+// Two channels per lane: opt-in (VM_SCAN_CPL=2).  Measured on MI355X at D=1152, L=3137,
+// B=224: 4.23 ms vs 2.95 ms for one channel per lane (half the waves, and the doubled
+// per-wave chains did not recover the lost occupancy), so the default stays at one.
 static bool seq_two_channels(const ScanParams& p, int es, int segs) {
+  (void)segs;
   const char* e = getenv("VM_SCAN_CPL");
-  if (e && atoi(e) == 1) return false;
-  const bool forced = e && atoi(e) == 2;
-  const long long waves = static_cast<long long>(p.batch) * ((p.dim + 127) / 128) * segs;
-  return (forced || waves >= 1536) && es == 2 && p.dim % 2 == 0 && seq_sgpr_bc(p, es) &&
+  return e && atoi(e) == 2 && es == 2 && p.dim % 2 == 0 && seq_sgpr_bc(p, es) &&
          (reinterpret_cast<uintptr_t>(p.u) & 3) == 0 && (reinterpret_cast<uintptr_t>(p.delta) & 3) == 0 &&
          (reinterpret_cast<uintptr_t>(p.out) & 3) == 0 &&
          (p.z == nullptr || (reinterpret_cast<uintptr_t>(p.z) & 3) == 0) &&
