@@ -48,7 +48,7 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--batch", type=int, default=336, help="clips per GPU")
     ap.add_argument("--config", default="m16", choices=sorted(CONFIGS))
     ap.add_argument("--p50-chunks", type=int, default=30)
     ap.add_argument("--scan-reps", type=int, default=50)

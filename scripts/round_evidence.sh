@@ -1,14 +1,19 @@
 #!/bin/bash
-# Round evidence: default bench (with cpu baseline), rocprofv3 kernel stats of the same
-# command, and FETCH_SIZE / WRITE_SIZE passes on the scan microbench at the bench shape.
+# Round evidence: the default bench (with CPU baseline), rocprofv3 kernel stats of the same
+# command, kernel stats of the scan microbench alone at the bench shape (the roofline
+# kernel), and FETCH_SIZE / WRITE_SIZE / SQ counter passes on that microbench.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r01}
-mkdir -p gpurun_out/$R
-timeout -k 10 900 python bench.py > gpurun_out/$R/bench.json 2> gpurun_out/$R/bench.err || { echo bench failed; tail gpurun_out/$R/bench.err; exit 1; }
-cat gpurun_out/$R/bench.json
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$R/prof -o bench -- python bench.py --no-cpu-baseline > gpurun_out/$R/prof_bench.log 2>&1 || { echo prof failed; tail gpurun_out/$R/prof_bench.log; exit 1; }
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/$R/pmc_$c -o scan -- python scripts/bench_scan.py --batches ${BATCH:-32} --reps 3 > gpurun_out/$R/pmc_$c.log 2>&1 || { echo pmc $c failed; tail gpurun_out/$R/pmc_$c.log; exit 1; }
+B=${BATCH:-336}
+O=gpurun_out/$R
+mkdir -p $O
+timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --no-cpu-baseline > $O/prof_bench.log 2>&1 || { echo prof failed; tail $O/prof_bench.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_scan -o scan -- python scripts/bench_scan.py --batches $B --reps 20 > $O/prof_scan.log 2>&1 || { echo scan prof failed; tail $O/prof_scan.log; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+  tag=$(echo $c | cut -d' ' -f1)
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$tag -o scan -- python scripts/bench_scan.py --batches $B --reps 3 > $O/pmc_$tag.log 2>&1 || { echo pmc $c failed; tail $O/pmc_$tag.log; exit 1; }
 done
 echo evidence done
