@@ -29,6 +29,8 @@ struct SeqWork {
   int S, seg_len;
 };
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 constexpr int kTS = 32;       // steps per LDS block
 constexpr int kPF = 8;        // u / delta / z prefetch distance in steps
 constexpr int kMaxSeg = 64;   // segments per sequence (carry kernel keeps them in registers)
@@ -71,8 +73,14 @@ __device__ __forceinline__ float raw_f32(uint32_t r) {
 // SB: B_t / C_t (16 states, unit state stride, 4-byte aligned rows) come in as scalar
 // loads — wave-uniform SGPR operands of the VALU ops, one step ahead — instead of the LDS
 // staging + broadcast reads.
-template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB>
+// PK (requires SB): the four per-state VALU ops run as packed-f32 ops over state pairs
+// (v_pk_mul_f32 delta*A and (delta*u)*B, v_pk_fma_f32 for h and y) — B/C pairs are SGPR
+// pairs — leaving the 16 v_exp_f32 unpaired.  Measured in the step mix
+// (tools/probes/pk_rate.hip) a pair costs ~4.7 cycles per packed op against ~3.6 per
+// scalar op in dependent chains, so the step drops from ~343 to ~265 cycles per wave.
+template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB, bool PK>
 __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, const SeqWork w) {
+  static_assert(!PK || SB, "packed pairs take B/C from SGPR pairs");
   static_assert(NW * 64 >= 4 * kTS, "B/C staging needs 4 threads per block step");
   typedef __attribute__((address_space(4))) const uint32_t* cptr;
   constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
@@ -92,16 +100,24 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const int t_end = min(L, t_beg + w.seg_len);
   const long long ws_row = (static_cast<long long>(b) * w.S + seg) * p.dim + d;
 
-  float A2[kMaxN], h[kMaxN];
+  // state pairs (n, n+1) live in f2 register pairs: scalar code addresses .x / .y, the
+  // packed form operates on whole pairs
+  f2 A2[kMaxN / 2], h[kMaxN / 2];
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) {
-    A2[n] = n < N ? p.A[d * N + n] * kLog2e : 0.0f;
+    const float a = n < N ? p.A[d * N + n] * kLog2e : 0.0f;
     float h_init = 0.0f;
     if constexpr (MODE == 0) {
       if (n < N && p.h0) h_init = load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype);
     }
     if constexpr (MODE == 2) h_init = w.hin[ws_row * kMaxN + n];
-    h[n] = h_init;
+    if (n & 1) {
+      A2[n >> 1].y = a;
+      h[n >> 1].y = h_init;
+    } else {
+      A2[n >> 1].x = a;
+      h[n >> 1].x = h_init;
+    }
   }
   const float Dv = p.D ? p.D[d] : 0.0f;
   const float bias = p.dbias ? p.dbias[d] : 0.0f;
@@ -221,6 +237,38 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         if (SP) dl = softplus_fast(dl);
         dl = live ? dl : 0.0f;
         const float du = dl * uu;
+        if constexpr (PK) {
+          const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+          const f2 dl2 = {dl, dl}, du2 = {du, du};
+          f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};  // two pair chains
+#pragma unroll
+          for (int q = 0; q < kMaxN / 2; ++q) {
+            f2 Bp, Cp;
+            if constexpr (sizeof(T) == 2) {
+              Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
+              Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
+            } else {
+              Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
+              Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
+            }
+            const f2 x = dl2 * A2[q];
+            const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+            h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
+            if constexpr (MODE != 1) {
+              if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
+              else ya = __builtin_elementwise_fma(h[q], Cp, ya);
+            }
+          }
+          if constexpr (MODE == 1) {
+            sdel += dl;
+          } else {
+            const f2 ys = ya + yb;
+            float y = ys.x + ys.y;
+            if (HZ) y *= silu_fast(zz);
+            bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+          }
+          continue;
+        }
         float Bv[kMaxN], Cv[kMaxN];
         if constexpr (SB) {
           const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
@@ -250,16 +298,18 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         if constexpr (MODE == 1) {
           sdel += dl;
 #pragma unroll
-          for (int n = 0; n < kMaxN; ++n)
-            h[n] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n]), h[n], du * Bv[n]);
+          for (int q = 0; q < kMaxN / 2; ++q) {
+            h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
+            h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
+          }
         } else {
           float y0 = Dv * uu, y1 = 0.0f;  // two chains: ILP for the 16-term dot product
 #pragma unroll
-          for (int n = 0; n < kMaxN; n += 2) {
-            h[n] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n]), h[n], du * Bv[n]);
-            h[n + 1] = fmaf(__builtin_amdgcn_exp2f(dl * A2[n + 1]), h[n + 1], du * Bv[n + 1]);
-            y0 = fmaf(h[n], Cv[n], y0);
-            y1 = fmaf(h[n + 1], Cv[n + 1], y1);
+          for (int q = 0; q < kMaxN / 2; ++q) {
+            h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
+            h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
+            y0 = fmaf(h[q].x, Cv[2 * q], y0);
+            y1 = fmaf(h[q].y, Cv[2 * q + 1], y1);
           }
           float y = y0 + y1;
           if (HZ) y *= silu_fast(zz);
@@ -278,7 +328,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   if constexpr (MODE == 1) {
     if (active) {
 #pragma unroll
-      for (int n = 0; n < kMaxN; ++n) w.hend[ws_row * kMaxN + n] = h[n];
+      for (int n = 0; n < kMaxN; ++n) w.hend[ws_row * kMaxN + n] = (n & 1) ? h[n >> 1].y : h[n >> 1].x;
       w.sdel[ws_row] = sdel;
     }
   } else {
@@ -286,7 +336,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       if (p.hl) {
 #pragma unroll
         for (int n = 0; n < kMaxN; ++n)
-          if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, h[n]);
+          if (n < N)
+            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, (n & 1) ? h[n >> 1].y : h[n >> 1].x);
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
     }
@@ -500,6 +551,12 @@ static bool seq_sgpr_bc(const ScanParams& p, int es) {
   return p.dstate == kMaxN && ok(p.B, p.b_sb, p.b_sn, p.b_sl) && ok(p.C, p.c_sb, p.c_sn, p.c_sl);
 }
 
+// Packed state pairs (PK) on the SGPR-B/C path; VM_SCAN_PK=0 selects the scalar form.
+static bool seq_packed() {
+  const char* e = getenv("VM_SCAN_PK");
+  return !(e && atoi(e) == 0);
+}
+
 // Two channels per lane: opt-in (VM_SCAN_CPL=2).  Measured on MI355X at D=1152, L=3137,
 // B=224: 4.23 ms vs 2.95 ms for one channel per lane (half the waves, and the doubled
 // per-wave chains did not recover the lost occupancy), so the default stays at one.
@@ -526,12 +583,17 @@ static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hip
   }
   const int groups = (p.dim + 63) / 64;
   dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
-  if (seq_sgpr_bc(p, sizeof(T)))
-    hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true>), grid, dim3(64 * kSeqNW),
-                       0, s, p, w);
-  else
-    hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, false>), grid,
+  if (seq_sgpr_bc(p, sizeof(T))) {
+    if (seq_packed())
+      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true>), grid,
+                         dim3(64 * kSeqNW), 0, s, p, w);
+    else
+      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, false>), grid,
+                         dim3(64 * kSeqNW), 0, s, p, w);
+  } else {
+    hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, false, false>), grid,
                        dim3(64 * kSeqNW), 0, s, p, w);
+  }
 }
 
 template <typename T, bool SP, bool HZ>
