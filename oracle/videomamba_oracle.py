@@ -187,6 +187,82 @@ def mamba_mixer(p: Dict[str, Tensor], prefix: str, hidden: Tensor, *, d_state: i
     return out
 
 
+# ----------------------------------------------------------------------------- block
+def block_forward(p: Dict[str, Tensor], pre: str, h: Tensor, residual: Optional[Tensor], *,
+                  fused: bool, residual_in_fp32: bool, is_rms: bool, eps: float, d_state: int,
+                  d_conv: int, state: Optional[Tuple[Tensor, Tensor]] = None):
+    """``Block.forward`` (``videomamba.py:120-246``): (fused) add + norm, then the mixer
+    (stateful when ``state`` is given).  Returns ``(hidden, residual, new_state|None)``."""
+    nw, nb = p[pre + "norm.weight"], p.get(pre + "norm.bias")
+    C = h.shape[-1]
+    if fused:  # ``:151-166``
+        h, residual = add_norm(h, residual, nw, nb, eps, True, residual_in_fp32, is_rms)
+    else:  # ``:141-150``
+        residual = h if residual is None else residual + h
+        r = residual.to(nw.dtype)
+        if is_rms:
+            h = add_norm(r, None, nw, None, eps, False, False, True)
+        else:
+            h = F.layer_norm(r.float(), (C,), nw.float(),
+                             None if nb is None else nb.float(), eps).to(nw.dtype)
+        if residual_in_fp32:
+            residual = residual.float()
+    if state is not None:
+        h, st = mamba_mixer(p, pre + "mixer.", h, d_state=d_state, d_conv=d_conv, state=state,
+                            return_state=True)
+        return h, residual, st
+    return mamba_mixer(p, pre + "mixer.", h, d_state=d_state, d_conv=d_conv), residual, None
+
+
+def refiner_forward(p: Dict[str, Tensor], x: Tensor, *, state_fwd=None, state_bwd_init=None,
+                    fused: bool = True, residual_in_fp32: bool = True, is_rms: bool = True,
+                    eps: float = 1e-5, d_state: int = 16, d_conv: int = 4):
+    """``BiMambaRefinerBlock.forward`` (``models/refiner_backbone.py:98-135``): forward
+    block on the sequence, backward block on the time-flipped sequence (4-D input: frame
+    order flipped, within-frame order kept, ``:61-68``), sigmoid gate, Linear.  States
+    default to zeros (``:70-79``); only the forward block's new state is returned."""
+    packed = None
+    seq = x
+    if x.ndim == 4:
+        b, t, n, c = x.shape
+        packed = (b, t, n)
+        seq = x.reshape(b, t * n, c)
+    elif x.ndim != 3:
+        raise ValueError("Expected x to be [B, L, C] or [B, T, N, C].")
+
+    def flip(v):
+        if packed is None:
+            return torch.flip(v, dims=[1])
+        b_, t_, n_ = packed
+        return torch.flip(v.reshape(b_, t_, n_, v.shape[-1]), dims=[1]).reshape(b_, t_ * n_, -1)
+
+    dt_ = seq.dtype
+    bsz = seq.shape[0]
+
+    def zeros_state(pre):
+        d_inner = p[pre + "mixer.in_proj.weight"].shape[0] // 2
+        return (torch.zeros(bsz, d_inner, d_conv, dtype=dt_),
+                torch.zeros(bsz, d_inner, d_state, dtype=dt_))
+
+    kw = dict(fused=fused, residual_in_fp32=residual_in_fp32, is_rms=is_rms, eps=eps,
+              d_state=d_state, d_conv=d_conv)
+    st_f = state_fwd if state_fwd is not None else zeros_state("block_fwd.")
+    out_f, _, new_f = block_forward(p, "block_fwd.", seq, None, state=st_f, **kw)
+    st_b = state_bwd_init if state_bwd_init is not None else zeros_state("block_bwd.")
+    out_b_rev, _, _ = block_forward(p, "block_bwd.", flip(seq), None, state=st_b, **kw)
+    out_b = flip(out_b_rev)
+    gin = torch.cat([out_f, out_b], dim=-1).float()
+    lin = (gin @ p["fusion_gate.0.weight"].float().t() + p["fusion_gate.0.bias"].float()).to(dt_)
+    gate = torch.sigmoid(lin.float()).to(dt_)  # nn.Linear then nn.Sigmoid, each in the dtype
+    mix = (gate.float() * out_f.float()).to(dt_).float() + ((1.0 - gate.float()).to(dt_).float()
+                                                             * out_b.float()).to(dt_).float()
+    mix = mix.to(dt_)
+    out = (mix.float() @ p["out_proj.weight"].float().t() + p["out_proj.bias"].float()).to(dt_)
+    if packed is not None:
+        out = out.reshape(*packed, out.shape[-1])
+    return out, new_f
+
+
 # ----------------------------------------------------------------------------- encoder
 def _infer_spatial_grid(token_count: int, ref: Tuple[int, int]) -> Tuple[int, int]:
     """``videomamba.py:32-55``."""
@@ -266,27 +342,12 @@ def encoder_forward(p: Dict[str, Tensor], cfg: dict, x: Tensor, *, mask=None,
     fused = cfg["fused_add_norm"]
     rif = cfg["residual_in_fp32"]
     for i in range(cfg["depth"]):
-        pre = f"layers.{i}."
-        nw, nb = p[pre + "norm.weight"], p.get(pre + "norm.bias")
-        if fused:  # ``:151-166``
-            h, residual = add_norm(h, residual, nw, nb, eps, True, rif, is_rms)
-        else:  # ``:141-150``
-            residual = h if residual is None else residual + h
-            r = residual.to(nw.dtype)
-            if is_rms:
-                hn = add_norm(r, None, nw, None, eps, False, False, True)
-            else:
-                hn = F.layer_norm(r.float(), (C,), nw.float(),
-                                  None if nb is None else nb.float(), eps).to(nw.dtype)
-            h = hn
-            if rif:
-                residual = residual.float()
+        h, residual, st = block_forward(
+            p, f"layers.{i}.", h, residual, fused=fused, residual_in_fp32=rif, is_rms=is_rms,
+            eps=eps, d_state=cfg["d_state"], d_conv=cfg["d_conv"],
+            state=state[i] if state is not None else None)
         if state is not None:
-            h, st = mamba_mixer(p, pre + "mixer.", h, d_state=cfg["d_state"],
-                                d_conv=cfg["d_conv"], state=state[i], return_state=True)
             new_state.append(st)
-        else:
-            h = mamba_mixer(p, pre + "mixer.", h, d_state=cfg["d_state"], d_conv=cfg["d_conv"])
     nw, nb = p["norm.weight"], p.get("norm.bias")
     if fused:  # ``:903-918``
         out = add_norm(h, residual, nw, nb, eps, False, rif, is_rms)

@@ -1,6 +1,6 @@
 """Generate golden fixtures from the REFERENCE model code (run in the dev container).
 
-    python tests/golden/gen_golden.py            # writes tests/golden/*.npz
+    python tests/golden/gen_golden.py [scan|mixer|model|refiner ...]   # writes tests/golden/*.npz
 
 This script imports ``/root/reference/models/videomamba/{mamba_simple,videomamba}.py``
 as-is (read-only, nothing is copied) with ``_standins.py`` registered for the absent
@@ -39,10 +39,11 @@ def _import_reference():
     sys.path.insert(0, REF)
     import models.videomamba.mamba_simple as ms  # noqa: E402
     import models.videomamba.videomamba as vm  # noqa: E402
+    import models.refiner_backbone as rb  # noqa: E402
 
     ms.selective_scan_fn = ms._selective_scan_ref
     ms._SELECTIVE_SCAN_HAS_INITIAL_STATE = True
-    return ms, vm
+    return ms, vm, rb
 
 
 @contextlib.contextmanager
@@ -250,12 +251,58 @@ def gen_model(vm):
     _save("model_cases.npz", out, meta)
 
 
+# --------------------------------------------------------------------------- refiner
+def gen_refiner(rb):
+    """``BiMambaRefinerBlock.forward`` (``models/refiner_backbone.py:98-135``): 3-D and 4-D
+    input (frame-order flip for 4-D), with and without a carried forward state, fused
+    RMSNorm and plain LayerNorm blocks, fp32 and bf16."""
+    out = {}
+    meta = {}
+    cases = [
+        # name, dim, block kwargs, x shape, dtype, carried forward state
+        ("r_3d", 16, dict(), (2, 9, 16), torch.float32, False),
+        ("r_4d_state", 16, dict(), (2, 3, 5, 16), torch.float32, True),
+        ("r_4d_ln", 16, dict(rms_norm=False, fused_add_norm=False, residual_in_fp32=False),
+         (1, 4, 3, 16), torch.float32, True),
+        ("r_4d_bf16", 32, dict(), (1, 4, 6, 32), torch.bfloat16, True),
+    ]
+    for i, (name, dim, kw, shape, dt, carried) in enumerate(cases):
+        torch.manual_seed(4000 + i)
+        blk = rb.BiMambaRefinerBlock(dim, ssm_cfg={"use_fast_path": False}, layer_idx=0,
+                                     **kw).to(dt).eval()
+        x = torch.randn(*shape).to(dt)
+        arrs = dict(x=x)
+        st_f = None
+        if carried:
+            (cs, ss), _ = blk.allocate_state(shape[0], dtype=dt)
+            cs.copy_(0.5 * torch.randn_like(cs.float()).to(dt))
+            ss.copy_(0.5 * torch.randn_like(ss.float()).to(dt))
+            arrs.update(state_fwd_conv=cs.clone(), state_fwd_ssm=ss.clone())
+            st_f = (cs, ss)
+        with torch.no_grad(), _pretend_cuda():
+            y, (nc, nss) = blk(x, state_fwd=st_f)
+        arrs.update(out=y, new_conv=nc, new_ssm=nss)
+        for k, v in blk.state_dict().items():
+            arrs[f"param.{k}"] = v
+        for k, v in arrs.items():
+            out[f"{name}/{k}"] = v
+        meta[name] = dict(dim=dim, block=kw, shape=list(shape), carried=carried,
+                          dtype=str(dt).replace("torch.", ""))
+    _save("refiner_cases.npz", out, meta)
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    ms, vm = _import_reference()
-    gen_scan(ms)
-    gen_mixer(ms)
-    gen_model(vm)
+    ms, vm, rb = _import_reference()
+    only = set(sys.argv[1:])
+    if not only or "scan" in only:
+        gen_scan(ms)
+    if not only or "mixer" in only:
+        gen_mixer(ms)
+    if not only or "model" in only:
+        gen_model(vm)
+    if not only or "refiner" in only:
+        gen_refiner(rb)
 
 
 if __name__ == "__main__":

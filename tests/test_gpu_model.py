@@ -295,6 +295,28 @@ def test_block_return_state_flag_is_respected():
         assert len(block(x, state=state, return_state=True)) == 3
 
 
+REF_, REF_META = load_golden("refiner_cases.npz")
+
+
+@pytest.mark.parametrize("name", sorted(REF_META))
+def test_refiner_matches_reference_fixture(name, layout):
+    """HIP BiMambaRefinerBlock vs the reference's own forward (refiner_backbone.py:98-135)
+    recorded in refiner_cases.npz: 3-D / 4-D (frame-flip) input, carried forward state,
+    fused RMSNorm and LayerNorm blocks; fp32 held at 1e-4, bf16 at 2e-2."""
+    meta = REF_META[name]
+    dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
+    blk = _load(video_mamba.BiMambaRefinerBlock(meta["dim"], layer_idx=0, **meta["block"]),
+                REF_, name, dt)
+    g = lambda k: torch.from_numpy(REF_[f"{name}/{k}"].copy()).to(dt).to(DEV)  # noqa: E731
+    st = (g("state_fwd_conv"), g("state_fwd_ssm")) if meta["carried"] else None
+    with torch.no_grad():
+        out, (nc, ns) = blk(g("x"), state_fwd=st)
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    _close(out, g("out"), tol)
+    _close(nc, g("new_conv"), tol)
+    _close(ns, g("new_ssm"), tol)
+
+
 def test_refiner_block_runs_and_reverses_time():
     blk = video_mamba.BiMambaRefinerBlock(16, layer_idx=0).cuda().eval()
     x = torch.randn(2, 3, 4, 16, device=DEV)
@@ -420,3 +442,35 @@ def test_fused_conv_proj_mixer_bf16_matches_oracle_and_unfused(d_model, L, split
                                      return_state=True)
     _close(c1_0, rc1, 2e-2)
     _close(s1_0, rs1, 5e-2)
+
+
+# ------------------------------------------------------------------ HIP-graph replay
+@pytest.mark.parametrize("pool,add_pool_norm", [("avg", True), ("cls+avg", False)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_graph_replay_matches_eager_streaming(layout, pool, add_pool_norm, dt):
+    """StreamingChunkGraph (videomamba_amd/graphs.py): first chunk (CLS) + continuation
+    chunks replayed from captured graphs equal the eager stateful loop exactly (same
+    kernels), and the carried state matches."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    torch.manual_seed(0)
+    model = _small_model(img_size=32, patch_size=16, depth=3, embed_dim=32, fused_add_norm=True,
+                         rms_norm=True, residual_in_fp32=True, num_frames=8, pool_type=pool,
+                         add_pool_norm=add_pool_norm).to(DEV, dt).eval()
+    x = torch.randn(2, 3, 8, 32, 32, device=DEV).to(dt)
+    chunk = 2
+    runner = StreamingChunkGraph(model, batch=2, frames=chunk, height=32, width=32)
+    state = model.allocate_state(2, dtype=dt, device=DEV)
+    with torch.no_grad():
+        for c in range(4):
+            xc = x[:, :, c * chunk:(c + 1) * chunk]
+            if pool == "cls+avg" and add_pool_norm and c > 0:
+                break
+            eager = model(xc, ssm_state=state, temporal_pos_offset=c * chunk)
+            state = eager[-1]
+            got = runner.run(xc, temporal_pos_offset=c * chunk)
+            got = got if isinstance(got, tuple) else (got,)
+            for a, b in zip(got, eager[:-1]):
+                torch.testing.assert_close(a, b, rtol=0, atol=0)
+            for (c1, s1), (c2, s2) in zip(runner.state, state):
+                torch.testing.assert_close(c1, c2, rtol=0, atol=0)
+                torch.testing.assert_close(s1, s2, rtol=0, atol=0)

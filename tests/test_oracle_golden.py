@@ -137,3 +137,27 @@ def test_oracle_encoder_matches_reference(name):
     chk(xp2, "pool_chunk2_avg")
     if dt == torch.float32:  # test_videomamba_regressions.py:562-588 (tighter)
         torch.testing.assert_close(torch.cat([c1, c2], 1), full, rtol=1e-4, atol=1e-4)
+
+
+REF_, REF_META = load_golden("refiner_cases.npz")
+
+
+@pytest.mark.parametrize("name", sorted(REF_META))
+def test_oracle_refiner_matches_reference(name):
+    """BiMambaRefinerBlock (models/refiner_backbone.py:98-135): 3-D / 4-D input, carried
+    forward state, fused RMSNorm and LayerNorm blocks."""
+    meta = REF_META[name]
+    dt = torch.bfloat16 if meta["dtype"] == "bfloat16" else torch.float32
+    p = {k: v.to(dt) for k, v in orc.params_from_npz(REF_, name + "/").items()}
+    g = lambda k: _t(REF_, f"{name}/{k}", dt)  # noqa: E731
+    blk = meta["block"]
+    st = (g("state_fwd_conv"), g("state_fwd_ssm")) if meta["carried"] else None
+    out, (nc, ns) = orc.refiner_forward(
+        p, g("x"), state_fwd=st, fused=blk.get("fused_add_norm", True),
+        residual_in_fp32=blk.get("residual_in_fp32", True), is_rms=blk.get("rms_norm", True))
+    rtol, atol = _tol(meta["dtype"])
+    chk = lambda a, k: torch.testing.assert_close(  # noqa: E731
+        a.float(), _t(REF_, f"{name}/{k}"), rtol=rtol, atol=atol)
+    chk(out, "out")
+    chk(nc, "new_conv")
+    chk(ns, "new_ssm")

@@ -1,0 +1,120 @@
+"""HIP-graph replay of the stateful streaming chunk (the B=1 latency path).
+
+A streaming chunk of VideoMamba-M issues ~230 kernel launches (patch embed, then per
+layer add+norm, in_proj, conv, x_proj, dt_proj, scan, out_proj, ...).  At B=1 every kernel
+is short, so host launch latency leaves the GPU idle between them (profiles: 5.8 ms wall
+for 4.4 ms of kernels).  ``StreamingChunkGraph`` captures the whole chunk forward once per
+chunk kind (first chunk with CLS, continuation chunk without) into a ``torch.cuda.CUDAGraph``
+(a hipGraph on ROCm) and replays it:
+
+* the clip chunk, the temporal-position slice and the per-layer ``(conv_state, ssm_state)``
+  live in static device buffers owned by the runner;
+* ``run(x, temporal_pos_offset)`` copies the chunk and its temporal-embedding slice into
+  the static buffers (two device copies), replays the graph, and returns the outputs the
+  eager ``model(x, ssm_state=..., temporal_pos_offset=...)`` would return minus the state
+  container — views of static buffers, valid until the next ``run``;
+* the state advances in place (the ssm state is updated in place by the scan as in the
+  eager path; the graph copies each layer's new conv window back into its static buffer),
+  so consecutive ``run`` calls stream exactly like the eager loop with carried state.
+
+Semantics are the eager path's (same kernels, same rounding points); tests check replay
+against eager chunk by chunk.  Masks and keep_temporal pooling are not graph-captured
+(use the eager forward for those).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+__all__ = ["StreamingChunkGraph"]
+
+
+class StreamingChunkGraph:
+    def __init__(self, model, batch: int, frames: int, height: int = 224, width: int = 224,
+                 dtype: Optional[torch.dtype] = None, device=None):
+        self.model = model
+        p = model.patch_embed.proj.weight
+        self.dtype = p.dtype if dtype is None else dtype
+        self.device = p.device if device is None else torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("StreamingChunkGraph requires the model on a HIP device")
+        self.batch, self.frames = batch, frames
+        self.tt = model._validate_temporal_length(frames)
+        self.static_x = torch.zeros(batch, 3, frames, height, width, dtype=self.dtype,
+                                    device=self.device)
+        self.static_tpos = torch.zeros(1, self.tt, model.embed_dim, dtype=self.dtype,
+                                       device=self.device)
+        self._state: List[Tuple[Tensor, Tensor]] = [
+            (c, s) for c, s in model.allocate_state(batch, dtype=self.dtype, device=self.device)]
+        self._graphs: Dict[bool, Tuple[torch.cuda.CUDAGraph, object]] = {}
+        self._pool = None
+
+    # ------------------------------------------------------------------ state
+    @property
+    def state(self) -> List[Tuple[Tensor, Tensor]]:
+        """The carried per-layer (conv_state, ssm_state) — static buffers, updated by run()."""
+        return self._state
+
+    def reset_state(self) -> None:
+        for c, s in self._state:
+            c.zero_()
+            s.zero_()
+
+    def load_state(self, state) -> None:
+        for (c, s), (c2, s2) in zip(self._state, state):
+            c.copy_(c2)
+            s.copy_(s2)
+
+    # ------------------------------------------------------------------ capture / replay
+    def _body(self, has_cls: bool):
+        m = self.model
+        offset = 0 if has_cls else 1  # only has_cls matters inside; tpos comes from the buffer
+        x_vis, new_state = m._forward_features(self.static_x, None, self._state, offset,
+                                               tpos=self.static_tpos)
+        for (c, _), (c_new, _) in zip(self._state, new_state):
+            if c_new.data_ptr() != c.data_ptr():
+                c.copy_(c_new)
+        if not m.add_pool_norm:
+            return (x_vis,)
+        gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
+        return m._pool(self.static_x, x_vis, None, False, has_cls, self.tt, gh * gw)
+
+    def _capture(self, has_cls: bool):
+        saved = [(c.clone(), s.clone()) for c, s in self._state]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
+                self._body(has_cls)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool):
+            outs = self._body(has_cls)
+        self._pool = g.pool()
+        self.load_state(saved)  # warm-up passes advanced the state: restore it
+        self._graphs[has_cls] = (g, outs)
+
+    def run(self, x: Tensor, temporal_pos_offset: int = 0):
+        """One chunk: (x_vis, x_pool) with ``add_pool_norm``, else x_vis — as the eager
+        forward with a full carried state, minus the returned state (see ``state``)."""
+        if tuple(x.shape) != tuple(self.static_x.shape):
+            raise ValueError(f"chunk shape {tuple(x.shape)} != captured "
+                             f"{tuple(self.static_x.shape)}")
+        m = self.model
+        has_cls = temporal_pos_offset <= 0
+        if not has_cls and m.pool_type in {"cls", "cls+avg", "cls_cat_avg"} and m.add_pool_norm:
+            raise ValueError(
+                f"pool_type='{m.pool_type}' requires a CLS token, but continuation streaming "
+                "chunks do not include CLS. Use pool_type='avg' for chunked streaming.")
+        tpos = m._get_temporal_pos_embedding(self.tt, offset=temporal_pos_offset,
+                                             dtype=self.dtype, device=self.device)
+        self.static_tpos.copy_(tpos)
+        self.static_x.copy_(x)
+        if has_cls not in self._graphs:
+            self._capture(has_cls)
+        g, outs = self._graphs[has_cls]
+        g.replay()
+        return outs[0] if len(outs) == 1 else outs

@@ -436,16 +436,19 @@ class PretrainVideoMamba(nn.Module):
         return sums / counts
 
     # ------------------------------------------------------------------ forward
-    def _embed(self, x: Tensor, has_cls: bool, temporal_pos_offset: int):
-        """Patch embed + positional adds (+ CLS row) into a zero-padded (B, Lp, C) buffer."""
+    def _embed(self, x: Tensor, has_cls: bool, temporal_pos_offset: int, tpos=None):
+        """Patch embed + positional adds (+ CLS row) into a zero-padded (B, Lp, C) buffer.
+        ``tpos`` (1, T', C) replaces the temporal-embedding slice (graph replay keeps it in a
+        static buffer that is refilled per chunk)."""
         Bsz, _, T, H, W = x.shape
         k = self.patch_embed.tubelet_size
         P = self.patch_embed.patch_size[0]
         Tt, Gh, Gw = T // k, H // P, W // P
         dt = self.patch_embed.proj.weight.dtype
         spos = self._get_spatial_pos_embedding(Gh, Gw, dtype=dt, device=x.device)
-        tpos = self._get_temporal_pos_embedding(Tt, offset=temporal_pos_offset, dtype=dt,
-                                                device=x.device)
+        if tpos is None:
+            tpos = self._get_temporal_pos_embedding(Tt, offset=temporal_pos_offset, dtype=dt,
+                                                    device=x.device)
         L = Tt * Gh * Gw + (1 if has_cls else 0)
         Lp = round_up(L)
         buf = torch.empty((Bsz, Lp, self.embed_dim), dtype=dt, device=x.device)
@@ -468,9 +471,9 @@ class PretrainVideoMamba(nn.Module):
         with torch.no_grad():
             return self._forward_features(x, mask, ssm_state, temporal_pos_offset)
 
-    def _forward_features(self, x, mask, ssm_state, temporal_pos_offset):
+    def _forward_features(self, x, mask, ssm_state, temporal_pos_offset, tpos=None):
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
-        h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset)
+        h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset, tpos=tpos)
         Bsz = x.shape[0]
         _, visible = self._visible_token_positions(mask, Bsz, L, x.device,
                                                    require_cls_visible=has_cls)
