@@ -474,3 +474,36 @@ def test_graph_replay_matches_eager_streaming(layout, pool, add_pool_norm, dt):
             for (c1, s1), (c2, s2) in zip(runner.state, state):
                 torch.testing.assert_close(c1, c2, rtol=0, atol=0)
                 torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+
+
+# ------------------------------------------------------------------ concurrent batch slices
+@pytest.mark.parametrize("streams", ["2", "3"])
+def test_multistream_batch_slices_match_single_stream(streams, monkeypatch):
+    """VM_BATCH_STREAMS>1 (videomamba.py _layers_multistream): batch slices on concurrent
+    HIP streams give bit-identical features and carried state to the one-stream loop, for
+    the stateless and the full-state streaming paths (token-major forced so the slicing
+    engages at a small model)."""
+    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
+    torch.manual_seed(0)
+    model = _small_model(img_size=32, patch_size=16, depth=3, embed_dim=32, fused_add_norm=True,
+                         rms_norm=True, residual_in_fp32=True, num_frames=4,
+                         add_pool_norm=False).to(DEV, torch.bfloat16).eval()
+    x = torch.randn(5, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        monkeypatch.setenv("VM_BATCH_STREAMS", "1")
+        ref = model(x)
+        st_ref = model.allocate_state(5, dtype=torch.bfloat16, device=DEV)
+        c1_ref, st_ref = model(x[:, :, :2], ssm_state=st_ref)
+        c2_ref, st_ref = model(x[:, :, 2:], ssm_state=st_ref, temporal_pos_offset=2)
+        monkeypatch.setenv("VM_BATCH_STREAMS", streams)
+        assert model._stream_slices(5, None) is not None
+        got = model(x)
+        st = model.allocate_state(5, dtype=torch.bfloat16, device=DEV)
+        c1, st = model(x[:, :, :2], ssm_state=st)
+        c2, st = model(x[:, :, 2:], ssm_state=st, temporal_pos_offset=2)
+    torch.cuda.synchronize()
+    for a, b in ((got, ref), (c1, c1_ref), (c2, c2_ref)):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for (ca, sa), (cb, sb) in zip(st, st_ref):
+        torch.testing.assert_close(ca, cb, rtol=0, atol=0)
+        torch.testing.assert_close(sa, sb, rtol=0, atol=0)

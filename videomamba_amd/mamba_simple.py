@@ -47,6 +47,42 @@ from . import kernels as K
 from .gemm_tuning import enable_tuned_gemms
 from .layers import round_up, warn_if_grad
 
+# Cross-stream GEMM ordering.  When PretrainVideoMamba issues batch slices on concurrent
+# streams (videomamba._layers_multistream) two library GEMMs must never run at the same
+# time: hipBLASLt's stream-K kernels spin on partial-tile flags of their own workgroups
+# (and share the handle's workspace), so two of them co-resident can wait on each other
+# forever (measured: a hang at B=336 with two streams).  While ``serial_gemms`` is on,
+# every token-major GEMM waits for the previously issued GEMM of any other stream; the
+# scan / conv / norm kernels of one slice still overlap the GEMMs of the other.
+_GEMM_ORDER = {"on": 0, "last": None}
+
+
+class serial_gemms:
+    def __enter__(self):
+        _GEMM_ORDER["on"] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _GEMM_ORDER["on"] -= 1
+        if _GEMM_ORDER["on"] == 0:
+            _GEMM_ORDER["last"] = None
+        return False
+
+
+def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
+    if not _GEMM_ORDER["on"]:
+        return F.linear(x, w, b)
+    cur = torch.cuda.current_stream(x.device)
+    last = _GEMM_ORDER["last"]
+    if last is not None and last[0] != cur.cuda_stream:
+        cur.wait_event(last[1])
+    out = F.linear(x, w, b)
+    ev = torch.cuda.Event()
+    ev.record(cur)
+    _GEMM_ORDER["last"] = (cur.cuda_stream, ev)
+    return out
+
+
 _CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP "
                "kernels (libvideomamba_hip, gfx950) are GPU-only.")
 
@@ -219,7 +255,7 @@ class Mamba(nn.Module):
         A, Dv, dbias, cw, cb = self._fp32_params()
         s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
 
-        xz = F.linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
+        xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
         u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
         csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
                  if conv_state_in is not None else (0, 0))
@@ -236,15 +272,15 @@ class Mamba(nn.Module):
         else:
             K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                        u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
-            x_dbl = F.linear(u, self.x_proj.weight)  # (n, R+2N)
-            dt = F.linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
+            x_dbl = _linear(u, self.x_proj.weight)  # (n, R+2N)
+            dt = _linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
         y = torch.empty_like(u)
         K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                    xz[:, Dm:], s_xz, dbias, True,
                    h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
                    h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
                    y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
-        out = F.linear(y, self.out_proj.weight, self.out_proj.bias)  # (n, C)
+        out = _linear(y, self.out_proj.weight, self.out_proj.bias)  # (n, C)
         return out.view(Bsz, Lp, C)
 
     def _check_state(self, t: Tensor, last: int, what: str, batch: int) -> Tensor:
