@@ -134,7 +134,7 @@ def _tm(t):
     return None if t is None else t.transpose(1, 2).contiguous().transpose(1, 2)
 
 
-@pytest.mark.parametrize("segments", ["0", "1", "3", "64"])
+@pytest.mark.parametrize("segments", ["0", "1", "3", "64", "256"])
 @pytest.mark.parametrize("Bz,D,L,N", [(1, 40, 3137, 16),    # ragged channel group
                                       (64, 72, 300, 16),    # many rows
                                       (2, 24, 777, 8), (3, 20, 100, 4), (1, 8, 0, 16),
@@ -154,7 +154,7 @@ def test_scan_token_major_matches_oracle(Bz, D, L, N, segments, monkeypatch):
     _close(h, ref_h, 1e-4)
 
 
-@pytest.mark.parametrize("segments", ["0", "1", "16"])
+@pytest.mark.parametrize("segments", ["0", "1", "16", "256"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_scan_token_major_full_size_chunked_equals_full(dt, segments, monkeypatch):
     """North-star size (D_inner=1152, L=3137), token-major: split scan with the carried

@@ -33,7 +33,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int kTS = 32;       // steps per LDS block
 constexpr int kPF = 8;        // u / delta / z prefetch distance in steps
-constexpr int kMaxSeg = 64;   // segments per sequence (carry kernel keeps them in registers)
+constexpr int kMaxSeg = 256;  // segments per sequence
 constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
 
 // Buffer descriptor over a wave-uniform base: per-step byte offsets go in soffset (SGPR),
@@ -161,7 +161,10 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
     }
   };
 
-  const int nblk = t_end > t_beg ? (t_end - t_beg + kTS - 1) / kTS : 0;
+  // SGPR B/C needs no LDS blocks: step in groups of kPF so a short segment does not run a
+  // whole 32-step block of masked steps
+  constexpr int kBlk = SB ? kPF : kTS;
+  const int nblk = t_end > t_beg ? (t_end - t_beg + kBlk - 1) / kBlk : 0;
   float stg[8];
   if constexpr (!SB) {
     if (nblk > 0) {
@@ -203,13 +206,13 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
 
   float sdel = 0.0f;
   for (int k = 0; k < nblk; ++k) {
-    const int tb = t_beg + k * kTS;
+    const int tb = t_beg + k * kBlk;
     const bool more = k + 1 < nblk;
     if constexpr (!SB) {
       if (more) stage_load(tb + kTS, stg);
     }
     const float* blk = &sbc[k & 1][0][0];
-    for (int g = 0; g < kTS; g += kPF) {
+    for (int g = 0; g < kBlk; g += kPF) {
 #pragma unroll
       for (int j = 0; j < kPF; ++j) {
         const int t = tb + g + j;
@@ -506,7 +509,8 @@ __global__ __launch_bounds__(128) void scan_seq2_kernel(const ScanParams p, cons
 }
 
 // Entry state of every segment: h_in[0] = h0, h_in[s+1] = exp2(A*log2e*sum_delta[s]) *
-// h_in[s] + h_end[s].  One thread per (b, d, n); the S summaries are loaded up front.
+// h_in[s] + h_end[s].  One thread per (b, d, n), sequential over the S segments; the
+// summaries stream through a 16-deep register window so their loads overlap the chain.
 __global__ __launch_bounds__(256) void scan_seq_carry_kernel(const ScanParams p, const SeqWork w) {
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
@@ -521,21 +525,24 @@ __global__ __launch_bounds__(256) void scan_seq_carry_kernel(const ScanParams p,
   const float* __restrict__ sdel = w.sdel;
   const float* __restrict__ hend = w.hend;
   float* __restrict__ hin = w.hin;
-  float sd[kMaxSeg], he[kMaxSeg];
-#pragma unroll
-  for (int s = 0; s < kMaxSeg; ++s) {
-    if (s + 1 < w.S) {
-      const long long row = row0 + s * stride;
-      sd[s] = sdel[row];
-      he[s] = hend[row * kMaxN + n];
-    }
-  }
+  constexpr int kWin = 16;
   float h = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
+  for (int s0 = 0; s0 < w.S; s0 += kWin) {
+    float sd[kWin], he[kWin];
 #pragma unroll
-  for (int s = 0; s < kMaxSeg; ++s) {
-    if (s < w.S) {
-      hin[(row0 + s * stride) * kMaxN + n] = h;
-      if (s + 1 < w.S) h = fmaf(__builtin_amdgcn_exp2f(A2 * sd[s]), h, he[s]);
+    for (int j = 0; j < kWin; ++j) {
+      const int s = s0 + j;
+      const long long row = row0 + (s + 1 < w.S ? s : 0) * stride;
+      sd[j] = sdel[row];
+      he[j] = hend[row * kMaxN + n];
+    }
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) {
+      const int s = s0 + j;
+      if (s < w.S) {
+        hin[(row0 + s * stride) * kMaxN + n] = h;
+        if (s + 1 < w.S) h = fmaf(__builtin_amdgcn_exp2f(A2 * sd[j]), h, he[j]);
+      }
     }
   }
 }
@@ -621,9 +628,12 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
   }
 }
 
-// Segment count: minimise the busiest SIMD's cycles.  Per wave-step ~470 cycles for a
-// wave alone on its SIMD, ~380 per wave when two or more share it (gfx950 issue costs);
-// segmenting costs ~1.8x the work (summary + final pass) plus two launches.
+// Segment count: minimise the busiest SIMD's cycles.  Measured on MI355X (scan_lab,
+// profiles/r01c_scan_lab*.txt, r01c_b1_segments.txt): a wave step costs ~366 issue cycles
+// of its SIMD, and a wave alone on its SIMD still needs ~590 cycles per step (latency-
+// bound), so a wave advances one step every max(590, 366 * waves_per_SIMD) cycles.
+// Segmenting runs every step twice (summary + final pass) and pays ~25 us of fixed
+// start-up per pass plus the carry kernel.
 static int choose_segments(int batch, int dim, int seqlen) {
   if (seqlen < 64) return 1;
   const double groups = (dim + 63) / 64;
@@ -631,12 +641,11 @@ static int choose_segments(int batch, int dim, int seqlen) {
   double best_cost = 0.0;
   for (int S = 1; S <= kMaxSeg; S *= 2) {
     const int seg = (seqlen + S - 1) / S;
-    if (S > 1 && seg < 16) break;
+    if (S > 1 && seg < 8) break;
     const int s_eff = (seqlen + seg - 1) / seg;
-    const double waves = batch * groups * s_eff;
-    const double per_simd = waves / 1024.0 > 1.0 ? waves / 1024.0 : 1.0;
-    const double step = per_simd <= 1.0 ? 470.0 : 380.0 * per_simd;
-    const double cost = step * seg * (s_eff > 1 ? 1.8 : 1.0) + (s_eff > 1 ? 20000.0 : 0.0);
+    const double per_simd = batch * groups * s_eff / 1024.0;
+    const double step = 366.0 * per_simd > 590.0 ? 366.0 * per_simd : 590.0;
+    const double cost = s_eff > 1 ? step * seg * 2.0 + 100000.0 + 40.0 * s_eff : step * seg;
     if (S == 1 || cost < best_cost) {
       best = s_eff;
       best_cost = cost;
