@@ -261,6 +261,115 @@ __global__ __launch_bounds__(64 * NWV) void lab_kernel(const LabP p) {
 }
 
 
+// LDS-DMA staged variant: u / delta / z arrive 8 steps x 64 channels (1 KB) per
+// global_load_lds_dwordx4 into a per-wave ring of R tiles; each step reads its channel
+// with ds_read_u16_d16_hi (the bf16 lands in the high half of a zeroed VGPR = the fp32
+// value, no unpack).  Waits are explicit: vmcnt before a tile's first step (DMA), one
+// lgkmcnt(0) per step (B/C scalar loads + the three LDS reads).
+template <int R>
+__global__ __launch_bounds__(128) void lab_dma_kernel(const LabP p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = blockIdx.x * 2 + wave;
+  const int b = blockIdx.y;
+  const int d0 = g * 64;
+  if (d0 >= p.D) return;
+  const int d = d0 + lane;
+  const int L = p.L;
+  f2 A2[8], h[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    A2[q] = f2{p.A[d * 16 + 2 * q] * kLog2e, p.A[d * 16 + 2 * q + 1] * kLog2e};
+    h[q] = f2{0.0f, 0.0f};
+  }
+  const float Dv = p.Dv[d], bias = p.bias[d];
+  const long long row0 = static_cast<long long>(b) * p.Lp;
+  const bf16* ub = p.u + row0 * p.D + d0;
+  const bf16* db = p.dl + row0 * p.D + d0;
+  const bf16* zb = p.xz + row0 * 2 * p.D + p.D + d0;
+  const auto yr = rsrc(p.y + row0 * p.D + d0);
+  const int us = p.D * 2;
+  const int voff = lane * 2;
+  // wave's LDS ring: [op 0..2][slot 0..R-1][8 steps][64 ch] bf16
+  uint8_t* ring = lds_raw + wave * (3 * R * 1024);
+  const uint32_t ring_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ring));
+  const int lrow = lane >> 3, lcol = (lane & 7) * 8;
+  auto dma = [&](int k) {  // tile k -> slot k % R
+    const int slot = k % R;
+    int r = k * 8 + lrow;
+    r = r < L ? r : L - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(ub + (long long)r * p.D + lcol),
+        (__attribute__((address_space(3))) void*)(ring + (0 * R + slot) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(db + (long long)r * p.D + lcol),
+        (__attribute__((address_space(3))) void*)(ring + (1 * R + slot) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(zb + (long long)r * 2 * p.D + lcol),
+        (__attribute__((address_space(3))) void*)(ring + (2 * R + slot) * 1024), 16, 0, 0);
+  };
+  const uint32_t* bcbase = reinterpret_cast<const uint32_t*>(p.xdbl + row0 * (p.R + 2 * p.N) + p.R);
+  const int bcw = (p.R + 2 * p.N) / 2;
+  uint32_t bcv[2][16];
+  auto bc_load = [&](int t, uint32_t (&dst)[16]) {
+    const cptr bp = (cptr)(bcbase + static_cast<long long>(t) * bcw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dst[i] = bp[i];
+  };
+  const int ntiles = (L + 7) / 8;
+  __builtin_amdgcn_s_waitcnt(0);
+  for (int k = 0; k < R - 1 && k < ntiles; ++k) dma(k);
+  bc_load(0, bcv[0]);
+  uint32_t ru = 0, rd = 0, rz = 0;
+  const uint32_t my = ring_lds + voff;
+  for (int k = 0; k < ntiles; ++k) {
+    if (k + R - 1 < ntiles) dma(k + R - 1);
+    // tile k's DMA is the oldest outstanding group but (R-1) x (3 DMA + 8 stores)
+    if constexpr (R == 2) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+    else if constexpr (R == 3) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(33)" ::: "memory");
+    const uint32_t su = my + ((0 * R + k % R) * 1024), sdl = my + ((1 * R + k % R) * 1024),
+                   sz = my + ((2 * R + k % R) * 1024);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = k * 8 + j;
+      asm volatile("ds_read_u16_d16_hi %0, %1 offset:%2" : "+v"(ru) : "v"(su), "i"(j * 128));
+      asm volatile("ds_read_u16_d16_hi %0, %1 offset:%2" : "+v"(rd) : "v"(sdl), "i"(j * 128));
+      asm volatile("ds_read_u16_d16_hi %0, %1 offset:%2" : "+v"(rz) : "v"(sz), "i"(j * 128));
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this step's B/C + the LDS reads
+      asm volatile("" : "+v"(ru), "+v"(rd), "+v"(rz));  // order the reads' uses after it
+      bc_load(t + 1 < L ? t + 1 : L - 1, bcv[(j + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool live = t < L;
+      const float uu = __uint_as_float(ru), zz = __uint_as_float(rz);
+      float dlv = softplus_fast(__uint_as_float(rd) + bias);
+      dlv = live ? dlv : 0.0f;
+      const float du = dlv * uu;
+      const uint32_t (&cw)[16] = bcv[j & 1];
+      const f2 dl2 = {dlv, dlv}, du2 = {du, du};
+      f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const f2 Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
+        const f2 Cp = f2{__uint_as_float(cw[8 + q] << 16), __uint_as_float(cw[8 + q] & 0xffff0000u)};
+        const f2 x = dl2 * A2[q];
+        const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
+        if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
+        else ya = __builtin_elementwise_fma(h[q], Cp, ya);
+      }
+      const f2 ys = ya + yb;
+      const float y = (ys.x + ys.y) * silu_fast(zz);
+      __builtin_amdgcn_raw_buffer_store_b16(to_bf16(y), yr, live ? voff : kDead, t * us, 0);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  float* hl = p.hl + (static_cast<long long>(b) * p.D + d) * 16;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    hl[2 * q] = h[q].x;
+    hl[2 * q + 1] = h[q].y;
+  }
+}
+
 // Pure streaming reference (no scan math): the scan's u / delta / z reads and y writes at
 // VEC bf16 channels per lane (VEC 1 = the scan's 2-byte lanes; VEC 8 = 16-byte lanes).
 template <int VEC>
@@ -401,14 +510,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double algo = static_cast<double>(B) * D * L * 4 * 2 + 2.0 * B * N * L * 2 + 4.0 * D * N + 8.0 * D;
-  auto bench = [&](const char* name, void (*k)(LabP), bool ref, int nwv = 2) {
+  auto bench = [&](const char* name, void (*k)(LabP), bool ref, int nwv = 2, size_t lds = 0) {
     dim3 grid(nwv == 16 ? (D / 512 + 2) / 2 : (D / 64 + nwv - 1) / nwv, B);
     LabP q = p;
     if (ref) { q.y = y0; q.hl = hl0; }
-    hipLaunchKernelGGL(k, grid, dim3(nwv == 16 ? 128 : 64 * nwv), 0, 0, q);
+    hipLaunchKernelGGL(k, grid, dim3(nwv == 16 ? 128 : 64 * nwv), lds, 0, q);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, grid, dim3(nwv == 16 ? 128 : 64 * nwv), 0, 0, q);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, grid, dim3(nwv == 16 ? 128 : 64 * nwv), lds, 0, q);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -444,8 +553,10 @@ int main(int argc, char** argv) {
   bench("ref scalar bf16-BC (baseline)", lab_kernel<false, false, false, true, true>, true);
   for (int rep = 0; rep < 2; ++rep) {
     bench("pk pf8", lab_kernel<true, false, false, true, true>, false);
-    bench("pk pf8 no vmem", lab_kernel<true, false, true, true, true, 2>, false);
-    bench("pk pf8 u/dl/z stand-ins (B/C loads kept)", lab_kernel<true, false, true, true, true, 1>, false);
+    bench("pk voff pf8", lab_kernel<true, false, true, true, true>, false);
+    bench("dma R=2", lab_dma_kernel<2>, false, 2, 2 * 3 * 2 * 1024);
+    bench("dma R=3", lab_dma_kernel<3>, false, 2, 2 * 3 * 3 * 1024);
+    bench("dma R=4", lab_dma_kernel<4>, false, 2, 2 * 3 * 4 * 1024);
   }
   return 0;
 }
