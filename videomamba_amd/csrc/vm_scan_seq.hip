@@ -78,7 +78,7 @@ __device__ __forceinline__ float raw_f32(uint32_t r) {
 // pairs — leaving the 16 v_exp_f32 unpaired.  Measured in the step mix
 // (tools/probes/pk_rate.hip) a pair costs ~4.7 cycles per packed op against ~3.6 per
 // scalar op in dependent chains, so the step drops from ~343 to ~265 cycles per wave.
-template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB, bool PK>
+template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB, bool PK, bool BC1 = false>
 __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, const SeqWork w) {
   static_assert(!PK || SB, "packed pairs take B/C from SGPR pairs");
   static_assert(NW * 64 >= 4 * kTS, "B/C staging needs 4 threads per block step");
@@ -176,13 +176,23 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const T* Bq = static_cast<const T*>(p.B) + b * p.b_sb;
   const T* Cq = static_cast<const T*>(p.C) + b * p.c_sb;
   uint32_t bcw[2][2 * NWD];  // [step parity][B words | C words]
+  // byte offsets of a step's B / C rows within this batch row fit 32 bits (host checks),
+  // so a step costs one scalar multiply; BC1: C directly follows B in the same row
+  // (the mixer's x_dbl layout) and both arrive in one s_load_dwordx16
+  const uint32_t bsl = static_cast<uint32_t>(p.b_sl * sizeof(T));
+  const uint32_t csl = static_cast<uint32_t>(p.c_sl * sizeof(T));
   auto bc_load = [&](int t, uint32_t (&dst)[2 * NWD]) {
-    const cptr bp = (cptr)(Bq + static_cast<long long>(t) * p.b_sl);  // generic -> constant AS
-    const cptr cp = (cptr)(Cq + static_cast<long long>(t) * p.c_sl);
+    const cptr bp = (cptr)(reinterpret_cast<const char*>(Bq) + static_cast<uint32_t>(t) * bsl);
+    if constexpr (BC1) {
 #pragma unroll
-    for (int i = 0; i < NWD; ++i) {
-      dst[i] = bp[i];
-      if constexpr (MODE != 1) dst[NWD + i] = cp[i];
+      for (int i = 0; i < 2 * NWD; ++i) dst[i] = bp[i];
+    } else {
+      const cptr cp = (cptr)(reinterpret_cast<const char*>(Cq) + static_cast<uint32_t>(t) * csl);
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) {
+        dst[i] = bp[i];
+        if constexpr (MODE != 1) dst[NWD + i] = cp[i];
+      }
     }
   };
 
@@ -205,121 +215,152 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 
   float sdel = 0.0f;
-  for (int k = 0; k < nblk; ++k) {
-    const int tb = t_beg + k * kBlk;
-    const bool more = k + 1 < nblk;
-    if constexpr (!SB) {
-      if (more) stage_load(tb + kTS, stg);
-    }
-    const float* blk = &sbc[k & 1][0][0];
-    for (int g = 0; g < kBlk; g += kPF) {
+  // One step of the recurrence (step t, prefetch slot j): consume the registers loaded
+  // kPF steps ago and refill the slot at the given (per-lane voffset, SGPR soffset) pairs.
+  const float* blk = &sbc[0][0][0];
+  int tb_lds = t_beg;  // first step of the LDS block `blk` holds (non-SB path)
+  auto step = [&](const int t, const int j, const bool live, const int vu, const int su,
+                  const int vd, const int sd, const int vz, const int sz) {
+      const float uu = raw_f32<T>(ru[j]);
+      const float dr = raw_f32<T>(rd[j]);
+      const float zz = raw_f32<T>(rz[j]);
+      ru[j] = bload<T>(ur, vu, su);
+      rd[j] = bload<T>(dr_, vd, sd);
+      if (HZ && MODE != 1) rz[j] = bload<T>(zr, vz, sz);
+      if constexpr (SB) {
+        // this step's B/C rows (issued one step ago) have landed — explicit lgkmcnt(0),
+        // scalar loads return out of order — then fetch the next step's rows
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        bc_load(t + 1 < tlast ? t + 1 : tlast, bcw[(j + 1) & 1]);
+      }
+      // keep each step's refill loads at the step head: the scheduler would otherwise
+      // sink them below all eight steps, collapsing the prefetch distance to zero
+      // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
+      __builtin_amdgcn_sched_barrier(0);
+      float dl = dr + bias;
+      if (SP) dl = softplus_fast(dl);
+      dl = live ? dl : 0.0f;
+      const float du = dl * uu;
+      if constexpr (PK) {
+        const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+        const f2 dl2 = {dl, dl}, du2 = {du, du};
+        f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};  // two pair chains
 #pragma unroll
-      for (int j = 0; j < kPF; ++j) {
-        const int t = tb + g + j;
-        const float uu = raw_f32<T>(ru[j]);
-        const float dr = raw_f32<T>(rd[j]);
-        const float zz = raw_f32<T>(rz[j]);
-        {
-          const int tn = min(t + kPF, tlast);
-          ru[j] = bload<T>(ur, voff, tn * us);
-          rd[j] = bload<T>(dr_, voff, tn * ds);
-          if (HZ && MODE != 1) rz[j] = bload<T>(zr, voff, tn * zs);
-        }
-        if constexpr (SB) {
-          // this step's B/C rows (issued one step ago) have landed — explicit lgkmcnt(0),
-          // scalar loads return out of order — then fetch the next step's rows
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-          bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
-        }
-        // keep each step's refill loads at the step head: the scheduler would otherwise
-        // sink them below all eight steps, collapsing the prefetch distance to zero
-        // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
-        __builtin_amdgcn_sched_barrier(0);
-        const bool live = t < t_end;
-        float dl = dr + bias;
-        if (SP) dl = softplus_fast(dl);
-        dl = live ? dl : 0.0f;
-        const float du = dl * uu;
-        if constexpr (PK) {
-          const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
-          const f2 dl2 = {dl, dl}, du2 = {du, du};
-          f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};  // two pair chains
-#pragma unroll
-          for (int q = 0; q < kMaxN / 2; ++q) {
-            f2 Bp, Cp;
-            if constexpr (sizeof(T) == 2) {
-              Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
-              Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
-            } else {
-              Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
-              Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
-            }
-            const f2 x = dl2 * A2[q];
-            const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-            h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
-            if constexpr (MODE != 1) {
-              if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
-              else ya = __builtin_elementwise_fma(h[q], Cp, ya);
-            }
-          }
-          if constexpr (MODE == 1) {
-            sdel += dl;
+        for (int q = 0; q < kMaxN / 2; ++q) {
+          f2 Bp, Cp;
+          if constexpr (sizeof(T) == 2) {
+            Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
+            Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
           } else {
-            const f2 ys = ya + yb;
-            float y = ys.x + ys.y;
-            if (HZ) y *= silu_fast(zz);
-            bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+            Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
+            Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
           }
-          continue;
-        }
-        float Bv[kMaxN], Cv[kMaxN];
-        if constexpr (SB) {
-          const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
-#pragma unroll
-          for (int n = 0; n < kMaxN; ++n) {
-            if constexpr (sizeof(T) == 2) {
-              const uint32_t wb = cw[n >> 1], wc = cw[NWD + (n >> 1)];
-              Bv[n] = __uint_as_float((n & 1) ? (wb & 0xffff0000u) : (wb << 16));
-              Cv[n] = __uint_as_float((n & 1) ? (wc & 0xffff0000u) : (wc << 16));
-            } else {
-              Bv[n] = __uint_as_float(cw[n]);
-              Cv[n] = __uint_as_float(cw[NWD + n]);
-            }
-          }
-        } else {
-          const float4* row = reinterpret_cast<const float4*>(blk + (g + j) * 2 * kMaxN);
-#pragma unroll
-          for (int q = 0; q < kMaxN / 4; ++q) {
-            const float4 bq = row[q];
-            Bv[4 * q] = bq.x; Bv[4 * q + 1] = bq.y; Bv[4 * q + 2] = bq.z; Bv[4 * q + 3] = bq.w;
-            if constexpr (MODE != 1) {
-              const float4 cq = row[kMaxN / 4 + q];
-              Cv[4 * q] = cq.x; Cv[4 * q + 1] = cq.y; Cv[4 * q + 2] = cq.z; Cv[4 * q + 3] = cq.w;
-            }
+          const f2 x = dl2 * A2[q];
+          const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
+          if constexpr (MODE != 1) {
+            if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
+            else ya = __builtin_elementwise_fma(h[q], Cp, ya);
           }
         }
         if constexpr (MODE == 1) {
           sdel += dl;
-#pragma unroll
-          for (int q = 0; q < kMaxN / 2; ++q) {
-            h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
-            h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
-          }
         } else {
-          float y0 = Dv * uu, y1 = 0.0f;  // two chains: ILP for the 16-term dot product
-#pragma unroll
-          for (int q = 0; q < kMaxN / 2; ++q) {
-            h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
-            h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
-            y0 = fmaf(h[q].x, Cv[2 * q], y0);
-            y1 = fmaf(h[q].y, Cv[2 * q + 1], y1);
-          }
-          float y = y0 + y1;
+          const f2 ys = ya + yb;
+          float y = ys.x + ys.y;
           if (HZ) y *= silu_fast(zz);
-          // unconditional store (a branch here makes the loop-carried vmcnt accounting
-          // conservative): dead lanes / steps get an out-of-range voffset instead
           bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
         }
+        return;
+      }
+      float Bv[kMaxN], Cv[kMaxN];
+      if constexpr (SB) {
+        const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+#pragma unroll
+        for (int n = 0; n < kMaxN; ++n) {
+          if constexpr (sizeof(T) == 2) {
+            const uint32_t wb = cw[n >> 1], wc = cw[NWD + (n >> 1)];
+            Bv[n] = __uint_as_float((n & 1) ? (wb & 0xffff0000u) : (wb << 16));
+            Cv[n] = __uint_as_float((n & 1) ? (wc & 0xffff0000u) : (wc << 16));
+          } else {
+            Bv[n] = __uint_as_float(cw[n]);
+            Cv[n] = __uint_as_float(cw[NWD + n]);
+          }
+        }
+      } else {
+        const float4* row = reinterpret_cast<const float4*>(blk + (t - tb_lds) * 2 * kMaxN);
+#pragma unroll
+        for (int q = 0; q < kMaxN / 4; ++q) {
+          const float4 bq = row[q];
+          Bv[4 * q] = bq.x; Bv[4 * q + 1] = bq.y; Bv[4 * q + 2] = bq.z; Bv[4 * q + 3] = bq.w;
+          if constexpr (MODE != 1) {
+            const float4 cq = row[kMaxN / 4 + q];
+            Cv[4 * q] = cq.x; Cv[4 * q + 1] = cq.y; Cv[4 * q + 2] = cq.z; Cv[4 * q + 3] = cq.w;
+          }
+        }
+      }
+      if constexpr (MODE == 1) {
+        sdel += dl;
+#pragma unroll
+        for (int q = 0; q < kMaxN / 2; ++q) {
+          h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
+          h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
+        }
+      } else {
+        float y0 = Dv * uu, y1 = 0.0f;  // two chains: ILP for the 16-term dot product
+#pragma unroll
+        for (int q = 0; q < kMaxN / 2; ++q) {
+          h[q].x = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].x), h[q].x, du * Bv[2 * q]);
+          h[q].y = fmaf(__builtin_amdgcn_exp2f(dl * A2[q].y), h[q].y, du * Bv[2 * q + 1]);
+          y0 = fmaf(h[q].x, Cv[2 * q], y0);
+          y1 = fmaf(h[q].y, Cv[2 * q + 1], y1);
+        }
+        float y = y0 + y1;
+        if (HZ) y *= silu_fast(zz);
+        // unconditional store (a branch here makes the loop-carried vmcnt accounting
+        // conservative): dead lanes / steps get an out-of-range voffset instead
+        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+      }
+  };
+
+  int k0 = 0;
+  if constexpr (SB) {
+    // Main loop: whole 8-step groups that are all live and whose refills (kPF steps
+    // ahead) stay inside the sequence — per-lane step offsets in VGPRs, one SGPR base per
+    // group, no clamps.  Measured ~5 % faster than the clamped form (scan_lab "voff").
+    // (u and delta share their step stride here — the mixer's layout — so one offset
+    // table serves both and the kernel stays at <= 96 VGPRs)
+    int vou[kPF], voz[kPF];
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) {
+      vou[j] = voff + j * us;
+      voz[j] = voff + j * zs;
+    }
+    int t0 = t_beg;
+    if (ds == us) {
+      for (; t0 + kPF <= t_end && t0 + 2 * kPF <= L; t0 += kPF) {
+        const int su = (t0 + kPF) * us, sz = (t0 + kPF) * zs;
+#pragma unroll
+        for (int j = 0; j < kPF; ++j) step(t0 + j, j, true, vou[j], su, vou[j], su, voz[j], sz);
+      }
+    }
+    k0 = (t0 - t_beg) / kBlk;
+  }
+  // Clamped steps: the tail (SGPR path) or every block (LDS path).
+  for (int k = k0; k < nblk; ++k) {
+    const int tb = t_beg + k * kBlk;
+    const bool more = k + 1 < nblk;
+    if constexpr (!SB) {
+      if (more) stage_load(tb + kTS, stg);
+      blk = &sbc[k & 1][0][0];
+      tb_lds = tb;
+    }
+    for (int g = 0; g < kBlk; g += kPF) {
+#pragma unroll
+      for (int j = 0; j < kPF; ++j) {
+        const int t = tb + g + j;
+        const int tn = min(t + kPF, tlast);
+        step(t, j, t < t_end, voff, tn * us, voff, tn * ds, voff, tn * zs);
       }
     }
     if constexpr (!SB) {
@@ -327,7 +368,6 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       __syncthreads();
     }
   }
-
   if constexpr (MODE == 1) {
     if (active) {
 #pragma unroll
@@ -555,7 +595,9 @@ static bool seq_sgpr_bc(const ScanParams& p, int es) {
     return sn == 1 && (reinterpret_cast<uintptr_t>(ptr) & 3) == 0 && (sb * es) % 4 == 0 &&
            (sl * es) % 4 == 0;
   };
-  return p.dstate == kMaxN && ok(p.B, p.b_sb, p.b_sn, p.b_sl) && ok(p.C, p.c_sb, p.c_sn, p.c_sl);
+  const long long span = static_cast<long long>(p.seqlen > 0 ? p.seqlen : 1) * es;
+  return p.dstate == kMaxN && ok(p.B, p.b_sb, p.b_sn, p.b_sl) && ok(p.C, p.c_sb, p.c_sn, p.c_sl) &&
+         span * p.b_sl < (1ll << 31) && span * p.c_sl < (1ll << 31);
 }
 
 // Packed state pairs (PK) on the SGPR-B/C path; VM_SCAN_PK=0 selects the scalar form.
@@ -591,7 +633,12 @@ static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hip
   const int groups = (p.dim + 63) / 64;
   dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
   if (seq_sgpr_bc(p, sizeof(T))) {
-    if (seq_packed())
+    const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
+                     static_cast<const T*>(p.C) == static_cast<const T*>(p.B) + kMaxN;
+    if (seq_packed() && bc1)
+      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true, true>), grid,
+                         dim3(64 * kSeqNW), 0, s, p, w);
+    else if (seq_packed())
       hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true>), grid,
                          dim3(64 * kSeqNW), 0, s, p, w);
     else
