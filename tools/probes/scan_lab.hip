@@ -47,7 +47,7 @@ __device__ __forceinline__ uint16_t to_bf16(float v) {
 }
 
 template <bool PK, bool BC32, bool VOFF, bool SP, bool HZ, int MEM = 0, int kPF = 8, int NWV = 2, int LAY = 0>
-__global__ __launch_bounds__(64 * NWV) void lab_kernel(const LabP p) {
+__global__ __launch_bounds__(64 * NWV) LAB_ATTR void lab_kernel(const LabP p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = blockIdx.x * NWV + wave;
@@ -102,6 +102,7 @@ __global__ __launch_bounds__(64 * NWV) void lab_kernel(const LabP p) {
     ru[j] = __builtin_amdgcn_raw_buffer_load_b16(ur, voff, t * us, 0);
     rd[j] = __builtin_amdgcn_raw_buffer_load_b16(dr, voff, t * us, 0);
     rz[j] = HZ ? __builtin_amdgcn_raw_buffer_load_b16(zr, voff, t * zs, 0) : 0u;
+    __builtin_amdgcn_sched_barrier(0);  // same (u, delta, z) per-step order as the loop
   }
   bc_load(0, bcv[0]);
 
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(64 * NWV) void lab_kernel(const LabP p) {
         const float uu = __uint_as_float(ru[j] << 16);
         const float dr_ = __uint_as_float(rd[j] << 16);
         const float zz = __uint_as_float(rz[j] << 16);
-        if constexpr (MEM == 0 || MEM == 3) {
+        if constexpr (MEM == 0 || MEM == 3 || MEM == 5) {
           ru[j] = __builtin_amdgcn_raw_buffer_load_b16(ur, vo[j], su, 0);
           rd[j] = __builtin_amdgcn_raw_buffer_load_b16(dr, vo[j], su, 0);
           if (HZ) rz[j] = __builtin_amdgcn_raw_buffer_load_b16(zr, vz[j], sz, 0);
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(64 * NWV) void lab_kernel(const LabP p) {
           y = y0 + y1;
         }
         if (HZ) y *= silu_fast(zz);
-        if (MEM < 2 || y == 12345.0f) __builtin_amdgcn_raw_buffer_store_b16(to_bf16(y), yr, vo[j], t0 * us, 0);
+        if ((MEM < 2 || MEM == 3) || y == 12345.0f) __builtin_amdgcn_raw_buffer_store_b16(to_bf16(y), yr, vo[j], t0 * us, 0);
       }
     }
   }
@@ -552,11 +553,9 @@ int main(int argc, char** argv) {
   };
   bench("ref scalar bf16-BC (baseline)", lab_kernel<false, false, false, true, true>, true);
   for (int rep = 0; rep < 2; ++rep) {
-    bench("pk pf8", lab_kernel<true, false, false, true, true>, false);
-    bench("pk voff pf8", lab_kernel<true, false, true, true, true>, false);
-    bench("dma R=2", lab_dma_kernel<2>, false, 2, 2 * 3 * 2 * 1024);
-    bench("dma R=3", lab_dma_kernel<3>, false, 2, 2 * 3 * 3 * 1024);
-    bench("dma R=4", lab_dma_kernel<4>, false, 2, 2 * 3 * 4 * 1024);
+    bench("pk voff pf8 (ordered prologue)", lab_kernel<true, false, true, true, true>, false);
+    bench("pk pf8 (ordered prologue)", lab_kernel<true, false, false, true, true>, false);
+    bench("pk voff pf8 no vmem", lab_kernel<true, false, true, true, true, 2>, false);
   }
   return 0;
 }

@@ -211,6 +211,10 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       ru[j] = bload<T>(ur, voff, t * us);
       rd[j] = bload<T>(dr_, voff, t * ds);
       rz[j] = HZ && MODE != 1 ? bload<T>(zr, voff, t * zs) : 0u;
+      // keep the loop's per-step (u, delta, z) issue order: a prologue the scheduler
+      // regroups (all u, then all delta, ...) makes the compiler's loop-header vmcnt waits
+      // 8 / 16 loads tighter than the steady state needs
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -219,8 +223,9 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   // kPF steps ago and refill the slot at the given (per-lane voffset, SGPR soffset) pairs.
   const float* blk = &sbc[0][0][0];
   int tb_lds = t_beg;  // first step of the LDS block `blk` holds (non-SB path)
-  auto step = [&](const int t, const int j, const bool live, const int vu, const int su,
-                  const int vd, const int sd, const int vz, const int sz) {
+  auto step = [&](uint32_t (&ru)[kPF], uint32_t (&rd)[kPF], uint32_t (&rz)[kPF], const int t,
+                  const int j, const bool live, const int vu, const int su, const int vd,
+                  const int sd, const int vz, const int sz) {
       const float uu = raw_f32<T>(ru[j]);
       const float dr = raw_f32<T>(rd[j]);
       const float zz = raw_f32<T>(rz[j]);
@@ -341,12 +346,36 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       for (; t0 + kPF <= t_end && t0 + 2 * kPF <= L; t0 += kPF) {
         const int su = (t0 + kPF) * us, sz = (t0 + kPF) * zs;
 #pragma unroll
-        for (int j = 0; j < kPF; ++j) step(t0 + j, j, true, vou[j], su, vou[j], su, voz[j], sz);
+        for (int j = 0; j < kPF; ++j)
+          step(ru, rd, rz, t0 + j, j, true, vou[j], su, vou[j], su, voz[j], sz);
       }
     }
-    k0 = (t0 - t_beg) / kBlk;
+    // Tail (SGPR path): clamped steps on registers of their own.  Re-issuing the tail's
+    // prefetch (instead of continuing on the main loop's registers) keeps the main loop's
+    // prefetch registers loop-local: carried into a second loop they made the register
+    // allocator shuffle in-flight load destinations at the loop head (v_mov + vmcnt(0)).
+    if (t0 < t_end) {
+      uint32_t tu[kPF], td[kPF], tz[kPF];
+#pragma unroll
+      for (int j = 0; j < kPF; ++j) {
+        const int t = min(t0 + j, tlast);
+        tu[j] = bload<T>(ur, voff, t * us);
+        td[j] = bload<T>(dr_, voff, t * ds);
+        tz[j] = HZ && MODE != 1 ? bload<T>(zr, voff, t * zs) : 0u;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      for (int tb = t0; tb < t_end; tb += kPF) {
+#pragma unroll
+        for (int j = 0; j < kPF; ++j) {
+          const int t = tb + j;
+          const int tn = min(t + kPF, tlast);
+          step(tu, td, tz, t, j, t < t_end, voff, tn * us, voff, tn * ds, voff, tn * zs);
+        }
+      }
+    }
+    k0 = nblk;
   }
-  // Clamped steps: the tail (SGPR path) or every block (LDS path).
+  // LDS path: clamped blocks.
   for (int k = k0; k < nblk; ++k) {
     const int tb = t_beg + k * kBlk;
     const bool more = k + 1 < nblk;
@@ -360,7 +389,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       for (int j = 0; j < kPF; ++j) {
         const int t = tb + g + j;
         const int tn = min(t + kPF, tlast);
-        step(t, j, t < t_end, voff, tn * us, voff, tn * ds, voff, tn * zs);
+        step(ru, rd, rz, t, j, t < t_end, voff, tn * us, voff, tn * ds, voff, tn * zs);
       }
     }
     if constexpr (!SB) {
