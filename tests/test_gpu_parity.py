@@ -208,6 +208,44 @@ def test_scan_token_major_bf16_channel_pairs(Bz, D, L, segments, cpl, monkeypatc
     assert ((h - h_cm).norm() / h_cm.norm()).item() < 1e-5
 
 
+@pytest.mark.parametrize("segments", ["0", "4"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Bz,D,L", [(2, 128, 1501), (1, 192, 3137), (3, 64, 13)])
+def test_scan_mixer_layout_matches_oracle(Bz, D, L, dt, segments, monkeypatch):
+    """The token-major mixer's exact operand layout (mamba_simple._forward_padded_tm):
+    u / delta / y rows (B*Lp, D) with Lp = round_up(L, 8) and zeroed padding rows, z the
+    second half of xz rows (B*Lp, 2D), B and C adjacent columns of one x_dbl row
+    (B*Lp, R + 2N) — the one-scalar-load B/C form — and an in-place stateful h.  Covers the
+    unclamped main loop, the clamped tail and the padded-row zeroing, vs the oracle."""
+    monkeypatch.setenv("VM_SCAN_SEGMENTS", segments)
+    N, R = 16, 8
+    E = R + 2 * N
+    Lp = (L + 7) // 8 * 8
+    n = Bz * Lp
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(Bz, D, L, N, dt, 31 + L)
+    ref_y, ref_h = orc.selective_scan(u.float(), delta.float(), A, Bm.float(), Cm.float(), Dv,
+                                      z.float(), bias, True, init, True)
+    rows = lambda t: t.transpose(1, 2)  # noqa: E731  (b, d, l) -> (b, l, d)
+    U = torch.zeros(Bz, Lp, D, dtype=dt)
+    DL = torch.zeros(Bz, Lp, D, dtype=dt)
+    XZ = torch.zeros(Bz, Lp, 2 * D, dtype=dt)
+    XD = torch.zeros(Bz, Lp, E, dtype=dt)
+    U[:, :L], DL[:, :L], XZ[:, :L, D:] = rows(u), rows(delta), rows(z)
+    XD[:, :L, R:R + N], XD[:, :L, R + N:] = rows(Bm), rows(Cm)
+    U, DL, XZ, XD = (t.reshape(n, -1).to(DEV) for t in (U, DL, XZ, XD))
+    y = torch.full((n, D), 7.0, dtype=dt, device=DEV)  # padding rows must come back 0
+    h = init.to(DEV).contiguous()
+    s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * E, 1, E)
+    K.scan_raw(U, s_u, DL, s_u, A.to(DEV).contiguous(), XD[:, R:R + N], s_bc, XD[:, R + N:],
+               s_bc, Dv.to(DEV), XZ[:, D:], s_z, bias.to(DEV), True, h, (D * N, N), h,
+               (D * N, N), y, s_u, Lp, Bz, D, L, N, K.dtype_code(dt),
+               torch.cuda.current_stream().cuda_stream)
+    y = y.view(Bz, Lp, D)
+    _close(y[:, :L].transpose(1, 2), ref_y, 1e-4 if dt == torch.float32 else 2e-2)
+    assert not y[:, L:].float().abs().any()
+    _close(h, ref_h, 1e-4)
+
+
 def test_scan_token_major_inplace_bf16_state():
     u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(2, 16, 50, 16, torch.float32, 3)
     st = init.to(DEV).to(torch.bfloat16)
