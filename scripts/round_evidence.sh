@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round evidence: the default bench (with CPU baseline), rocprofv3 kernel stats of the same
 # command, kernel stats of the scan microbench alone at the bench shape (the roofline
-# kernel), and FETCH_SIZE / WRITE_SIZE / SQ counter passes on that microbench.
+# kernel), FETCH_SIZE / WRITE_SIZE / SQ counter passes on that microbench, the same
+# FETCH/WRITE passes on a calibration kernel with the scan's access pattern and a known byte
+# count (tools/probes/scan_lab calib), and the C5 long-video run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r01}
@@ -16,4 +18,9 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VA
   tag=$(echo $c | cut -d' ' -f1)
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$tag -o scan -- python scripts/bench_scan.py --batches $B --reps 3 > $O/pmc_$tag.log 2>&1 || { echo pmc $c failed; tail $O/pmc_$tag.log; exit 1; }
 done
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/calib_$c -o calib -- ./tools/probes/scan_lab $B 2 3137 calib > $O/calib_$c.log 2>&1 || { echo calib $c failed; tail $O/calib_$c.log; exit 1; }
+done
+timeout -k 10 600 python scripts/bench_long_video.py > $O/long_video.json 2> $O/long_video.err || { echo long video failed; tail $O/long_video.err; exit 1; }
+cat $O/long_video.json
 echo evidence done

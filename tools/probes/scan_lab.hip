@@ -15,6 +15,10 @@
 
 #include <vector>
 
+#ifndef LAB_ATTR
+#define LAB_ATTR
+#endif
+
 typedef uint16_t bf16;
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(4))) const uint32_t* cptr;
@@ -551,6 +555,13 @@ int main(int argc, char** argv) {
     printf("%-34s B=%d %9.1f us  %6.2f us/clip-layer  %6.1f GB/s  frac %.4f  maxdiff y %.2e h %.2e\n",
            name, B, us, us / B, algo / (us * 1e-6) / 1e9, algo / (us * 1e-6) / 8e12, maxdiff, maxh);
   };
+  if (argc > 4 && strcmp(argv[4], "calib") == 0) {
+    // PMC calibration run: the scan's access pattern (2-byte lanes, one 128-B row segment
+    // per wave per operand and step) with a known byte count and no scan math
+    bench("stream only, 2 B/lane (calibration)", stream_kernel<1>, false);
+    printf("calibration bytes per launch: read %.0f write %.0f\n", 3.0 * rows * D * 2, 1.0 * rows * D * 2);
+    return 0;
+  }
   bench("ref scalar bf16-BC (baseline)", lab_kernel<false, false, false, true, true>, true);
   for (int rep = 0; rep < 2; ++rep) {
     bench("pk voff pf8 (ordered prologue)", lab_kernel<true, false, true, true, true>, false);
