@@ -37,6 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # wave64 instruction per SIMD.  The scan's irreducible work per (element, state) is one
 # v_exp_f32 plus four fp32 mul/fma (delta*A, (delta*u)*B, h update, y += h*C).
 CYC_EXP, CYC_FMA, SIMDS, CLOCK_HZ = 8.2, 2.8, 1024, 2.4e9
+# The same scan instruction stream with its global loads and stores removed
+# (tools/probes/scan_lab.hip "voff no vmem", profiles/r01c_scan_lab.txt): us per clip-layer
+# at M-16f.  What the kernel's own VALU/SALU work costs with no memory at all.
+LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
     "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),
@@ -51,7 +55,7 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=336, help="clips per GPU")
     ap.add_argument("--config", default="m16", choices=sorted(CONFIGS))
-    ap.add_argument("--p50-chunks", type=int, default=30)
+    ap.add_argument("--p50-chunks", type=int, default=100)
     ap.add_argument("--scan-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -141,15 +145,18 @@ def scan_roofline(batch, reps, device, layout="tm"):
             "bytes_per_launch": algo, "shape": shape,
             "valu_model": {"floor_us": round(floor_s * 1e6, 2),
                            "frac_of_valu_floor": round(floor_s / avg_s, 4),
+                           "no_memory_us": round(LAB_NO_MEMORY_US_PER_CLIP_LAYER * batch, 1),
+                           "frac_of_no_memory": round(
+                               LAB_NO_MEMORY_US_PER_CLIP_LAYER * batch * 1e-6 / avg_s, 4),
                            "note": "1 exp + 4 fma-class per (element, state) at measured gfx950 "
                                    "issue costs, 2.4 GHz; the HBM floor is below it"}}
 
 
-def cpu_baseline(cfg, threads):
+def _oracle_clip_seconds(cfg, runs=3):
+    """Median wall time of the oracle's fp32 B=1 forward of one clip, after one warm-up."""
     from oracle import videomamba_oracle as orc
     from videomamba_amd.videomamba import PretrainVideoMamba
 
-    torch.set_num_threads(threads)
     torch.manual_seed(0)
     m = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],
                            num_frames=cfg["frames"])
@@ -159,14 +166,30 @@ def cpu_baseline(cfg, threads):
                 residual_in_fp32=True, pool_type="cls+avg", norm_epsilon=1e-5, d_state=16,
                 d_conv=4)
     x = torch.randn(1, 3, cfg["frames"], 224, 224)
+    times = []
     with torch.no_grad():
-        t0 = time.perf_counter()
-        orc.encoder_forward(p, ocfg, x)
-        dt = time.perf_counter() - t0
+        for i in range(runs + 1):
+            t0 = time.perf_counter()
+            orc.encoder_forward(p, ocfg, x)
+            if i:
+                times.append(time.perf_counter() - t0)
+    return statistics.median(times)
+
+
+def cpu_baseline(cfg, threads):
+    """the oracle (the CPU restatement pinned to the reference) on the host
+    cores, median of 3 after 1 warm-up, fp32 B=1: the bench clip, and C1 (Ti 8x224^2)."""
+    torch.set_num_threads(threads)
+    dt = _oracle_clip_seconds(cfg)
+    ti = CONFIGS["ti8"]
+    dt_c1 = _oracle_clip_seconds(ti)
     return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
             "cores": threads, "kind": "port",
-            "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward "
-                      f"({dt:.2f} s), oracle/videomamba_oracle.py"}
+            "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
+                      f"median of 3 after 1 warm-up ({dt:.2f} s), oracle/videomamba_oracle.py",
+            "c1": {"value": round(ti["frames"] * 196 / dt_c1, 2), "unit": "video-tokens/s",
+                   "sample": f"C1: 1 clip {ti['name']} {ti['frames']}x224^2 fp32 B=1, median "
+                             f"of 3 after 1 warm-up ({dt_c1:.2f} s)"}}
 
 
 def main():
