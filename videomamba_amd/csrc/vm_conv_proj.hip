@@ -65,7 +65,9 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
 // LDS: sA [64][72] bf16 (u chunk, then x_dbl[:, :R]);  sU [4 waves][64][72] bf16 (W_x
 // chunk during the sweep, then per-wave output staging);  dynamic: conv weights (D, 4)
 // and bias (D) as fp32.
-template <bool DT, int NB>  // DT: also run dt_proj here; NB = e_pad / 16 x_proj blocks
+// EXP (tools/probes/cp_lab.hip only; 0 in the library) removes pieces to price them:
+// 1 W_x staging loads, 2 x_proj MFMAs, 4 u stores, 8 conv window loads, 16 loop barriers.
+template <bool DT, int NB, int EXP = 0>  // DT: also run dt_proj here; NB = e_pad / 16 blocks
 __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
   // sU: W_x chunk (<= 128 rows x kCPPad) / x_dbl tile (64 x 2*kCPPad); with DT also the
   // per-wave dt staging (4 x 64 x kCPPad)
@@ -116,12 +118,13 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
   __syncthreads();  // sW ready
   for (int c0 = 0; c0 < D; c0 += kCPCh) {
     const int c = c0 + cg * 8;
-    if (c0 + kCPCh < D) load_win(c + kCPCh, nxt);  // prefetch the next chunk's window
+    if (!(EXP & 8) && c0 + kCPCh < D) load_win(c + kCPCh, nxt);  // prefetch the next window
     // ---- stage W_x[:, c0:c0+64] ----
     for (int idx = tid; idx < p.e_pad * 8; idx += 256) {
       const int n = idx >> 3, q = idx & 7;
       *reinterpret_cast<uint4*>(&sB[n * kCPPad + q * 8]) =
-          *reinterpret_cast<const uint4*>(p.wx + (long long)n * D + c0 + q * 8);
+          (EXP & 1) ? make_uint4(n, q, 0, 0)
+                    : *reinterpret_cast<const uint4*>(p.wx + (long long)n * D + c0 + q * 8);
     }
     // ---- conv + silu, one channel pair (one packed word of each window row) at a time ----
     if (ta < 3 && p.csi) {  // window reaches before the sequence start: conv state
@@ -165,8 +168,8 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
     }
     const uint4 qa = make_uint4(pa[0], pa[1], pa[2], pa[3]);
     const uint4 qb = make_uint4(pb[0], pb[1], pb[2], pb[3]);
-    if (rva) *reinterpret_cast<uint4*>(p.u + (long long)rowa * p.u_sl + c) = qa;
-    if (rvb) *reinterpret_cast<uint4*>(p.u + (long long)(rowa + 1) * p.u_sl + c) = qb;
+    if (!(EXP & 4) && rva) *reinterpret_cast<uint4*>(p.u + (long long)rowa * p.u_sl + c) = qa;
+    if (!(EXP & 4) && rvb) *reinterpret_cast<uint4*>(p.u + (long long)(rowa + 1) * p.u_sl + c) = qb;
     *reinterpret_cast<uint4*>(&sA[(2 * tg) * kCPPad + cg * 8]) = qa;
     *reinterpret_cast<uint4*>(&sA[(2 * tg + 1) * kCPPad + cg * 8]) = qb;
     // new conv state: the last `width` raw inputs, from the row holding step L-1
@@ -182,10 +185,10 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
           store_dyn(p.cso, b * p.cso_sb + (long long)(c + k) * p.cso_sd + s, p.cso_dtype, val);
         }
     }
-    __syncthreads();
+    if (!(EXP & 16)) __syncthreads();
     // ---- x_proj MFMA: wave's 16 tokens x all e_pad outputs, K = 64 ----
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < ((EXP & 2) ? 0 : 2); ++ks) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(
           &sA[(wave * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
 #pragma unroll
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, acc[j], 0, 0, 0);
       }
     }
-    __syncthreads();
+    if (!(EXP & 16)) __syncthreads();
 #pragma unroll
     for (int j = 0; j < 5; ++j) cur[j] = nxt[j];
   }
