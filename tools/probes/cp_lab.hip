@@ -208,6 +208,21 @@ int main(int argc, char** argv) {
   RUN("  - window loads", 8);
   RUN("  - loop barriers", 16);
   RUN("  - all memory in loop", 13);
+  {  // with the streaming conv state in and out (the bench's stateful chunk)
+    bf16_t *csi, *cso;
+    CK(hipMalloc(&csi, (size_t)B * D * 4 * 2)); CK(hipMalloc(&cso, (size_t)B * D * 4 * 2));
+    CK(hipMemset(csi, 0, (size_t)B * D * 4 * 2));
+    ConvProjParams q = p;
+    q.csi = csi; q.cso = cso; q.csi_sb = q.cso_sb = (long long)D * 4; q.csi_sd = q.cso_sd = 4;
+    q.csi_dtype = q.cso_dtype = VM_DTYPE_BF16;
+    timeit("conv_proj (library), conv state in+out", cp_bytes, [&] {
+      hipLaunchKernelGGL((conv_proj_kernel<false, 5, 0>), grid, dim3(256), lds, 0, q);
+      hipLaunchKernelGGL(conv_state_out_kernel, dim3((D + 255) / 256, B), dim3(256), 0, 0, q); });
+    q.csi = nullptr;
+    timeit("conv_proj (library), conv state out", cp_bytes, [&] {
+      hipLaunchKernelGGL((conv_proj_kernel<false, 5, 0>), grid, dim3(256), lds, 0, q);
+      hipLaunchKernelGGL(conv_state_out_kernel, dim3((D + 255) / 256, B), dim3(256), 0, 0, q); });
+  }
   timeit("dt_proj (library)", dt_bytes, [&] {
     hipLaunchKernelGGL(dt_proj_kernel, grid, dim3(256), 0, 0, p);
   });

@@ -128,19 +128,18 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
     }
     // ---- conv + silu, one channel pair (one packed word of each window row) at a time ----
     if (ta < 3 && p.csi) {  // window reaches before the sequence start: conv state
+      // a row's 8 state loads are issued together, then packed
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int te = ta - 3 + j;
         const int sj = p.width + te;
         if (te < 0 && sj >= 0) {
-          uint32_t w4[4];
+          const long long base = b * p.csi_sb + (long long)c * p.csi_sd + sj;
+          float sv[8];
 #pragma unroll
-          for (int k = 0; k < 8; k += 2)
-            w4[k / 2] = pack2(
-                load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd + sj, p.csi_dtype),
-                load_dyn(p.csi, b * p.csi_sb + (long long)(c + k + 1) * p.csi_sd + sj,
-                         p.csi_dtype));
-          cur[j] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          for (int k = 0; k < 8; ++k) sv[k] = load_dyn(p.csi, base + k * p.csi_sd, p.csi_dtype);
+          cur[j] = make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]), pack2(sv[4], sv[5]),
+                              pack2(sv[6], sv[7]));
         }
       }
     }
@@ -172,19 +171,6 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
     if (!(EXP & 4) && rvb) *reinterpret_cast<uint4*>(p.u + (long long)(rowa + 1) * p.u_sl + c) = qb;
     *reinterpret_cast<uint4*>(&sA[(2 * tg) * kCPPad + cg * 8]) = qa;
     *reinterpret_cast<uint4*>(&sA[(2 * tg + 1) * kCPPad + cg * 8]) = qb;
-    // new conv state: the last `width` raw inputs, from the row holding step L-1
-    if (p.cso && ((la && ta == p.seqlen - 1) || (lb && ta + 1 == p.seqlen - 1))) {
-      const int t = p.seqlen - 1;
-      for (int k = 0; k < 8; ++k)
-        for (int s = 0; s < p.width; ++s) {
-          const int te = t - p.width + 1 + s;
-          float val = 0.0f;
-          if (te >= 0) val = to_f32(xrow[te * p.xz_sl + c + k]);
-          else if (p.csi) val = load_dyn(p.csi, b * p.csi_sb + (long long)(c + k) * p.csi_sd +
-                                                    p.width + te, p.csi_dtype);
-          store_dyn(p.cso, b * p.cso_sb + (long long)(c + k) * p.cso_sd + s, p.cso_dtype, val);
-        }
-    }
     if (!(EXP & 16)) __syncthreads();
     // ---- x_proj MFMA: wave's 16 tokens x all e_pad outputs, K = 64 ----
 #pragma unroll
@@ -293,6 +279,25 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
 }
 
 
+// New conv state (B, D, width): the last `width` raw inputs of each channel — steps
+// L-width .. L-1 of x, or of the old state for steps before the sequence start
+// (mamba_simple.py:383-399). Its own small launch keeps the chunk loop of conv_proj_kernel
+// free of the one-row-per-sequence branch that held a workgroup per sequence back.
+__global__ __launch_bounds__(256) void conv_state_out_kernel(const ConvProjParams p) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= p.dim) return;
+  const bf16_t* xrow = p.xz + b * p.xz_sb;
+  for (int s = 0; s < p.width; ++s) {
+    const int te = p.seqlen - p.width + s;
+    float val = 0.0f;
+    if (te >= 0) val = to_f32(xrow[(long long)te * p.xz_sl + c]);
+    else if (p.csi) val = load_dyn(p.csi, b * p.csi_sb + (long long)c * p.csi_sd + p.width + te,
+                                   p.csi_dtype);
+    store_dyn(p.cso, b * p.cso_sb + (long long)c * p.cso_sd + s, p.cso_dtype, val);
+  }
+}
+
 // dt = x_dbl[:, :R] @ W_dt^T for 64-token tiles (the split form of conv_proj_kernel<true>).
 __global__ __launch_bounds__(256) void dt_proj_kernel(const ConvProjParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
@@ -386,5 +391,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   }
   // conv + x_proj at lower register pressure, then dt_proj from x_dbl
   if (!fused_dt) hipLaunchKernelGGL(dt_proj_kernel, grid, dim3(256), 0, st, p);
+  if (cs_out)
+    hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
   return vmhost::launch_status("vm_conv_proj_fwd");
 }
