@@ -223,9 +223,12 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((conv_proj_kernel<false, 5, 0>), grid, dim3(256), lds, 0, q);
       hipLaunchKernelGGL(conv_state_out_kernel, dim3((D + 255) / 256, B), dim3(256), 0, 0, q); });
   }
-  timeit("dt_proj (library)", dt_bytes, [&] {
-    hipLaunchKernelGGL(dt_proj_kernel, grid, dim3(256), 0, 0, p);
-  });
+  for (int rep = 0; rep < 2; ++rep) {
+    timeit("dt_proj 16 B stores, 4 waves", dt_bytes, [&] {
+      hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, 0, p); });
+    timeit("dt_proj (library: 8 B stores, 4 waves)", dt_bytes, [&] {
+      hipLaunchKernelGGL((dt_proj_kernel<8, 4>), grid, dim3(256), 0, 0, p); });
+  }
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   return 0;

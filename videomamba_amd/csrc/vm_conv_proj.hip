@@ -59,6 +59,7 @@ __device__ __forceinline__ float silu_f(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2e));
 }
 
+template <int SW = 16, int NW = 4>
 __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
                                          int row0, int lane, int wave);
 
@@ -224,8 +225,9 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
 }
 
 // dt_proj for one 64-token tile: A = x_dbl[:, :R] (zero-padded to r_pad) in sA,
-// wave = 64-column blocks wave, wave+4, ...; outputs staged per wave in sU and stored as
-// 128-byte row segments.
+// wave = 64-column blocks wave, wave+NW, ...; outputs staged per wave in sU and stored as
+// 128-byte row segments, SW bytes per lane-store.
+template <int SW, int NW>
 __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
                                          int row0, int lane, int wave) {
   const int D = p.dim;
@@ -238,7 +240,7 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
       af[i][ks] = *reinterpret_cast<const bf16x8*>(
           &sA[(i * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
   bf16_t* stg = sU + wave * kCPTok * kCPPad;
-  for (int cb = wave; cb * 64 < D; cb += 4) {
+  for (int cb = wave; cb * 64 < D; cb += NW) {
     f32x4 d[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -266,14 +268,34 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
         for (int e = 0; e < 4; ++e)
           stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
               from_f32<bf16_t>(d[i][j][e]);
-    // the wave reads back its own staging tile: 64 rows x 128 B, 16 B per lane-store
+    // the wave reads back its own staging tile: 64 rows x 128 B
+    if constexpr (SW == 16) {
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int lr = it * 8 + (lane >> 3), q = lane & 7;
-      const int row = row0 + lr;
-      const uint4 val = *reinterpret_cast<const uint4*>(&stg[lr * kCPPad + q * 8]);
-      if (row < p.rows)
-        *reinterpret_cast<uint4*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 8) = val;
+      for (int it = 0; it < 8; ++it) {
+        const int lr = it * 8 + (lane >> 3), q = lane & 7;
+        const int row = row0 + lr;
+        const uint4 val = *reinterpret_cast<const uint4*>(&stg[lr * kCPPad + q * 8]);
+        if (row < p.rows)
+          *reinterpret_cast<uint4*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 8) = val;
+      }
+    } else if constexpr (SW == 8) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int lr = it * 4 + (lane >> 4), q = lane & 15;
+        const int row = row0 + lr;
+        const uint2 val = *reinterpret_cast<const uint2*>(&stg[lr * kCPPad + q * 4]);
+        if (row < p.rows)
+          *reinterpret_cast<uint2*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 4) = val;
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 32; ++it) {
+        const int lr = it * 2 + (lane >> 5), q = lane & 31;
+        const int row = row0 + lr;
+        const uint32_t val = *reinterpret_cast<const uint32_t*>(&stg[lr * kCPPad + q * 2]);
+        if (row < p.rows)
+          *reinterpret_cast<uint32_t*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 2) = val;
+      }
     }
   }
 }
@@ -299,21 +321,23 @@ __global__ __launch_bounds__(256) void conv_state_out_kernel(const ConvProjParam
 }
 
 // dt = x_dbl[:, :R] @ W_dt^T for 64-token tiles (the split form of conv_proj_kernel<true>).
-__global__ __launch_bounds__(256) void dt_proj_kernel(const ConvProjParams p) {
+// NW waves share a tile's 64-column blocks (D = 1152: 18 blocks, 3 per wave at NW = 6).
+template <int SW = 16, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void dt_proj_kernel(const ConvProjParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
-  __shared__ __attribute__((aligned(16))) bf16_t sU[4 * kCPTok * kCPPad];
+  __shared__ __attribute__((aligned(16))) bf16_t sU[NW * kCPTok * kCPPad];
   const int tid = threadIdx.x;
   const int row0 = blockIdx.x * kCPTok;
-  for (int idx = tid; idx < kCPTok * kCPPad / 8; idx += 256)
+  for (int idx = tid; idx < kCPTok * kCPPad / 8; idx += 64 * NW)
     *reinterpret_cast<uint4*>(&sA[idx * 8]) = make_uint4(0, 0, 0, 0);
   __syncthreads();
-  for (int idx = tid; idx < kCPTok * p.r; idx += 256) {
+  for (int idx = tid; idx < kCPTok * p.r; idx += 64 * NW) {
     const int lr = idx / p.r, k = idx - lr * p.r;
     const int row = row0 + lr;
     sA[lr * kCPPad + k] = row < p.rows ? p.xdbl[(long long)row * p.xd_sl + k] : bf16_t(0);
   }
   __syncthreads();
-  dt_phase(p, sA, sU, row0, tid & 63, tid >> 6);
+  dt_phase<SW, NW>(p, sA, sU, row0, tid & 63, tid >> 6);
 }
 
 }  // namespace vm
@@ -390,7 +414,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
 #undef VM_CP_CASE
   }
   // conv + x_proj at lower register pressure, then dt_proj from x_dbl
-  if (!fused_dt) hipLaunchKernelGGL(dt_proj_kernel, grid, dim3(256), 0, st, p);
+  if (!fused_dt) hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, st, p);
   if (cs_out)
     hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
   return vmhost::launch_status("vm_conv_proj_fwd");
