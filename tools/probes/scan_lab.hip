@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <vector>
+#include <algorithm>
 
 #ifndef LAB_ATTR
 #define LAB_ATTR
@@ -29,6 +30,7 @@ struct LabP {
   const bf16* u; const bf16* dl; const bf16* xz; const bf16* xdbl; const float* bc32;
   const float* A; const float* Dv; const float* bias; bf16* y; float* hl;
   int B, D, L, Lp, R, N;
+  unsigned long long* clk;  // optional per-workgroup (memtime, realtime) stamps
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
@@ -60,6 +62,12 @@ __global__ __launch_bounds__(64 * NWV) LAB_ATTR void lab_kernel(const LabP p) {
   if (d0 >= p.D) return;
   const int d = d0 + lane;
   const int L = p.L;
+  unsigned long long* clk = p.clk ? p.clk + (static_cast<long long>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 : nullptr;
+  if (clk && threadIdx.x == 0) {
+    const unsigned long long mt = __builtin_amdgcn_s_memtime(), rt = __builtin_amdgcn_s_memrealtime();
+    clk[0] = mt;
+    clk[1] = rt;
+  }
   f2 A2[8], h[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -262,6 +270,11 @@ __global__ __launch_bounds__(64 * NWV) LAB_ATTR void lab_kernel(const LabP p) {
   for (int q = 0; q < 8; ++q) {
     hl[2 * q] = h[q].x;
     hl[2 * q + 1] = h[q].y;
+  }
+  if (clk && threadIdx.x == 0) {
+    const unsigned long long mt = __builtin_amdgcn_s_memtime(), rt = __builtin_amdgcn_s_memrealtime();
+    clk[2] = mt;
+    clk[3] = rt;
   }
 }
 
@@ -510,7 +523,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(xdbl, xd.data(), xd.size() * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(bc32, b32.data(), b32.size() * 4, hipMemcpyHostToDevice));
   }
-  LabP p{u, dl, xz, xdbl, bc32, A, Dv, bias, y, hl, B, D, L, Lp, R, N};
+  LabP p{u, dl, xz, xdbl, bc32, A, Dv, bias, y, hl, B, D, L, Lp, R, N, nullptr};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -555,6 +568,50 @@ int main(int argc, char** argv) {
     printf("%-34s B=%d %9.1f us  %6.2f us/clip-layer  %6.1f GB/s  frac %.4f  maxdiff y %.2e h %.2e\n",
            name, B, us, us / B, algo / (us * 1e-6) / 1e9, algo / (us * 1e-6) / 8e12, maxdiff, maxh);
   };
+  if (argc > 4 && strcmp(argv[4], "clock") == 0) {
+    // in-kernel clock (MI355X_MICROARCH.md DVFS item 6): ~2 s of back-to-back launches,
+    // then one launch stamping s_memtime / s_memrealtime per workgroup; median over
+    // workgroups of dmemtime / drealtime * 100 MHz
+    const int nwg = (D / 64 + 1) / 2 * B;
+    unsigned long long* clk;
+    CK(hipMalloc(&clk, static_cast<size_t>(nwg) * 4 * 8));
+    auto clock_of = [&](const char* name, void (*k)(LabP)) {
+      dim3 grid((D / 64 + 1) / 2, B);
+      LabP q = p;
+      CK(hipEventRecord(e0));
+      int n = 0;
+      float ms = 0.0f;
+      for (; n < 2000; ++n) {
+        hipLaunchKernelGGL(k, grid, dim3(128), 0, 0, q);
+        if (n % 50 == 49) {
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (ms > 2000.0f) break;
+        }
+      }
+      q.clk = clk;
+      hipLaunchKernelGGL(k, grid, dim3(128), 0, 0, q);
+      std::vector<unsigned long long> c(static_cast<size_t>(nwg) * 4);
+      CK(hipMemcpy(c.data(), clk, c.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<double> f;
+      for (int i = 0; i < nwg; ++i) {
+        const double dm = static_cast<double>(c[4 * i + 2] - c[4 * i]);
+        const double dr = static_cast<double>(c[4 * i + 3] - c[4 * i + 1]);
+        if (dr > 0) f.push_back(dm / dr * 0.1);  // GHz (realtime ticks at 100 MHz)
+      }
+      std::sort(f.begin(), f.end());
+      printf("%-34s %d launches, %.1f us each; in-kernel clock median %.3f GHz (p10 %.3f, p90 %.3f)\n",
+             name, n + 1, ms * 1e3 / (n + 1), f[f.size() / 2], f[f.size() / 10], f[f.size() * 9 / 10]);
+      fflush(stdout);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+      clock_of("pk voff pf8 (product stream)", lab_kernel<true, false, true, true, true>);
+      clock_of("pk voff pf8 no vmem", lab_kernel<true, false, true, true, true, 2>);
+      clock_of("pk voff pf8 shared rows (L2)", lab_kernel<true, false, true, true, true, 3>);
+    }
+    return 0;
+  }
   if (argc > 4 && strcmp(argv[4], "calib") == 0) {
     // PMC calibration run: the scan's access pattern (2-byte lanes, one 128-B row segment
     // per wave per operand and step) with a known byte count and no scan math
