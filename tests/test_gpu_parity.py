@@ -80,7 +80,7 @@ def _oracle_scan(Bz, D, L, N):
     return _ORACLE_CACHE[key]
 
 
-SCAN_VARIANTS = ["0", "1", "5", "6", "13", "14", "15", "16", "17"]
+SCAN_VARIANTS = ["0", "1", "5", "6", "13", "14", "15", "16", "17", "18", "19"]
 
 
 @pytest.fixture(params=SCAN_VARIANTS)

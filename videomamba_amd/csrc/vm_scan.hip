@@ -706,6 +706,31 @@ __device__ __forceinline__ void load_even(const T* row, int t0, int L, bool vec,
   }
 }
 
+// bf16 pairs as raw words (the pipelined v5 keeps the next block's inputs packed)
+template <int K>
+__device__ __forceinline__ void load_even_raw(const bf16_t* row, int t0, int L, bool vec,
+                                              uint32_t (&w)[K / 2]) {
+  if (vec && t0 + K <= L) {
+#pragma unroll
+    for (int j = 0; j < K / 2; ++j) w[j] = *reinterpret_cast<const uint32_t*>(row + t0 + 2 * j);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K / 2; ++j) {
+      const uint32_t lo = t0 + 2 * j < L ? static_cast<uint32_t>(row[t0 + 2 * j]) : 0u;
+      const uint32_t hi = t0 + 2 * j + 1 < L ? static_cast<uint32_t>(row[t0 + 2 * j + 1]) : 0u;
+      w[j] = lo | (hi << 16);
+    }
+  }
+}
+template <int K>
+__device__ __forceinline__ void unpack_even(const uint32_t (&w)[K / 2], float (&v)[K]) {
+#pragma unroll
+  for (int j = 0; j < K / 2; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+
 template <typename T, int K>
 __device__ __forceinline__ void store_even(T* row, int t0, int LO, bool vec, const float (&v)[K]) {
   if (vec && t0 + K <= LO) {
@@ -727,9 +752,13 @@ __device__ __forceinline__ void store_even(T* row, int t0, int LO, bool vec, con
   }
 }
 
-template <typename T, int K, int NW>
+// PIPE (bf16, small grids: one workgroup per CU): the next time block's B/C rows and
+// u / delta / z are loaded into registers while the current block computes, so a block
+// no longer waits on its own global loads (three round trips per block otherwise).
+template <typename T, int K, int NW, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   static_assert(K % 2 == 0, "K must be even");
+  static_assert(!PIPE || sizeof(T) == 2, "the pipelined form keeps bf16 words");
   constexpr int TB = 64 * K;
   constexpr int K2 = K / 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -764,30 +793,102 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   const float Dv = p.D ? p.D[d] : 0.0f;
   const float bias = p.dbias ? p.dbias[d] : 0.0f;
 
+  // B/C staging role: chunk idx = (B|C row, 8-step chunk); PIPE keeps kSt chunks per thread
+  const int chunks = 2 * N * (TB / 8);
+  constexpr int kSt = (2 * kMaxN * (TB / 8) + 64 * NW - 1) / (64 * NW);
+  auto stage_src = [&](int idx, int t_blk, const T*& src, int& t, int& n, bool& isC) {
+    const int row = idx / (TB / 8);
+    const int c8 = idx - row * (TB / 8);
+    isC = row >= N;
+    n = isC ? row - N : row;
+    src = (isC ? Cb + n * p.c_sn : Bb + n * p.b_sn);
+    t = t_blk + c8 * 8;
+  };
+  auto stage_put = [&](int idx, const float (&w)[8]) {
+    const int row = idx / (TB / 8);
+    const int c8 = idx - row * (TB / 8);
+    const bool isC = row >= N;
+    const int n = isC ? row - N : row;
+    float* base = (isC ? sC : sB) + n * TB;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const int r = c8 * 8 + j;       // block-relative step (even)
+      const int ln = r / K, k = r - ln * K;
+      *reinterpret_cast<float2*>(base + ((k >> 1) * 64 + ln) * 2) = make_float2(w[j], w[j + 1]);
+    }
+  };
+  uint4 stq[PIPE ? kSt : 1];
+  auto stage_fetch = [&](int t_blk) {  // PIPE: raw bf16 chunks into registers
+#pragma unroll
+    for (int c = 0; c < kSt; ++c) {
+      const int idx = tid + c * 64 * NW;
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (idx < chunks) {
+        const T* src; int t, n; bool isC;
+        stage_src(idx, t_blk, src, t, n, isC);
+        if (p.vec_bc && t + 8 <= L) {
+          q = *reinterpret_cast<const uint4*>(src + t);
+        } else {
+          uint32_t h8[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t lo = t + 2 * j < L ? static_cast<uint32_t>(src[t + 2 * j]) : 0u;
+            const uint32_t hi = t + 2 * j + 1 < L ? static_cast<uint32_t>(src[t + 2 * j + 1]) : 0u;
+            h8[j] = lo | (hi << 16);
+          }
+          q = make_uint4(h8[0], h8[1], h8[2], h8[3]);
+        }
+      }
+      if constexpr (PIPE) stq[c] = q;
+    }
+  };
+  const int t0_first = lane * K;
+  uint32_t nu[PIPE ? K / 2 : 1], nd[PIPE ? K / 2 : 1], nz[PIPE ? K / 2 : 1];
+  auto row_fetch = [&](int t_blk) {
+    if constexpr (PIPE) {
+      const int t0n = t_blk + t0_first;
+      load_even_raw<K>(reinterpret_cast<const bf16_t*>(urow), t0n, L, vx, nu);
+      load_even_raw<K>(reinterpret_cast<const bf16_t*>(drow), t0n, L, vx, nd);
+      if (zrow) load_even_raw<K>(reinterpret_cast<const bf16_t*>(zrow), t0n, L, vx, nz);
+    }
+  };
+  if constexpr (PIPE) {
+    if (LO > 0) {
+      stage_fetch(0);
+      row_fetch(0);
+    }
+  }
+
   for (int t_blk = 0; t_blk < LO; t_blk += TB) {
     // ---- stage B/C: thread = (B|C, state, 8-step chunk) -> four float2 writes ----
     __syncthreads();
-    const int chunks = 2 * N * (TB / 8);
-    for (int idx = tid; idx < chunks; idx += 64 * NW) {
-      const int row = idx / (TB / 8);
-      const int c8 = idx - row * (TB / 8);
-      const bool isC = row >= N;
-      const int n = isC ? row - N : row;
-      const T* src = (isC ? Cb + n * p.c_sn : Bb + n * p.b_sn);
-      const int t = t_blk + c8 * 8;
-      float w[8];
-      if (p.vec_bc && t + 8 <= L) {
-        load8(src + t, w);
-      } else {
+    if constexpr (PIPE) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
+      for (int c = 0; c < kSt; ++c) {
+        const int idx = tid + c * 64 * NW;
+        if (idx < chunks) {
+          const uint32_t q4[4] = {stq[c].x, stq[c].y, stq[c].z, stq[c].w};
+          float w[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            w[2 * j] = __uint_as_float(q4[j] << 16);
+            w[2 * j + 1] = __uint_as_float(q4[j] & 0xffff0000u);
+          }
+          stage_put(idx, w);
+        }
       }
-      float* base = (isC ? sC : sB) + n * TB;
+    } else {
+      for (int idx = tid; idx < chunks; idx += 64 * NW) {
+        const T* src; int t, n; bool isC;
+        stage_src(idx, t_blk, src, t, n, isC);
+        float w[8];
+        if (p.vec_bc && t + 8 <= L) {
+          load8(src + t, w);
+        } else {
 #pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const int r = c8 * 8 + j;       // block-relative step (even)
-        const int ln = r / K, k = r - ln * K;
-        *reinterpret_cast<float2*>(base + ((k >> 1) * 64 + ln) * 2) = make_float2(w[j], w[j + 1]);
+          for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
+        }
+        stage_put(idx, w);
       }
     }
     __syncthreads();
@@ -795,10 +896,22 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
     // ---- per-lane prologue ----
     const int t0 = t_blk + lane * K;
     float dl[K], du[K], y[K];
+    uint32_t cz[PIPE ? K / 2 : 1];
     {
       float uv[K], dv[K];
-      load_even<T, K>(urow, t0, L, vx, uv);
-      load_even<T, K>(drow, t0, L, vx, dv);
+      if constexpr (PIPE) {
+        unpack_even<K>(nu, uv);
+        unpack_even<K>(nd, dv);
+#pragma unroll
+        for (int j = 0; j < K / 2; ++j) cz[j] = nz[j];
+        if (t_blk + TB < LO) {  // the next block's inputs land while this one computes
+          stage_fetch(t_blk + TB);
+          row_fetch(t_blk + TB);
+        }
+      } else {
+        load_even<T, K>(urow, t0, L, vx, uv);
+        load_even<T, K>(drow, t0, L, vx, dv);
+      }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         float dd = dv[k] + bias;
@@ -867,7 +980,8 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
 
     if (zrow) {
       float zv[K];
-      load_even<T, K>(zrow, t0, L, vx, zv);
+      if constexpr (PIPE) unpack_even<K>(cz, zv);
+      else load_even<T, K>(zrow, t0, L, vx, zv);
 #pragma unroll
       for (int k = 0; k < K; ++k) y[k] *= silu_fast(zv[k]);
     }
@@ -883,10 +997,18 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   }
 }
 
+// pipe: -1 auto (bf16 grids of at most one workgroup per CU), 0 off, 1 on (bf16 only)
 template <typename T, int K, int NW>
-static void launch_v5(const ScanParams& p, hipStream_t s) {
+static void launch_v5(const ScanParams& p, hipStream_t s, int pipe = -1) {
   const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
   dim3 grid((p.dim + NW - 1) / NW, p.batch);
+  const bool use_pipe = sizeof(T) == 2 && (pipe == 1 || (pipe < 0 && grid.x * grid.y <= 256));
+  if constexpr (sizeof(T) == 2) {
+    if (use_pipe) {
+      hipLaunchKernelGGL((scan_v5_kernel<T, K, NW, true>), grid, dim3(64 * NW), lds, s, p);
+      return;
+    }
+  }
   hipLaunchKernelGGL((scan_v5_kernel<T, K, NW>), grid, dim3(64 * NW), lds, s, p);
 }
 
@@ -1153,6 +1275,8 @@ static void dispatch_scan(const ScanParams& p, hipStream_t s) {
     case 15: launch_v5<T, 8, 4>(p, s); break;
     case 16: launch_v5<T, 16, 4>(p, s); break;
     case 17: launch_v5<T, 8, 8>(p, s); break;
+    case 18: launch_v5<T, 10, 8>(p, s, 0); break;     // v5 K=10 without the pipelined form
+    case 19: launch_v5<T, 10, 8>(p, s, 1); break;     // v5 K=10 pipelined at any grid (bf16)
     default: launch_v5_auto<T>(p, s); break;          // v5: scalar, K chosen per L
   }
 }
