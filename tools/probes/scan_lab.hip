@@ -620,6 +620,15 @@ int main(int argc, char** argv) {
     return 0;
   }
   bench("ref scalar bf16-BC (baseline)", lab_kernel<false, false, false, true, true>, true);
+  if (argc > 4 && strcmp(argv[4], "occupancy") == 0) {
+    // waves per SIMD capped by dynamic LDS per 2-wave workgroup (160 KB per CU)
+    for (int rep = 0; rep < 2; ++rep) {
+      bench("pk voff pf8, 5 waves/SIMD (16 KB)", lab_kernel<true, false, true, true, true>, false, 2, 16 * 1024);
+      bench("pk voff pf8, 4 waves/SIMD (20 KB)", lab_kernel<true, false, true, true, true>, false, 2, 20 * 1024);
+      bench("pk voff pf8, 3 waves/SIMD (26 KB)", lab_kernel<true, false, true, true, true>, false, 2, 26 * 1024);
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     bench("pk voff pf8 (ordered prologue)", lab_kernel<true, false, true, true, true>, false);
     bench("pk pf8 (ordered prologue)", lab_kernel<true, false, false, true, true>, false);
