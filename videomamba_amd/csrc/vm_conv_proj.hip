@@ -52,8 +52,13 @@ __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+// two floats -> packed bf16 pair in one v_cvt_pk_bf16_f32 (round to nearest even, as
+// from_f32<bf16_t>)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(from_f32<bf16_t>(a)) | (static_cast<uint32_t>(from_f32<bf16_t>(b)) << 16);
+  const bf16x2 h = __builtin_convertvector(f32x2{a, b}, bf16x2);
+  return __builtin_bit_cast(uint32_t, h);
 }
 __device__ __forceinline__ float silu_f(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2e));

@@ -12,6 +12,8 @@
 // one 16-byte load), block tile 64 tokens x 64 channels (2x2 waves of 32x32).
 // Other shapes / fp32: a scalar implicit-GEMM kernel (same math, fp32 accumulate).
 
+#include <stdlib.h>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -121,6 +123,120 @@ __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
       }
 }
 
+// 16x16 patches, bf16, embed % 192 == 0 (the VideoMamba shapes): workgroup tile
+// 64 tokens x 192 channels (2x2 waves of 32 x 96, so each video patch row is read by 3
+// workgroups instead of 9), im2col offsets advanced by shifts (one k-step of 32 = two
+// patch rows of one channel), and the epilogue staged through LDS so the bias / spatial /
+// temporal adds and the stores run on 8-channel vectors of whole output rows.
+constexpr int kPT = 64, kPN = 192, kPJ = 6;  // tokens, channels per workgroup; 16-col tiles per wave
+__global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t stile[kPT * (kPN + 8)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int mt0 = blockIdx.x * kPT;
+  const int m0 = mt0 + (wave & 1) * 32;
+  const int n0 = blockIdx.y * kPN + (wave >> 1) * 96;
+  const int r = lane & 15;
+  const int kg = lane >> 4;
+  const bf16_t* vid = static_cast<const bf16_t*>(p.video);
+  const bf16_t* wt = static_cast<const bf16_t*>(p.w);
+  const long long plane = (long long)p.frames * p.height * p.width;  // one input channel
+  // lane's k within a 32-wide k-step: patch row 2*step + (kg >> 1), columns (kg & 1) * 8
+  const long long lane_k = (long long)(kg >> 1) * p.width + (kg & 1) * 8;
+
+  long long abase[2];
+  bool mval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + i * 16 + r;
+    mval[i] = m < p.M;
+    abase[i] = token_base(p, mval[i] ? m : 0) + lane_k;
+  }
+  const bf16_t* wrow[kPJ];
+#pragma unroll
+  for (int j = 0; j < kPJ; ++j) wrow[j] = wt + (long long)(n0 + j * 16 + r) * p.K + kg * 8;
+  f32x4 acc[2][kPJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < kPJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bf16x8 zero = {};
+  const int steps_per_c = 8 * p.kt;  // 256 * kt k per input channel, 32 per step
+  for (int kk = 0; kk < p.K; kk += 32) {
+    const int step = kk >> 5;
+    const int ci = step / steps_per_c;
+    const int sr = step - ci * steps_per_c;  // (kz, row pair) within the channel
+    const int kz = sr >> 3;
+    const long long koff = ci * plane + (long long)kz * p.height * p.width +
+                           (long long)(2 * (sr & 7)) * p.width;
+    bf16x8 a[2], b[kPJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      a[i] = mval[i] ? *reinterpret_cast<const bf16x8*>(vid + abase[i] + koff) : zero;
+#pragma unroll
+    for (int j = 0; j < kPJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kk);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < kPJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+  // stage round(acc + bias) (the conv output's rounding point) as bf16 [token][channel]
+#pragma unroll
+  for (int j = 0; j < kPJ; ++j) {
+    const int nl = (wave >> 1) * 96 + j * 16 + r;
+    const float bj = p.bias[blockIdx.y * kPN + nl];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ml = (wave & 1) * 32 + i * 16 + kg * 4 + e;
+        stile[ml * (kPN + 8) + nl] = from_f32<bf16_t>(acc[i][j][e] + bj);
+      }
+  }
+  __syncthreads();
+  // + spatial pos (rounded), + temporal pos, 8 channels per thread-vector
+  const int hw = p.gh * p.gw;
+  const int per_b = p.tt * hw;
+  const bf16_t* spos = static_cast<const bf16_t*>(p.spos);
+  const bf16_t* tpos = static_cast<const bf16_t*>(p.tpos);
+  bf16_t* out = static_cast<bf16_t*>(p.out);
+  for (int idx = tid; idx < kPT * (kPN / 8); idx += 256) {
+    const int ml = idx / (kPN / 8);
+    const int c8 = (idx - ml * (kPN / 8)) * 8;
+    const int m = mt0 + ml;
+    if (m >= p.M) continue;
+    const int b = m / per_b;
+    const int rem = m - b * per_b;
+    const int t = rem / hw;
+    const int sp = rem - t * hw;
+    const int n = blockIdx.y * kPN + c8;
+    const uint4 cv = *reinterpret_cast<const uint4*>(&stile[ml * (kPN + 8) + c8]);
+    const uint4 sv = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
+    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
+    const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w},
+                   tw[4] = {tv.x, tv.y, tv.z, tv.w};
+    uint32_t ow[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float c = __uint_as_float(h ? (cw[q] & 0xffff0000u) : (cw[q] << 16));
+        const float sp_ = __uint_as_float(h ? (sw[q] & 0xffff0000u) : (sw[q] << 16));
+        const float tp = __uint_as_float(h ? (tw[q] & 0xffff0000u) : (tw[q] << 16));
+        o[h] = round_to<bf16_t>(c + sp_) + tp;
+      }
+      ow[q] = static_cast<uint32_t>(from_f32<bf16_t>(o[0])) |
+              (static_cast<uint32_t>(from_f32<bf16_t>(o[1])) << 16);
+    }
+    *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
+        make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void patch_generic_kernel(const PatchParams p) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -168,7 +284,14 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch % 8 == 0 && width % 8 == 0 &&
                        p.K % 8 == 0 && vmhost::aligned16(video) && vmhost::aligned16(weight);
-  if (mfma_ok) {
+  const char* pv = getenv("VM_PATCH_KERNEL");  // "1": the 64x64-tile kernel (A/B)
+  const bool wide_ok = mfma_ok && patch == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
+                       out_sb % 8 == 0 && vmhost::aligned16(out) && vmhost::aligned16(spos) &&
+                       vmhost::aligned16(tpos) && !(pv && atoi(pv) == 1);
+  if (wide_ok) {
+    dim3 grid((p.M + kPT - 1) / kPT, embed / kPN);
+    hipLaunchKernelGGL(patch_mfma16_kernel, grid, dim3(256), 0, s, p);
+  } else if (mfma_ok) {
     dim3 grid((p.M + 63) / 64, (embed + 63) / 64);
     hipLaunchKernelGGL(patch_mfma_kernel, grid, dim3(256), 0, s, p);
   } else {
