@@ -11,6 +11,10 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
+Other configs: --config m32 (VideoMamba-M 32x224^2, the C4 clip shape; run under torchrun
+for the 8-GPU batch-sharded case), --config ti8 --full-sequence (C2).  The roofline block
+is always the scan at the M-16f shape.
+
 Extra fields: chunk_p50_ms (B=1 chunk latency, HIP-graph replay; chunk_p50_eager_ms the
 eager launch path), roofline of the selective-scan kernel
 (HIP-event timed at the bench shape; algorithmic bytes per launch), cpu_baseline (the
@@ -43,8 +47,9 @@ CYC_EXP, CYC_FMA, SIMDS, CLOCK_HZ = 8.2, 2.8, 1024, 2.4e9
 LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
-    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),
-    "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti"),
+    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),  # C3 (default)
+    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M"),  # C4 clip shape
+    "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti"),  # C1 / C2 shape
 }
 
 
@@ -59,6 +64,8 @@ def _args():
     ap.add_argument("--scan-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--full-sequence", action="store_true",
+                    help="stateless full-sequence forward (C2) instead of a stateful chunk")
     return ap.parse_args()
 
 
@@ -215,6 +222,8 @@ def main():
     state = model.allocate_state(B, dtype=torch.bfloat16, device=device)
 
     def step():
+        if args.full_sequence:
+            return model(x)
         return model(x, ssm_state=state, temporal_pos_offset=0)
 
     with torch.no_grad():
@@ -264,8 +273,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic clips (randn), random-init weights (seed 0)",
-            "config": {"workload": f"{cfg['name']} {T}x224^2 bf16, one stateful streaming "
-                                   f"chunk (chunk_size 32) per step",
+            "config": {"workload": f"{cfg['name']} {T}x224^2 bf16, " + (
+                           "full-sequence forward per step" if args.full_sequence else
+                           "one stateful streaming chunk (chunk_size 32) per step"),
                        "model": cfg["name"], "global_batch": world * B, "per_gpu_batch": B,
                        "frames": T, "seq_len": 1 + T * 196,
                        "parallelism": f"batch-sharded x{world}, no data-path collectives"},
