@@ -391,3 +391,22 @@ def test_patch_embed_wide_tile_matches_small_tile_bitwise(Bz, T, H, W, kt, C, mo
         K.patch_embed(video, w, b, spos, tpos, out, 1, out.stride(0))
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_conv_proj_fused_dt_matches_split_bitwise(monkeypatch):
+    """conv_proj with dt_proj inside (default) and as its own kernel (VM_CONV_PROJ_SPLIT=1)
+    give identical mixer outputs and states (token-major bf16 mixer, stateful chunks)."""
+    from videomamba_amd.mamba_simple import Mamba
+    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
+    torch.manual_seed(3)
+    m = Mamba(d_model=64, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    x = torch.randn(3, 301, 64, device=DEV).to(torch.bfloat16)
+    res = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("VM_CONV_PROJ_SPLIT", split)
+        with torch.no_grad():
+            o1, (c1, s1) = m(x[:, :150], return_state=True)
+            o2, (c2, s2) = m(x[:, 150:], state=(c1, s1.clone()), return_state=True)
+        res.append((o1, c1, o2, c2, s2))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

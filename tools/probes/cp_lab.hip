@@ -233,6 +233,25 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(conv_state_out_kernel, dim3((D + 255) / 256, B), dim3(256), 0, 0, q); });
   }
   for (int rep = 0; rep < 2; ++rep) {
+    timeit("split: conv_proj + dt_proj (library)", cp_bytes + dt_bytes, [&] {
+      hipLaunchKernelGGL((conv_proj_kernel<false, 5, 0>), grid, dim3(256), lds, 0, p);
+      hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, 0, p); });
+    timeit("fused: conv_proj<DT> (half-tile dt)", cp_bytes + dt_bytes, [&] {
+      hipLaunchKernelGGL((conv_proj_kernel<true, 5, 0>), grid, dim3(256), lds, 0, p); });
+  }
+  {  // fused dt must equal the split kernels' dt bit for bit
+    std::vector<uint16_t> r1(rows * D), r2(rows * D);
+    hipLaunchKernelGGL((conv_proj_kernel<false, 5, 0>), grid, dim3(256), lds, 0, p);
+    hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, 0, p);
+    CK(hipMemcpy(r1.data(), dt, rows * D * 2, hipMemcpyDeviceToHost));
+    CK(hipMemset(dt, 0, rows * D * 2));
+    hipLaunchKernelGGL((conv_proj_kernel<true, 5, 0>), grid, dim3(256), lds, 0, p);
+    CK(hipMemcpy(r2.data(), dt, rows * D * 2, hipMemcpyDeviceToHost));
+    long long diff = 0;
+    for (long long i = 0; i < rows * D; ++i) diff += r1[i] != r2[i];
+    printf("fused vs split dt: %lld differing elements of %lld\n", diff, rows * D);
+  }
+  for (int rep = 0; rep < 2; ++rep) {
     timeit("dt_proj 16 B stores, 4 waves", dt_bytes, [&] {
       hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, 0, p); });
     timeit("dt_proj (library: 8 B stores, 4 waves)", dt_bytes, [&] {

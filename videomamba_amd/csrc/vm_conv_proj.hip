@@ -67,6 +67,8 @@ __device__ __forceinline__ float silu_f(float x) {
 template <int SW = 16, int NW = 4>
 __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
                                          int row0, int lane, int wave);
+__device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
+                                              bf16_t* sU, int row0, int lane, int wave);
 
 // LDS: sA [64][72] bf16 (u chunk, then x_dbl[:, :R]);  sU [4 waves][64][72] bf16 (W_x
 // chunk during the sweep, then per-wave output staging);  dynamic: conv weights (D, 4)
@@ -77,7 +79,7 @@ template <bool DT, int NB, int EXP = 0>  // DT: also run dt_proj here; NB = e_pa
 __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
   // sU: W_x chunk (<= 128 rows x kCPPad) / x_dbl tile (64 x 2*kCPPad); with DT also the
   // per-wave dt staging (4 x 64 x kCPPad)
-  constexpr int kSU = DT ? 4 * kCPTok * kCPPad : 2 * kCPTok * kCPPad;
+  constexpr int kSU = 2 * kCPTok * kCPPad;  // with DT the dt staging is 4 waves x 32 rows
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
   __shared__ __attribute__((aligned(16))) bf16_t sU[kSU];
   extern __shared__ __attribute__((aligned(16))) float sW[];  // [D][4] taps, then [D] bias
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
   }
   if constexpr (DT) {
     __syncthreads();  // sU is reused below as per-wave output staging
-    dt_phase(p, sA, sU, row0, lane, wave);
+    dt_phase_half(p, sA, sU, row0, lane, wave);
   }
 }
 
@@ -305,6 +307,65 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
   }
 }
 
+
+// dt_proj inside conv_proj (DT): as dt_phase, but each 64-column block in two 32-row
+// halves, so the per-wave staging is 32 rows and the fused kernel keeps conv_proj's LDS
+// budget (3 workgroups per CU) and half the accumulators.
+__device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
+                                              bf16_t* sU, int row0, int lane, int wave) {
+  const int D = p.dim;
+  const int ksteps = p.r_pad / 32;
+  bf16_t* stg = sU + wave * 32 * kCPPad;
+  for (int cb = wave; cb * 64 < D; cb += 4) {
+    bf16x8 bw[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        if (ks < ksteps)
+          bw[j][ks] = *reinterpret_cast<const bf16x8*>(
+              p.wdt + (long long)(cb * 64 + j * 16 + (lane & 15)) * p.r_pad + ks * 32 +
+              (lane >> 4) * 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 d[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks < ksteps) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+                &sA[((2 * h + i) * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              d[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][ks], d[i][j], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
+                from_f32<bf16_t>(d[i][j][e]);
+      // 32 rows x 128 B out, 16 B per lane-store
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int lr = it * 8 + (lane >> 3), q = lane & 7;
+        const int row = row0 + h * 32 + lr;
+        const uint4 val = *reinterpret_cast<const uint4*>(&stg[lr * kCPPad + q * 8]);
+        if (row < p.rows)
+          *reinterpret_cast<uint4*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 8) = val;
+      }
+    }
+  }
+}
 
 // New conv state (B, D, width): the last `width` raw inputs of each channel — steps
 // L-width .. L-1 of x, or of the old state for steps before the sequence start
@@ -405,8 +466,10 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   dim3 grid((p.rows + kCPTok - 1) / kCPTok);
   const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // dt_proj runs inside conv_proj (half-tile dt phase, same LDS budget); VM_CONV_PROJ_SPLIT=1
+  // runs it as its own kernel instead (bit-identical output)
   const char* split = getenv("VM_CONV_PROJ_SPLIT");
-  const bool fused_dt = split && atoi(split) == 0;
+  const bool fused_dt = !(split && atoi(split) == 1);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
   switch (e_pad / 16) {  // x_proj output blocks
 #define VM_CP_CASE(NBV)                                              \
