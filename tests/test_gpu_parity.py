@@ -372,10 +372,12 @@ def test_patch_embed_matches_oracle(dt, Bz, T, H, W, P, kt, C):
     _close(out[:, 2:2 + ref.shape[1]], ref, 1e-5 if dt == torch.float32 else 2e-2)
 
 
-@pytest.mark.parametrize("Bz,T,H,W,kt,C", [(2, 4, 224, 224, 1, 576), (1, 4, 64, 48, 2, 192)])
+@pytest.mark.parametrize("Bz,T,H,W,kt,C", [(2, 4, 224, 224, 1, 576), (1, 4, 64, 48, 2, 192),
+                                           (6, 32, 224, 224, 1, 192)])  # >= 32768 tokens
 def test_patch_embed_wide_tile_matches_small_tile_bitwise(Bz, T, H, W, kt, C, monkeypatch):
-    """The 64x192-tile kernel (16x16 patches, embed % 192 == 0) accumulates in the same
-    k order as the 64x64-tile kernel and rounds at the same points: identical bits."""
+    """The 64x192-tile and the LDS-staged 128x192-tile kernels (16x16 patches, embed % 192
+    == 0) accumulate in the same k order as the 64x64-tile kernel and round at the same
+    points: identical bits."""
     g = torch.Generator().manual_seed(7 + C)
     bf = torch.bfloat16
     video = torch.randn(Bz, 3, T, H, W, generator=g).to(bf).to(DEV)
@@ -385,12 +387,13 @@ def test_patch_embed_wide_tile_matches_small_tile_bitwise(Bz, T, H, W, kt, C, mo
     spos = (0.02 * torch.randn(hw, C, generator=g)).to(bf).to(DEV)
     tpos = (0.02 * torch.randn(T // kt, C, generator=g)).to(bf).to(DEV)
     outs = []
-    for kern in ("0", "1"):
+    for kern in ("0", "1", "2"):
         monkeypatch.setenv("VM_PATCH_KERNEL", kern)
         out = torch.zeros(Bz, (T // kt) * hw + 1, C, dtype=bf, device=DEV)
         K.patch_embed(video, w, b, spos, tpos, out, 1, out.stride(0))
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[2], outs[1])
 
 
 def test_conv_proj_fused_dt_matches_split_bitwise(monkeypatch):

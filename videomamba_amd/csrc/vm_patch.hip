@@ -237,6 +237,157 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
   }
 }
 
+// 16x16 patches, bf16, embed % 192 == 0, an LDS-staged GEMM: workgroup tile 128 tokens x
+// 192 channels, 4 waves of 64 x 96 (24 accumulators), K in steps of 32 with the im2col A
+// tile (8 KB) and the weight tile (12 KB) staged through two LDS buffers by register
+// prefetch (the next step's loads are in flight during this step's 24 MFMAs per wave).
+// The epilogue re-uses the staging area for the same vectorised bias / pos adds as
+// patch_mfma16_kernel.  Same k order and rounding points as the 64x64 kernel.
+constexpr int kGT = 128, kGN = 192, kGP = 40;  // tile tokens, channels; LDS row pitch (bf16)
+__global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
+  // staging: 2 buffers x (A 128 x 40 + B 192 x 40) bf16 = 40 KB; epilogue: 128 x 200 bf16
+  __shared__ __attribute__((aligned(16))) bf16_t smem[kGT * (kGN + 8)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int mt0 = blockIdx.x * kGT;
+  const int nt0 = blockIdx.y * kGN;
+  const int wm = (wave & 1) * 64, wn = (wave >> 1) * 96;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const bf16_t* vid = static_cast<const bf16_t*>(p.video);
+  const bf16_t* wt = static_cast<const bf16_t*>(p.w);
+  const long long plane = (long long)p.frames * p.height * p.width;
+  constexpr int kA = kGT * kGP, kB = kGN * kGP, kBuf = kA + kB;
+
+  // staging roles: A: 512 16-byte chunks (row = idx >> 2, c = idx & 3) -> 2 per thread;
+  //                B: 768 chunks -> 3 per thread
+  long long abase[2];
+  bool aval[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = tid + q * 256;
+    const int row = idx >> 2, c = idx & 3;
+    const int m = mt0 + row;
+    aval[q] = m < p.M;
+    abase[q] = token_base(p, aval[q] ? m : 0) + (long long)(c >> 1) * p.width + (c & 1) * 8;
+  }
+  auto koff_of = [&](int kk) {
+    const int step = kk >> 5;
+    const int steps_per_c = 8 * p.kt;
+    const int ci = step / steps_per_c;
+    const int sr = step - ci * steps_per_c;
+    return ci * plane + (long long)(sr >> 3) * p.height * p.width +
+           (long long)(2 * (sr & 7)) * p.width;
+  };
+  uint4 ra[2], rb[3];
+  auto fetch = [&](int kk) {
+    const long long ko = koff_of(kk);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      ra[q] = aval[q] ? *reinterpret_cast<const uint4*>(vid + abase[q] + ko) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int idx = tid + q * 256;
+      const int row = idx >> 2, c = idx & 3;
+      rb[q] = *reinterpret_cast<const uint4*>(wt + (long long)(nt0 + row) * p.K + kk + c * 8);
+    }
+  };
+  auto put = [&](int buf) {
+    bf16_t* sa = smem + buf * kBuf;
+    bf16_t* sb = sa + kA;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + q * 256;
+      *reinterpret_cast<uint4*>(sa + (idx >> 2) * kGP + (idx & 3) * 8) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int idx = tid + q * 256;
+      *reinterpret_cast<uint4*>(sb + (idx >> 2) * kGP + (idx & 3) * 8) = rb[q];
+    }
+  };
+
+  f32x4 acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  fetch(0);
+  put(0);
+  __syncthreads();
+  const int nk = p.K / 32;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) fetch((ks + 1) * 32);  // lands while this step's MFMAs run
+    const bf16_t* sa = smem + buf * kBuf;
+    const bf16_t* sb = sa + kA;
+    bf16x8 a[4], b[6];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(sa + (wm + i * 16 + r16) * kGP + kg * 8);
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(sb + (wn + j * 16 + r16) * kGP + kg * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    if (ks + 1 < nk) put(buf ^ 1);  // the other buffer's readers finished before the last barrier
+    __syncthreads();
+  }
+  // epilogue staging: round(acc + bias) as bf16 [token][channel]
+  bf16_t* stile = smem;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int nl = wn + j * 16 + r16;
+    const float bj = p.bias[nt0 + nl];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        stile[(wm + i * 16 + kg * 4 + e) * (kGN + 8) + nl] = from_f32<bf16_t>(acc[i][j][e] + bj);
+  }
+  __syncthreads();
+  const int hw = p.gh * p.gw;
+  const int per_b = p.tt * hw;
+  const bf16_t* spos = static_cast<const bf16_t*>(p.spos);
+  const bf16_t* tpos = static_cast<const bf16_t*>(p.tpos);
+  bf16_t* out = static_cast<bf16_t*>(p.out);
+  for (int idx = tid; idx < kGT * (kGN / 8); idx += 256) {
+    const int ml = idx / (kGN / 8);
+    const int c8 = (idx - ml * (kGN / 8)) * 8;
+    const int m = mt0 + ml;
+    if (m >= p.M) continue;
+    const int b = m / per_b;
+    const int rem = m - b * per_b;
+    const int t = rem / hw;
+    const int sp = rem - t * hw;
+    const int n = nt0 + c8;
+    const uint4 cv = *reinterpret_cast<const uint4*>(&stile[ml * (kGN + 8) + c8]);
+    const uint4 sv = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
+    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
+    const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w},
+                   tw[4] = {tv.x, tv.y, tv.z, tv.w};
+    uint32_t ow[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float c = __uint_as_float(h ? (cw[q] & 0xffff0000u) : (cw[q] << 16));
+        const float sp_ = __uint_as_float(h ? (sw[q] & 0xffff0000u) : (sw[q] << 16));
+        const float tp = __uint_as_float(h ? (tw[q] & 0xffff0000u) : (tw[q] << 16));
+        o[h] = round_to<bf16_t>(c + sp_) + tp;
+      }
+      ow[q] = static_cast<uint32_t>(from_f32<bf16_t>(o[0])) |
+              (static_cast<uint32_t>(from_f32<bf16_t>(o[1])) << 16);
+    }
+    *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
+        make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void patch_generic_kernel(const PatchParams p) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -284,11 +435,16 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch % 8 == 0 && width % 8 == 0 &&
                        p.K % 8 == 0 && vmhost::aligned16(video) && vmhost::aligned16(weight);
-  const char* pv = getenv("VM_PATCH_KERNEL");  // "1": the 64x64-tile kernel (A/B)
+  const char* pv = getenv("VM_PATCH_KERNEL");  // A/B: "1" 64x64 tiles, "2" 64x192 tiles
   const bool wide_ok = mfma_ok && patch == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
                        out_sb % 8 == 0 && vmhost::aligned16(out) && vmhost::aligned16(spos) &&
                        vmhost::aligned16(tpos) && !(pv && atoi(pv) == 1);
-  if (wide_ok) {
+  // the 128-token LDS-staged tiles pay off on chip-filling batches; small ones keep more,
+  // smaller workgroups (B = 1: 147 of 64 x 192 against 75 of 128 x 192)
+  if (wide_ok && !(pv && atoi(pv) == 2) && p.M >= 32768) {
+    dim3 grid((p.M + kGT - 1) / kGT, embed / kGN);
+    hipLaunchKernelGGL(patch_gemm_kernel, grid, dim3(256), 0, s, p);
+  } else if (wide_ok) {  // VM_PATCH_KERNEL=2: the 64x192 register-fragment kernel
     dim3 grid((p.M + kPT - 1) / kPT, embed / kPN);
     hipLaunchKernelGGL(patch_mfma16_kernel, grid, dim3(256), 0, s, p);
   } else if (mfma_ok) {
