@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--check-chunks", type=int, default=4,
+                    help="chunks compared against one full-sequence forward (fp32 state)")
     a = ap.parse_args()
     from videomamba_amd.videomamba import PretrainVideoMamba
 
@@ -78,6 +80,22 @@ def main():
         elapsed = time.perf_counter() - t0
     assert torch.isfinite(out.float()).all()
     tokens = a.reps * a.batch * a.frames * 196
+
+    # chunked == full: the first check-chunks chunks streamed with an fp32
+    # state against one full-sequence forward over the same frames; relative error of the
+    # patch tokens of the last chunk (the stitched prefix is the same comparison earlier)
+    rel = None
+    if a.check_chunks > 0:
+        with torch.no_grad():
+            nc = min(a.check_chunks, nchunks)
+            st = model.allocate_state(a.batch, dtype=torch.float32, device=dev)
+            for c in range(nc):
+                # add_pool_norm=False: (x_vis, next_state); x_vis is the whole chunk
+                xv, st = model(x[:, :, c * a.chunk:(c + 1) * a.chunk], ssm_state=st,
+                               temporal_pos_offset=c * a.chunk)
+            full = model(x[:, :, :nc * a.chunk])
+            ref = full[:, -xv.shape[1]:].float()
+            rel = ((xv.float() - ref).norm() / ref.norm()).item()
     print(json.dumps({
         "workload": f"VideoMamba-M {a.frames} frames as {nchunks} x chunk{a.chunk}, carried "
                     f"state, bf16, B={a.batch}",
@@ -88,6 +106,8 @@ def main():
         "chunk_first_ms": round(lat[0], 3),
         "seq_len_first_chunk": 1 + a.chunk * 196, "seq_len_next_chunks": a.chunk * 196,
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+        "chunked_vs_full_rel": rel,
+        "chunked_vs_full_frames": min(a.check_chunks, nchunks) * a.chunk,
         "data": "synthetic clips (randn), random-init weights (seed 0)",
     }), flush=True)
 
