@@ -90,9 +90,12 @@ def _pmc_traffic(shape, kernel):
     return None
 
 
-def scan_roofline(batch, reps, device, layout="tm"):
+def scan_roofline(batch, reps, device, layout="tm", delta_in_scan=True):
     """Time the scan kernel at the bench shape (layer-0 geometry, padded layout) with HIP
     events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d).
+    delta_in_scan (the model's call, selective_scan_fn(delta_bias, delta_softplus=True)):
+    the scan activates delta itself; False times it on a pre-activated delta (the
+    VM_DELTA_IN_CONV_PROJ=1 form).
     layout "tm": the model's token-major buffers (u, dt: (B*Lp, D); z inside xz (B*Lp, 2D);
     B/C inside x_dbl (B*Lp, R+2N)); "cm": channel-major (D, B*Lp) buffers."""
     from videomamba_amd import kernels as K
@@ -115,6 +118,8 @@ def scan_roofline(batch, reps, device, layout="tm"):
         z, Bm, Cm = xz[:, D:], xdbl[:, R:], xdbl[:, R + N:]
         y = torch.empty_like(u)
         s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * (R + 2 * N), 1, R + 2 * N)
+        if not delta_in_scan:
+            dt = torch.nn.functional.softplus(dt.float() + bias).to(bf)
     else:
         u = torch.randn(D, n, device=device, generator=g).to(bf)
         dt = (0.5 * torch.randn(D, n, device=device, generator=g) - 4.0).to(bf)
@@ -124,9 +129,11 @@ def scan_roofline(batch, reps, device, layout="tm"):
         y = torch.empty_like(u)
         s_u = s_z = s_bc = (Lp, n, 1)
     stream = torch.cuda.current_stream(device).cuda_stream
+    pre = layout == "tm" and not delta_in_scan
 
     def launch():
-        K.scan_raw(u, s_u, dt, s_u, A, Bm, s_bc, Cm, s_bc, Dv, z, s_z, bias, True,
+        K.scan_raw(u, s_u, dt, s_u, A, Bm, s_bc, Cm, s_bc, Dv, z, s_z, None if pre else bias,
+                   not pre,
                    h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, s_u, Lp,
                    batch, D, L, N, 1, stream)
 

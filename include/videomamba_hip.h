@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 2
+#define VM_ABI_VERSION 3
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -129,6 +129,10 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
  * e_pad <= 128); wdt_pad: (dim, r_pad) with columns >= r zero (r_pad 32 or 64).  Rows
  * with step >= seqlen are written as 0.  conv state as vm_causal_conv1d_fwd (width <= 4).
  * dim % 64 == 0, seqlen >= 1.
+ * dt_softplus != 0: `dt` receives the scan's activated step instead,
+ *   delta = softplus(float(bf16(dt)) + dt_bias[d])  (dt_bias nullable = 0), rounded to bf16
+ *   — selective_scan_fn's delta_bias / delta_softplus prologue (mamba_simple.py:30-106),
+ *   moved into the producer; pass delta_softplus = 0 and no delta_bias to the scan then.
  */
 int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                      const float* conv_weight, const float* conv_bias,
@@ -138,6 +142,7 @@ int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                      void* u, long long u_sb, long long u_sl,
                      void* xdbl, long long xd_sb, long long xd_sl,
                      void* dt, long long dt_sb, long long dt_sl,
+                     const float* dt_bias, int dt_softplus,
                      int out_len, int batch, int dim, int seqlen, int width, int dtype,
                      vm_stream_t stream);
 

@@ -413,3 +413,65 @@ def test_conv_proj_fused_dt_matches_split_bitwise(monkeypatch):
         res.append((o1, c1, o2, c2, s2))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_conv_proj_delta_softplus_epilogue(split, monkeypatch):
+    """conv_proj's dt epilogue with dt_softplus: delta = softplus(float(bf16(dt)) + bias)
+    rounded to bf16, against torch's fp64 softplus applied to the same kernel's plain dt
+    output (one bf16 rounding apart: <= 1 ulp = 2^-8 relative).  u and x_dbl unchanged
+    (bitwise); fused and split dt_proj forms both.  Includes a stateful first chunk."""
+    from videomamba_amd.mamba_simple import Mamba
+    monkeypatch.setenv("VM_CONV_PROJ_SPLIT", split)
+    torch.manual_seed(5)
+    m = Mamba(d_model=96, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    Bsz, L = 3, 301
+    Lp = (L + 7) // 8 * 8
+    n = Bsz * Lp
+    xz = torch.randn(n, 2 * Dm, device=DEV).to(torch.bfloat16)
+    cs = torch.randn(Bsz, Dm, W, device=DEV).to(torch.bfloat16)
+    A, Dv, bias, cw, cb = m._fp32_params()
+    bias = bias + torch.linspace(-12.0, 8.0, Dm, device=DEV)  # reach both softplus branches
+    wx_pad, wdt_pad = m._padded_proj_weights()
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for sp in (False, True):
+        u = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+        xd = torch.empty(n, E, device=DEV, dtype=torch.bfloat16)
+        dt = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+        K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, (cs.stride(0), cs.stride(1)),
+                        None, (0, 0), wx_pad, E, wdt_pad, R, u, (Lp * Dm, Dm), xd, (Lp * E, E),
+                        dt, (Lp * Dm, Dm), Lp, Bsz, Dm, L, W, stream,
+                        dt_bias32=bias if sp else None, dt_softplus=sp)
+        outs.append((u, xd, dt))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    want = F.softplus(outs[0][2].double() + bias.double())
+    got = outs[1][2].double()
+    assert (got > 0).all()
+    err = ((got - want).abs() / want).max().item()
+    assert err <= 2.0 ** -8, err
+
+
+def test_mixer_delta_in_conv_proj_matches_delta_in_scan(monkeypatch):
+    """Token-major bf16 mixer: delta activated in conv_proj's epilogue
+    (VM_DELTA_IN_CONV_PROJ=1) vs inside the scan (default), full sequence and two stateful chunks — they differ
+    only by delta's bf16 rounding: 1e-2 relative on outputs, 2e-2 on the fp32 state."""
+    from videomamba_amd.mamba_simple import Mamba
+    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
+    torch.manual_seed(6)
+    m = Mamba(d_model=128, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    x = torch.randn(2, 517, 128, device=DEV).to(torch.bfloat16)
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    res = []
+    for pre in ("1", "0"):
+        monkeypatch.setenv("VM_DELTA_IN_CONV_PROJ", pre)
+        with torch.no_grad():
+            full = m(x)
+            o1, (c1, s1) = m(x[:, :200], return_state=True)
+            o2, (c2, s2) = m(x[:, 200:], state=(c1, s1), return_state=True)
+        res.append((full, o1, o2, s2))
+    for a, b in zip(res[0], res[1]):
+        assert rel(a, b) < 2e-2, rel(a, b)
+    assert rel(torch.cat([res[0][1], res[0][2]], 1), res[0][0]) < 1e-2

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _P = c_void_p
 _LL = c_longlong
@@ -55,6 +55,7 @@ _SIGNATURES = {
          _P, _I, _LL, _LL, _P, _I, _LL, _LL,      # conv state in / out
          _P, _I, _I, _P, _I, _I,                  # W_x pad, e, e_pad, W_dt pad, r, r_pad
          _P, _LL, _LL, _P, _LL, _LL, _P, _LL, _LL,  # u, x_dbl, dt
+         _P, _I,                                  # dt bias, dt softplus
          _I, _I, _I, _I, _I, _I, _P], _I),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),

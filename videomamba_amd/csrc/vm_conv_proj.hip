@@ -6,6 +6,12 @@
 //     x_dbl = u @ W_x^T                                   (x_proj, (R + 2N) outputs)
 //     dt    = x_dbl[:, :R] @ W_dt^T                       (dt_proj weight; bias -> scan)
 // with the reference's rounding points (u, x_dbl, dt in bf16; fp32 accumulation).
+// Optionally (dt_softplus) the dt epilogue also applies the scan's delta activation,
+//     delta = softplus(float(bf16(dt)) + dt_bias)  -> bf16,
+// the reference's selective_scan_fn(delta_bias=..., delta_softplus=True) prologue
+// (mamba_simple.py:109-172 / :30-106), so the scan streams a ready delta and spends no
+// transcendentals on it: the activation moves into a kernel whose VALU sits idle behind
+// its memory waits, and the scan (issue-bound) drops ~7 % per launch.
 //
 // One workgroup (4 waves) owns 64 token rows of the flattened (batch * Lp) axis and sweeps
 // the channels in chunks of 64:
@@ -34,6 +40,7 @@ struct ConvProjParams {
   const bf16_t* wx;   // (e_pad, D) zero-padded rows
   const bf16_t* wdt;  // (D, r_pad) zero-padded columns
   bf16_t* u; bf16_t* xdbl; bf16_t* dt;
+  const float* dtb;  // dt bias (nullable), used with SPD
   long long xz_sb, xz_sl, csi_sb, csi_sd, cso_sb, cso_sd;
   long long u_sb, u_sl, xd_sb, xd_sl, dt_sb, dt_sl;
   int batch, dim, seqlen, lp, rows, e, e_pad, r, r_pad, width, csi_dtype, cso_dtype;
@@ -64,9 +71,29 @@ __device__ __forceinline__ float silu_f(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2e));
 }
 
-template <int SW = 16, int NW = 4>
+// dt epilogue: bf16 dt (the reference's rounding point), or with SPD the activated
+// delta = softplus(float(bf16(dt)) + bias) rounded to bf16
+// softplus(x) = log1p(e^x) with log1p by the u = 1 + w correction (exact where 1 + w
+// rounds to 1, a few ulp elsewhere): unlike softplus_fast it keeps full relative precision
+// for small deltas — affordable here, where the VALU waits on memory anyway.
+__device__ __forceinline__ float softplus_acc(float x) {
+  if (x > 20.0f) return x;
+  const float w = __builtin_amdgcn_exp2f(x * kLog2e);
+  const float u = 1.0f + w;
+  const float d = u - 1.0f;
+  return d == 0.0f ? w : __builtin_amdgcn_logf(u) * 0.6931471805599453f * (w * __builtin_amdgcn_rcpf(d));
+}
+template <bool SPD>
+__device__ __forceinline__ bf16_t dt_out(float acc, float bias) {
+  const bf16_t v = from_f32<bf16_t>(acc);
+  if constexpr (SPD) return from_f32<bf16_t>(softplus_acc(to_f32(v) + bias));
+  return v;
+}
+
+template <int SW = 16, int NW = 4, bool SPD = false>
 __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
                                          int row0, int lane, int wave);
+template <bool SPD>
 __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
                                               bf16_t* sU, int row0, int lane, int wave);
 
@@ -75,7 +102,8 @@ __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf1
 // and bias (D) as fp32.
 // EXP (tools/probes/cp_lab.hip only; 0 in the library) removes pieces to price them:
 // 1 W_x staging loads, 2 x_proj MFMAs, 4 u stores, 8 conv window loads, 16 loop barriers.
-template <bool DT, int NB, int EXP = 0>  // DT: also run dt_proj here; NB = e_pad / 16 blocks
+// SPD: the dt epilogue emits softplus(dt + bias) (see the header)
+template <bool DT, int NB, int EXP = 0, bool SPD = false>  // DT: also run dt_proj here; NB = e_pad / 16 blocks
 __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
   // sU: W_x chunk (<= 128 rows x kCPPad) / x_dbl tile (64 x 2*kCPPad); with DT also the
   // per-wave dt staging (4 x 64 x kCPPad)
@@ -227,14 +255,14 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
   }
   if constexpr (DT) {
     __syncthreads();  // sU is reused below as per-wave output staging
-    dt_phase_half(p, sA, sU, row0, lane, wave);
+    dt_phase_half<SPD>(p, sA, sU, row0, lane, wave);
   }
 }
 
 // dt_proj for one 64-token tile: A = x_dbl[:, :R] (zero-padded to r_pad) in sA,
 // wave = 64-column blocks wave, wave+NW, ...; outputs staged per wave in sU and stored as
 // 128-byte row segments, SW bytes per lane-store.
-template <int SW, int NW>
+template <int SW, int NW, bool SPD>
 __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
                                          int row0, int lane, int wave) {
   const int D = p.dim;
@@ -248,6 +276,9 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
           &sA[(i * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
   bf16_t* stg = sU + wave * kCPTok * kCPPad;
   for (int cb = wave; cb * 64 < D; cb += NW) {
+    float bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = SPD && p.dtb ? p.dtb[cb * 64 + j * 16 + (lane & 15)] : 0.0f;
     f32x4 d[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -274,7 +305,7 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
-              from_f32<bf16_t>(d[i][j][e]);
+              dt_out<SPD>(d[i][j][e], bj[j]);
     // the wave reads back its own staging tile: 64 rows x 128 B
     if constexpr (SW == 16) {
 #pragma unroll
@@ -311,12 +342,16 @@ __device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* 
 // dt_proj inside conv_proj (DT): as dt_phase, but each 64-column block in two 32-row
 // halves, so the per-wave staging is 32 rows and the fused kernel keeps conv_proj's LDS
 // budget (3 workgroups per CU) and half the accumulators.
+template <bool SPD>
 __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
                                               bf16_t* sU, int row0, int lane, int wave) {
   const int D = p.dim;
   const int ksteps = p.r_pad / 32;
   bf16_t* stg = sU + wave * 32 * kCPPad;
   for (int cb = wave; cb * 64 < D; cb += 4) {
+    float bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = SPD && p.dtb ? p.dtb[cb * 64 + j * 16 + (lane & 15)] : 0.0f;
     bf16x8 bw[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -353,7 +388,7 @@ __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf1
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
-                from_f32<bf16_t>(d[i][j][e]);
+                dt_out<SPD>(d[i][j][e], bj[j]);
       // 32 rows x 128 B out, 16 B per lane-store
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -388,7 +423,7 @@ __global__ __launch_bounds__(256) void conv_state_out_kernel(const ConvProjParam
 
 // dt = x_dbl[:, :R] @ W_dt^T for 64-token tiles (the split form of conv_proj_kernel<true>).
 // NW waves share a tile's 64-column blocks (D = 1152: 18 blocks, 3 per wave at NW = 6).
-template <int SW = 16, int NW = 4>
+template <int SW = 16, int NW = 4, bool SPD = false>
 __global__ __launch_bounds__(64 * NW) void dt_proj_kernel(const ConvProjParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
   __shared__ __attribute__((aligned(16))) bf16_t sU[NW * kCPTok * kCPPad];
@@ -403,7 +438,7 @@ __global__ __launch_bounds__(64 * NW) void dt_proj_kernel(const ConvProjParams p
     sA[lr * kCPPad + k] = row < p.rows ? p.xdbl[(long long)row * p.xd_sl + k] : bf16_t(0);
   }
   __syncthreads();
-  dt_phase<SW, NW>(p, sA, sU, row0, tid & 63, tid >> 6);
+  dt_phase<SW, NW, SPD>(p, sA, sU, row0, tid & 63, tid >> 6);
 }
 
 }  // namespace vm
@@ -419,7 +454,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
                                 void* u, long long u_sb, long long u_sl,
                                 void* xdbl, long long xd_sb, long long xd_sl,
                                 void* dt, long long dt_sb, long long dt_sl,
-                                int out_len, int batch, int dim, int seqlen, int width, int dtype,
+                                const float* dt_bias, int dt_softplus, int out_len, int batch, int dim, int seqlen, int width, int dtype,
                                 vm_stream_t stream) {
   if (!xz || !conv_weight || !wx_pad || !wdt_pad || !u || !xdbl || !dt) {
     vmhost::set_error("vm_conv_proj_fwd: null required pointer");
@@ -457,6 +492,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   p.wx = static_cast<const bf16_t*>(wx_pad); p.wdt = static_cast<const bf16_t*>(wdt_pad);
   p.u = static_cast<bf16_t*>(u); p.xdbl = static_cast<bf16_t*>(xdbl);
   p.dt = static_cast<bf16_t*>(dt);
+  p.dtb = dt_bias;
   p.xz_sb = xz_sb; p.xz_sl = xz_sl; p.csi_sb = csi_sb; p.csi_sd = csi_sd;
   p.cso_sb = cso_sb; p.cso_sd = cso_sd;
   p.u_sb = u_sb; p.u_sl = u_sl; p.xd_sb = xd_sb; p.xd_sl = xd_sl; p.dt_sb = dt_sb; p.dt_sl = dt_sl;
@@ -470,11 +506,13 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   // runs it as its own kernel instead (bit-identical output)
   const char* split = getenv("VM_CONV_PROJ_SPLIT");
   const bool fused_dt = !(split && atoi(split) == 1);
+  const bool spd = dt_softplus != 0;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
   switch (e_pad / 16) {  // x_proj output blocks
 #define VM_CP_CASE(NBV)                                              \
     case NBV:                                                        \
-      if (fused_dt) go(conv_proj_kernel<true, NBV>);                 \
+      if (fused_dt && spd) go(conv_proj_kernel<true, NBV, 0, true>); \
+      else if (fused_dt) go(conv_proj_kernel<true, NBV>);            \
       else go(conv_proj_kernel<false, NBV>);                         \
       break;
     VM_CP_CASE(1) VM_CP_CASE(2) VM_CP_CASE(3) VM_CP_CASE(4)
@@ -482,7 +520,8 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
 #undef VM_CP_CASE
   }
   // conv + x_proj at lower register pressure, then dt_proj from x_dbl
-  if (!fused_dt) hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, st, p);
+  if (!fused_dt && spd) hipLaunchKernelGGL((dt_proj_kernel<16, 4, true>), grid, dim3(256), 0, st, p);
+  else if (!fused_dt) hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, st, p);
   if (cs_out)
     hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
   return vmhost::launch_status("vm_conv_proj_fwd");

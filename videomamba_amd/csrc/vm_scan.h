@@ -23,17 +23,6 @@ struct ScanParams {
   int vec_bc;  // B/C rows allow 8-element vector access
 };
 
-// softplus / silu from the hardware exp2 / log2 / rcp.  softplus = ln2*log2(1 + 2^(x/ln2))
-// is within ~1.2e-7 absolute of log1p(exp(x)) (the relative error grows only where the
-// step itself is < 1e-4 and contributes nothing measurable); threshold 20 as torch.
-__device__ __forceinline__ float softplus_fast(float x) {
-  return x > 20.0f ? x
-                   : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x * kLog2e)) *
-                         0.6931471805599453f;
-}
-__device__ __forceinline__ float silu_fast(float z) {
-  return z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * kLog2e));
-}
 
 // Token-major path (vm_scan_seq.hip).  Workspace for the time-segmented form, in bytes;
 // 0 when the single-pass form is chosen.  `segments` receives the chosen segment count.

@@ -146,10 +146,12 @@ def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, b
 
 
 def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, wdt_pad, r,
-                  u, u_s, xdbl, xd_s, dt, dt_s, out_len, batch, dim, seqlen, width, stream):
+                  u, u_s, xdbl, xd_s, dt, dt_s, out_len, batch, dim, seqlen, width, stream,
+                  dt_bias32=None, dt_softplus=False):
     """Fused token-major conv1d + SiLU -> x_proj -> dt_proj (bf16).  *_s = (batch, step)
     element strides of the token-major buffers; wx_pad (e_pad, D) / wdt_pad (D, r_pad) are
-    zero-padded copies of the projection weights."""
+    zero-padded copies of the projection weights.  dt_softplus: `dt` receives the scan's
+    activated step softplus(dt + dt_bias32) instead (the scan then runs without them)."""
     lib = _lib.load()
     rc = lib.vm_conv_proj_fwd(
         _p(xz), xz_s[0], xz_s[1], _p(cw32), _p(cb32),
@@ -157,7 +159,7 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
         _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
         _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad), r, wdt_pad.shape[1],
         _p(u), u_s[0], u_s[1], _p(xdbl), xd_s[0], xd_s[1], _p(dt), dt_s[0], dt_s[1],
-        out_len, batch, dim, seqlen, width, dtype_code(u.dtype), stream)
+        _p(dt_bias32), int(dt_softplus), out_len, batch, dim, seqlen, width, dtype_code(u.dtype), stream)
     _lib.check(rc, "vm_conv_proj_fwd")
 
 

@@ -261,14 +261,22 @@ class Mamba(nn.Module):
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
                  if conv_state_out is not None else (0, 0))
+        scan_bias, scan_softplus = dbias, True
         if self._fused_conv_proj_ok(hn, seqlen):
-            # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip)
+            # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip).
+            # VM_DELTA_IN_CONV_PROJ=1 moves the scan's delta activation softplus(dt + bias)
+            # into its dt epilogue: measured a wash at B = 336 (scan -222 us, conv_proj
+            # +385 us per layer, profiles/r01f_delta_placement.txt), so it stays in the scan
             wx_pad, wdt_pad = self._padded_proj_weights()
             x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
             dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            pre = os.getenv("VM_DELTA_IN_CONV_PROJ", "0") == "1"
             K.conv_proj_raw(xz, s_xz[::2], cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                             wx_pad, E, wdt_pad, R, u, s_u[::2], x_dbl, (Lp * E, E), dt,
-                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream)
+                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream,
+                            dt_bias32=dbias if pre else None, dt_softplus=pre)
+            if pre:
+                scan_bias, scan_softplus = None, False
         else:
             K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                        u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
@@ -276,7 +284,7 @@ class Mamba(nn.Module):
             dt = _linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
         y = torch.empty_like(u)
         K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
-                   xz[:, Dm:], s_xz, dbias, True,
+                   xz[:, Dm:], s_xz, scan_bias, scan_softplus,
                    h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
                    h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
                    y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
