@@ -16,6 +16,8 @@
  *   vm_conv_proj_fwd           <- causal_conv1d_fn + x_proj + dt_proj, fused, token-major
  *                                 (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
+ *   vm_out_proj_add_norm_fwd   <- out_proj (mamba_simple.py:445-446) + the next block's
+ *                                 fused add + norm (videomamba.py:152-166)
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
  *                                 (videomamba.py:359-368, :806-815)
@@ -145,6 +147,22 @@ int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                      const float* dt_bias, int dt_softplus,
                      int out_len, int batch, int dim, int seqlen, int width, int dtype,
                      vm_stream_t stream);
+
+/*
+ * out_proj GEMM + the next block's fused residual add + RMSNorm / LayerNorm
+ * (mamba_simple.py:445-446 then videomamba.py:152-166 / mamba-ssm rms_norm_fn, prenorm):
+ *   hidden = bf16(y @ w_out^T);  s = hidden + residual (fp32);  out = bf16(norm(s) * w + b)
+ *   residual_out = s.
+ * y: (rows, k) bf16, row stride y_sl; w_out: (n, k) bf16 (nn.Linear weight, contiguous);
+ * residual / residual_out: (rows, n) fp32, contiguous, nullable, may alias; out: (rows, n)
+ * bf16.  norm_bias nullable (RMSNorm ignores it); is_rms selects RMSNorm.
+ * k % 32 == 0, n % 64 == 0, n <= 768.
+ */
+int vm_out_proj_add_norm_fwd(const void* y, long long y_sl, const void* w_out,
+                             const float* residual, const float* norm_weight,
+                             const float* norm_bias, void* out, float* residual_out,
+                             long long rows, int n, int k, float eps, int is_rms,
+                             vm_stream_t stream);
 
 /*
  * One-token conv step: shift conv_state left by one, append x, dot with weight (+bias),

@@ -57,6 +57,8 @@ _SIGNATURES = {
          _P, _LL, _LL, _P, _LL, _LL, _P, _LL, _LL,  # u, x_dbl, dt
          _P, _I,                                  # dt bias, dt softplus
          _I, _I, _I, _I, _I, _I, _P], _I),
+    "vm_out_proj_add_norm_fwd": (
+        [_P, _LL, _P, _P, _P, _P, _P, _P, _LL, _I, _I, ctypes.c_float, _I, _P], _I),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_add_norm_fwd": (

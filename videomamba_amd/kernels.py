@@ -163,6 +163,18 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
     _lib.check(rc, "vm_conv_proj_fwd")
 
 
+def out_norm_raw(y, y_sl, w_out, residual, nw32, nb32, out, residual_out, rows, eps, is_rms,
+                 stream):
+    """out_proj GEMM + residual add + RMSNorm/LayerNorm in one launch (bf16 y / w_out,
+    fp32 residual); see vm_out_proj_add_norm_fwd."""
+    lib = _lib.load()
+    n, k = w_out.shape
+    rc = lib.vm_out_proj_add_norm_fwd(_p(y), y_sl, _p(w_out), _p(residual), _p(nw32), _p(nb32),
+                                      _p(out), _p(residual_out), rows, n, k, float(eps),
+                                      int(is_rms), stream)
+    _lib.check(rc, "vm_out_proj_add_norm_fwd")
+
+
 def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_rms, stream):
     lib = _lib.load()
     rc = lib.vm_add_norm_fwd(
