@@ -80,7 +80,8 @@ def _oracle_scan(Bz, D, L, N):
     return _ORACLE_CACHE[key]
 
 
-SCAN_VARIANTS = ["0", "1", "5", "6", "13", "14", "15", "16", "17", "18", "19"]
+SCAN_VARIANTS = ["0", "1", "5", "6", "13", "14", "15", "16", "17", "18", "19",
+                 "30", "31", "32", "33", "34", "35", "36", "37"]  # 30-35: v5 with the states split over waves
 
 
 @pytest.fixture(params=SCAN_VARIANTS)

@@ -755,12 +755,18 @@ __device__ __forceinline__ void store_even(T* row, int t0, int LO, bool vec, con
 // PIPE (bf16, small grids: one workgroup per CU): the next time block's B/C rows and
 // u / delta / z are loaded into registers while the current block computes, so a block
 // no longer waits on its own global loads (three round trips per block otherwise).
-template <typename T, int K, int NW, bool PIPE = false>
+// S > 1 (small grids): the 16 states of a channel are split over S waves (16/S each); the
+// waves' partial y sums meet in LDS and the first wave of the channel gates and stores.
+// A B = 1 chunk then runs S times as many waves, each with 1/S of the state chains.
+template <typename T, int K, int NW, bool PIPE = false, int S = 1>
 __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   static_assert(K % 2 == 0, "K must be even");
   static_assert(!PIPE || sizeof(T) == 2, "the pipelined form keeps bf16 words");
+  static_assert(NW % S == 0 && kMaxN % S == 0, "whole channels per workgroup");
   constexpr int TB = 64 * K;
   constexpr int K2 = K / 2;
+  constexpr int NS = kMaxN / S;  // states per wave
+  constexpr int NCH = NW / S;    // channels per workgroup
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sB = smem;                 // [N][K2][64][2]
   float* sC = smem + kMaxN * TB;
@@ -768,8 +774,9 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sg = S > 1 ? wave % S : 0;  // state group
   const int b = blockIdx.y;
-  const int d_raw = blockIdx.x * NW + wave;
+  const int d_raw = blockIdx.x * NCH + wave / S;
   const bool active = d_raw < p.dim;
   const int d = active ? d_raw : p.dim - 1;
   const int N = p.dstate;
@@ -784,11 +791,12 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
   const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
   const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
 
-  float A2[kMaxN], carry[kMaxN];  // wave-uniform (SGPRs)
+  float A2[NS], carry[NS];  // wave-uniform (SGPRs): this wave's states sg*NS ..
 #pragma unroll
-  for (int n = 0; n < kMaxN; ++n) {
-    A2[n] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
-    carry[n] = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
+  for (int nn = 0; nn < NS; ++nn) {
+    const int n = sg * NS + nn;
+    A2[nn] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
+    carry[nn] = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
   }
   const float Dv = p.D ? p.D[d] : 0.0f;
   const float bias = p.dbias ? p.dbias[d] : 0.0f;
@@ -919,7 +927,7 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
         dd = (t0 + k < L) ? dd : 0.0f;
         dl[k] = dd;
         du[k] = dd * uv[k];
-        y[k] = Dv * uv[k];
+        y[k] = sg == 0 ? Dv * uv[k] : 0.0f;
       }
     }
     float sd = 0.0f;
@@ -934,7 +942,8 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
 
     // ---- states ----
 #pragma unroll
-    for (int n = 0; n < kMaxN; ++n) {
+    for (int nn = 0; nn < NS; ++nn) {
+      const int n = sg * NS + nn;
       if (n < N) {
         const float* bs = sB + n * TB + lane * 2;
         float a[K], bb[K];
@@ -945,13 +954,13 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const int k = 2 * k2 + i;
-            a[k] = __builtin_amdgcn_exp2f(dl[k] * A2[n]);
+            a[k] = __builtin_amdgcn_exp2f(dl[k] * A2[nn]);
             bb[k] = du[k] * (i ? v.y : v.x);
             fold = fmaf(a[k], fold, bb[k]);
           }
         }
-        const float e1 = __builtin_amdgcn_exp2f(sd * A2[n]);
-        if (lane == 0) fold = fmaf(e1, carry[n], fold);
+        const float e1 = __builtin_amdgcn_exp2f(sd * A2[nn]);
+        if (lane == 0) fold = fmaf(e1, carry[nn], fold);
         const float e2 = e1 * dppz<0x111>(e1);
         const float e4 = e2 * dppz<0x112>(e2);
         const float e8 = e4 * dppz<0x114>(e4);
@@ -959,11 +968,11 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
         fold = fmaf(e2, dppz<0x112>(fold), fold);
         fold = fmaf(e4, dppz<0x114>(fold), fold);
         fold = fmaf(e8, dppz<0x118>(fold), fold);
-        fold = fmaf(__builtin_amdgcn_exp2f(srow * A2[n]), dppz<0x142, 0xa>(fold), fold);
-        fold = fmaf(__builtin_amdgcn_exp2f(shalf * A2[n]), dppz<0x143, 0xc>(fold), fold);
+        fold = fmaf(__builtin_amdgcn_exp2f(srow * A2[nn]), dppz<0x142, 0xa>(fold), fold);
+        fold = fmaf(__builtin_amdgcn_exp2f(shalf * A2[nn]), dppz<0x143, 0xc>(fold), fold);
         float h = dppz<0x138>(fold);
-        if (lane == 0) h = carry[n];
-        carry[n] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold), 63));
+        if (lane == 0) h = carry[nn];
+        carry[nn] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold), 63));
         const float* cs = sC + n * TB + lane * 2;
 #pragma unroll
         for (int k2 = 0; k2 < K2; ++k2) {
@@ -978,7 +987,21 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
       }
     }
 
-    if (zrow) {
+    if constexpr (S > 1) {  // partial y of the other state groups -> the channel's first wave
+      float* red = smem + 2 * kMaxN * TB;  // [NW][K][64]
+      if (sg != 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[(wave * K + k) * 64 + lane] = y[k];
+      }
+      __syncthreads();
+      if (sg == 0) {
+#pragma unroll
+        for (int g = 1; g < S; ++g)
+#pragma unroll
+          for (int k = 0; k < K; ++k) y[k] += red[((wave + g) * K + k) * 64 + lane];
+      }
+    }
+    if (zrow && sg == 0) {
       float zv[K];
       if constexpr (PIPE) unpack_even<K>(cz, zv);
       else load_even<T, K>(zrow, t0, L, vx, zv);
@@ -987,14 +1010,25 @@ __global__ __launch_bounds__(64 * NW) void scan_v5_kernel(const ScanParams p) {
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
-    if (active && t0 < LO) store_even<T, K>(orow, t0, LO, vx, y);
+    if (active && sg == 0 && t0 < LO) store_even<T, K>(orow, t0, LO, vx, y);
   }
 
   if (p.hl && active && lane == 0) {
 #pragma unroll
-    for (int n = 0; n < kMaxN; ++n)
-      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[n]);
+    for (int nn = 0; nn < NS; ++nn) {
+      const int n = sg * NS + nn;
+      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[nn]);
+    }
   }
+}
+
+// State-split form (S waves per channel, NW waves per workgroup), pipelined for bf16.
+template <typename T, int K, int NW, int S>
+static void launch_v5_split(const ScanParams& p, hipStream_t s) {
+  const size_t lds = (2 * kMaxN * 64 * K + NW * K * 64) * sizeof(float);
+  constexpr int NCH = NW / S;
+  dim3 grid((p.dim + NCH - 1) / NCH, p.batch);
+  hipLaunchKernelGGL((scan_v5_kernel<T, K, NW, sizeof(T) == 2, S>), grid, dim3(64 * NW), lds, s, p);
 }
 
 // pipe: -1 auto (bf16 grids of at most one workgroup per CU), 0 off, 1 on (bf16 only)
@@ -1022,7 +1056,12 @@ static void launch_v5_auto(const ScanParams& p, hipStream_t s) {
     const double tb = 64.0 * k;
     return ((p.out_len + tb - 1) / tb) * tb * (1.0 + 4.0 / k);
   };
-  if (cost(10) <= cost(8)) launch_v5<T, 10, 8>(p, s);
+  // Grids of at most one workgroup per CU (e.g. the B = 1 streaming chunk): the states
+  // split over two waves per channel (variant 30).  Measured at M (D = 1152, L = 3137,
+  // profiles/r01f_v5_state_split.txt): B = 1 58.0 -> 48.5 us, B = 2 equal, B >= 4 slower.
+  const long long wgs = static_cast<long long>((p.dim + 7) / 8) * p.batch;
+  if (sizeof(T) == 2 && wgs <= 256 && cost(10) <= cost(8)) launch_v5_split<T, 10, 10, 2>(p, s);
+  else if (cost(10) <= cost(8)) launch_v5<T, 10, 8>(p, s);
   else launch_v5<T, 8, 8>(p, s);
 }
 
@@ -1277,6 +1316,14 @@ static void dispatch_scan(const ScanParams& p, hipStream_t s) {
     case 17: launch_v5<T, 8, 8>(p, s); break;
     case 18: launch_v5<T, 10, 8>(p, s, 0); break;     // v5 K=10 without the pipelined form
     case 19: launch_v5<T, 10, 8>(p, s, 1); break;     // v5 K=10 pipelined at any grid (bf16)
+    case 30: launch_v5_split<T, 10, 10, 2>(p, s); break;  // states split over 2 waves
+    case 31: launch_v5_split<T, 10, 12, 2>(p, s); break;
+    case 32: launch_v5_split<T, 10, 16, 2>(p, s); break;
+    case 33: launch_v5_split<T, 10, 16, 4>(p, s); break;  // ... over 4 waves
+    case 34: launch_v5_split<T, 10, 12, 4>(p, s); break;
+    case 35: launch_v5_split<T, 8, 16, 4>(p, s); break;
+    case 36: launch_v5_split<T, 8, 8, 2>(p, s); break;   // 80 KB LDS: two workgroups per CU
+    case 37: launch_v5_split<T, 8, 6, 2>(p, s); break;
     default: launch_v5_auto<T>(p, s); break;          // v5: scalar, K chosen per L
   }
 }
