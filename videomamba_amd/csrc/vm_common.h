@@ -75,6 +75,7 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x));
 __device__ __forceinline__ float softplus(float x) { return x <= 20.0f ? log1pf(__expf(x)) : x; }
 
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2f = 0.6931471805599453f;
 
 // softplus / silu from the hardware exp2 / log2 / rcp.  softplus = ln2*log2(1 + 2^(x/ln2))
 // is within ~1.2e-7 absolute of log1p(exp(x)) (the relative error grows only where the

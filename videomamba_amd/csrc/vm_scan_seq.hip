@@ -100,15 +100,24 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const int t_end = min(L, t_beg + w.seg_len);
   const long long ws_row = (static_cast<long long>(b) * w.S + seg) * p.dim + d;
 
+  // LG (single pass with softplus): delta is carried in log2 units, dl' = softplus(x)*log2e
+  // = log2(1 + 2^(x*log2e)), so the exp argument is dl'*A with A unscaled and the softplus
+  // loses its two scaling multiplies.  Then du' = du*log2e, so the states run as
+  // h' = h*log2e (converted once at entry and exit), D is pre-scaled the same way, and the
+  // output's ln2 factor rides on the SiLU gate's 1+e term as an FMA.
+  constexpr bool LG = MODE == 0 && SP;
+  const float lg_in = LG ? kLog2e : 1.0f;
+
   // state pairs (n, n+1) live in f2 register pairs: scalar code addresses .x / .y, the
   // packed form operates on whole pairs
   f2 A2[kMaxN / 2], h[kMaxN / 2];
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) {
-    const float a = n < N ? p.A[d * N + n] * kLog2e : 0.0f;
+    const float a = n < N ? p.A[d * N + n] * (LG ? 1.0f : kLog2e) : 0.0f;
     float h_init = 0.0f;
     if constexpr (MODE == 0) {
-      if (n < N && p.h0) h_init = load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype);
+      if (n < N && p.h0)
+        h_init = load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * lg_in;
     }
     if constexpr (MODE == 2) h_init = w.hin[ws_row * kMaxN + n];
     if (n & 1) {
@@ -119,8 +128,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       h[n >> 1].x = h_init;
     }
   }
-  const float Dv = p.D ? p.D[d] : 0.0f;
-  const float bias = p.dbias ? p.dbias[d] : 0.0f;
+  const float Dv = (p.D ? p.D[d] : 0.0f) * lg_in;
+  const float bias = (p.dbias ? p.dbias[d] : 0.0f) * lg_in;
   // Wave-uniform row bases (buffer descriptors) + the lane's channel byte offset.
   const int d0 = __builtin_amdgcn_readfirstlane((blockIdx.x * NW + wave) * 64 < p.dim
                                                     ? (blockIdx.x * NW + wave) * 64
@@ -242,10 +251,27 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       // sink them below all eight steps, collapsing the prefetch distance to zero
       // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
       __builtin_amdgcn_sched_barrier(0);
-      float dl = dr + bias;
-      if (SP) dl = softplus_fast(dl);
+      float dl;
+      if constexpr (LG) {
+        const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
+        dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
+      } else {
+        dl = dr + bias;
+        if (SP) dl = softplus_fast(dl);
+      }
       dl = live ? dl : 0.0f;
       const float du = dl * uu;
+      // output gate; under LG it also carries y's ln2 factor: z / ((1 + e) * log2e)
+      auto gate = [&](float y) {
+        if constexpr (LG) {
+          if (HZ)
+            return y * (zz * __builtin_amdgcn_rcpf(
+                                 fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)));
+          return y * kLn2f;
+        } else {
+          return HZ ? y * silu_fast(zz) : y;
+        }
+      };
       if constexpr (PK) {
         const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
         const f2 dl2 = {dl, dl}, du2 = {du, du};
@@ -272,8 +298,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
           sdel += dl;
         } else {
           const f2 ys = ya + yb;
-          float y = ys.x + ys.y;
-          if (HZ) y *= silu_fast(zz);
+          const float y = gate(ys.x + ys.y);
           bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
         }
         return;
@@ -320,8 +345,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
           y0 = fmaf(h[q].x, Cv[2 * q], y0);
           y1 = fmaf(h[q].y, Cv[2 * q + 1], y1);
         }
-        float y = y0 + y1;
-        if (HZ) y *= silu_fast(zz);
+        const float y = gate(y0 + y1);
         // unconditional store (a branch here makes the loop-carried vmcnt accounting
         // conservative): dead lanes / steps get an out-of-range voffset instead
         bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
@@ -409,7 +433,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
 #pragma unroll
         for (int n = 0; n < kMaxN; ++n)
           if (n < N)
-            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, (n & 1) ? h[n >> 1].y : h[n >> 1].x);
+            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
+                      ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * (LG ? kLn2f : 1.0f));
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
     }
