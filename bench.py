@@ -11,9 +11,14 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
-Other configs: --config m32 (VideoMamba-M 32x224^2, the C4 clip shape; run under torchrun
-for the 8-GPU batch-sharded case), --config ti8 --full-sequence (C2).  The roofline block
-is always the scan at the M-16f shape.
+Other configs: --config m32 (VideoMamba-M 32x224^2, C4: a GLOBAL batch, --global-batch,
+default 672 clips, split across ranks with sharding.shard_range — strong scaling; run under
+torchrun for the 8-GPU case), --config ti8 --full-sequence (C2).  The roofline block is
+always the scan at the M-16f shape.
+
+--stub-cpu replaces the encoder by a trivial CPU op and runs the same rank / barrier /
+max-over-ranks / JSON-line control flow on the gloo backend (tests/test_sharding_gloo.py
+launches it under torchrun with 2 ranks).
 
 Extra fields: chunk_p50_ms (B=1 chunk latency, HIP-graph replay; chunk_p50_eager_ms the
 eager launch path), roofline of the selective-scan kernel
@@ -48,8 +53,10 @@ LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
     "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),  # C3 (default)
-    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M"),  # C4 clip shape
-    "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti"),  # C1 / C2 shape
+    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M",  # C4
+                global_batch=672),
+    "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti",  # C1 / C2 shape
+                batch=512),
 }
 
 
@@ -58,7 +65,11 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=336, help="clips per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU (C3, weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="clips split across all ranks (C4, strong scaling)")
+    ap.add_argument("--stub-cpu", action="store_true",
+                    help="CPU/gloo control-flow check with the encoder stubbed out")
     ap.add_argument("--config", default="m16", choices=sorted(CONFIGS))
     ap.add_argument("--p50-chunks", type=int, default=100)
     ap.add_argument("--scan-reps", type=int, default=50)
@@ -66,7 +77,11 @@ def _args():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--full-sequence", action="store_true",
                     help="stateless full-sequence forward (C2) instead of a stateful chunk")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.batch_default = a.batch is None
+    if a.batch is None:
+        a.batch = CONFIGS[a.config].get("batch", 336)
+    return a
 
 
 def _sync_barrier(world):
@@ -90,12 +105,10 @@ def _pmc_traffic(shape, kernel):
     return None
 
 
-def scan_roofline(batch, reps, device, layout="tm", delta_in_scan=True):
+def scan_roofline(batch, reps, device, layout="tm"):
     """Time the scan kernel at the bench shape (layer-0 geometry, padded layout) with HIP
-    events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d).
-    delta_in_scan (the model's call, selective_scan_fn(delta_bias, delta_softplus=True)):
-    the scan activates delta itself; False times it on a pre-activated delta (the
-    VM_DELTA_IN_CONV_PROJ=1 form).
+    events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d).  The
+    scan activates delta itself (the model's call: delta_bias, delta_softplus=True).
     layout "tm": the model's token-major buffers (u, dt: (B*Lp, D); z inside xz (B*Lp, 2D);
     B/C inside x_dbl (B*Lp, R+2N)); "cm": channel-major (D, B*Lp) buffers."""
     from videomamba_amd import kernels as K
@@ -118,8 +131,6 @@ def scan_roofline(batch, reps, device, layout="tm", delta_in_scan=True):
         z, Bm, Cm = xz[:, D:], xdbl[:, R:], xdbl[:, R + N:]
         y = torch.empty_like(u)
         s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * (R + 2 * N), 1, R + 2 * N)
-        if not delta_in_scan:
-            dt = torch.nn.functional.softplus(dt.float() + bias).to(bf)
     else:
         u = torch.randn(D, n, device=device, generator=g).to(bf)
         dt = (0.5 * torch.randn(D, n, device=device, generator=g) - 4.0).to(bf)
@@ -129,11 +140,9 @@ def scan_roofline(batch, reps, device, layout="tm", delta_in_scan=True):
         y = torch.empty_like(u)
         s_u = s_z = s_bc = (Lp, n, 1)
     stream = torch.cuda.current_stream(device).cuda_stream
-    pre = layout == "tm" and not delta_in_scan
 
     def launch():
-        K.scan_raw(u, s_u, dt, s_u, A, Bm, s_bc, Cm, s_bc, Dv, z, s_z, None if pre else bias,
-                   not pre,
+        K.scan_raw(u, s_u, dt, s_u, A, Bm, s_bc, Cm, s_bc, Dv, z, s_z, bias, True,
                    h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, s_u, Lp,
                    batch, D, L, N, 1, stream)
 
@@ -206,9 +215,89 @@ def cpu_baseline(cfg, threads):
                              f"of 3 after 1 warm-up ({dt_c1:.2f} s)"}}
 
 
+def _timed_steps(step, steps, warmup, world, device, sync):
+    """W untimed steps, then K steps bracketed by barrier + device sync on both sides;
+    returns the slowest rank's elapsed seconds (max over ranks)."""
+    from videomamba_amd.sharding import max_over_ranks
+
+    def barrier():
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+
+    out = None
+    with torch.no_grad():
+        for _ in range(warmup):
+            out = step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    return max_over_ranks(elapsed, device), out
+
+
+def _base_line(args, cfg, world, global_batch, per_rank, elapsed, strong):
+    T = cfg["frames"]
+    ms_per_step = elapsed / args.steps * 1e3
+    value = global_batch * T * 196 * args.steps / elapsed
+    return {
+        "metric": "video-tokens/sec per GPU + streaming-chunk p50 latency, VideoMamba-M 16f 224",
+        "value": round(value, 1), "unit": "video-tokens/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "strong" if strong else "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic clips (randn), random-init weights (seed 0)",
+        "config": {"workload": f"{cfg['name']} {T}x224^2 bf16, " + (
+                       "full-sequence forward per step" if args.full_sequence else
+                       "one stateful streaming chunk (chunk_size 32) per step"),
+                   "model": cfg["name"], "global_batch": global_batch,
+                   "per_gpu_batch": per_rank, "frames": T, "seq_len": 1 + T * 196,
+                   "parallelism": f"batch-sharded x{world}, no data-path collectives"},
+        "per_gpu_value": round(value / world, 1),
+    }
+
+
+def main_stub_cpu(args):
+    """The bench's multi-rank control flow on CPU/gloo with the encoder replaced by a small
+    matmul: rank/world from torchrun, per-rank batch, timed region, max over ranks, one
+    JSON line from rank 0."""
+    from videomamba_amd.sharding import dist_env, shard_range
+
+    rank, _, world = dist_env()
+    if world > 1:
+        dist.init_process_group("gloo")
+    cfg = CONFIGS[args.config]
+    if args.global_batch:
+        a, b = shard_range(args.global_batch, world, rank)
+        per_rank, global_batch, strong = b - a, args.global_batch, True
+    else:
+        per_rank, global_batch, strong = args.batch, args.batch * world, False
+    w = torch.randn(64, 64)
+    x = torch.randn(max(per_rank, 1), 64)
+
+    def step():
+        time.sleep(0.002 * (1 + rank))  # ranks differ: the max must be the slowest
+        return x @ w
+
+    elapsed, _ = _timed_steps(step, args.steps, args.warmup, world, torch.device("cpu"),
+                              lambda: None)
+    if rank == 0:
+        line = _base_line(args, cfg, world, global_batch, per_rank, elapsed, strong)
+        line["stub"] = "cpu"
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = _args()
-    from videomamba_amd.sharding import dist_env, max_over_ranks
+    if args.stub_cpu:
+        return main_stub_cpu(args)
+    from videomamba_amd.sharding import dist_env, shard_range
 
     rank, local, world = dist_env()
     torch.cuda.set_device(local)
@@ -223,7 +312,13 @@ def main():
     model = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],
                                num_frames=cfg["frames"], pool_type="cls+avg")
     model = model.to(device=device, dtype=torch.bfloat16).eval()
-    B, T = args.batch, cfg["frames"]
+    T = cfg["frames"]
+    global_batch = args.global_batch or (cfg.get("global_batch") if args.batch_default else None)
+    if global_batch:  # C4: one global batch split across ranks (strong scaling)
+        a, b = shard_range(global_batch, world, rank)
+        B, strong = b - a, True
+    else:  # C3: a fixed batch per rank (weak scaling)
+        B, strong, global_batch = args.batch, False, args.batch * world
     g = torch.Generator(device=device).manual_seed(1000 + rank)
     x = torch.randn(B, 3, T, 224, 224, device=device, generator=g).to(torch.bfloat16)
     state = model.allocate_state(B, dtype=torch.bfloat16, device=device)
@@ -233,20 +328,10 @@ def main():
             return model(x)
         return model(x, ssm_state=state, temporal_pos_offset=0)
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        _sync_barrier(world)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        _sync_barrier(world)
-        elapsed = time.perf_counter() - t0
+    elapsed, out = _timed_steps(step, args.steps, args.warmup, world, device,
+                                torch.cuda.synchronize)
     assert torch.isfinite(out[1].float()).all()
-    elapsed = max_over_ranks(elapsed, device)  # the slowest rank's clock
-    ms_per_step = elapsed / args.steps * 1e3
-    tokens = world * B * T * 196 * args.steps
-    value = tokens / elapsed
+    line = _base_line(args, cfg, world, global_batch, B, elapsed, strong)
 
     # streaming-chunk p50 latency at B=1 (one stateful chunk of the same clip shape):
     # replayed from a captured HIP graph (videomamba_amd/graphs.py), and eager for reference
@@ -270,32 +355,19 @@ def main():
         p50_eager = chunk_lat(lambda: model(x1, ssm_state=st1, temporal_pos_offset=0))
         p50_graph = chunk_lat(lambda: runner.run(x1, temporal_pos_offset=0))
         from videomamba_amd.mamba_simple import mixer_layout
-        roof = scan_roofline(B, args.scan_reps, device,
-                             mixer_layout(B, cfg["embed_dim"] * 2, device))
+        roof = scan_roofline(max(B, 1), args.scan_reps, device,
+                             mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device))
 
     if rank == 0:
-        line = {
-            "metric": "video-tokens/sec per GPU + streaming-chunk p50 latency, VideoMamba-M 16f 224",
-            "value": round(value, 1), "unit": "video-tokens/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic clips (randn), random-init weights (seed 0)",
-            "config": {"workload": f"{cfg['name']} {T}x224^2 bf16, " + (
-                           "full-sequence forward per step" if args.full_sequence else
-                           "one stateful streaming chunk (chunk_size 32) per step"),
-                       "model": cfg["name"], "global_batch": world * B, "per_gpu_batch": B,
-                       "frames": T, "seq_len": 1 + T * 196,
-                       "parallelism": f"batch-sharded x{world}, no data-path collectives"},
-            "per_gpu_value": round(value / world, 1),
+        line.update({
             "chunk_p50_ms": round(p50_graph, 3),
             "chunk_p50_eager_ms": round(p50_eager, 3),
             "chunk_p50_batch": 1, "chunk_p50_mode": "hipGraph replay (StreamingChunkGraph)",
             "roofline": roof,
-        }
+        })
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         print(json.dumps(line), flush=True)
-    # (VM_GEMM_TUNING=tune: TunableOp writes its results file at process exit)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

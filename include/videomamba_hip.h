@@ -16,8 +16,6 @@
  *   vm_conv_proj_fwd           <- causal_conv1d_fn + x_proj + dt_proj, fused, token-major
  *                                 (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
- *   vm_out_proj_add_norm_fwd   <- out_proj (mamba_simple.py:445-446) + the next block's
- *                                 fused add + norm (videomamba.py:152-166)
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
  *                                 (videomamba.py:359-368, :806-815)
@@ -40,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 3
+#define VM_ABI_VERSION 4
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -70,9 +68,12 @@ const char* vm_last_error(void);
  * h0 (nullable) / h_last (nullable): (batch, dim, dstate) with strides (sb, sd, 1) in
  * their own dtype; h_last may alias h0 (in-place state update).  dstate <= 16.
  * Steps [seqlen, out_len) of every out row are written as 0 (padded token layouts).
- * workspace: scratch for the time-segmented token-major form (small batches), at least
- * vm_selective_scan_workspace_bytes() bytes; with less (or NULL) a single-pass kernel
- * runs instead — same result, less parallelism.
+ * segments: token-major only — 0 lets the cost model choose how many time segments the
+ * sequence is cut into (small batches run summary / carry / final passes), > 0 forces that
+ * count (tests and sweeps).  There is no other configuration channel (no environment).
+ * workspace: scratch for the time-segmented token-major form, at least
+ * vm_selective_scan_workspace_bytes(..., segments) bytes; with less (or NULL) a
+ * single-pass kernel runs instead — same result, less parallelism.
  */
 int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd, long long u_sl,
                           const void* delta, long long dl_sb, long long dl_sd, long long dl_sl,
@@ -85,10 +86,13 @@ int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd, long lo
                           void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
                           void* out, long long o_sb, long long o_sd, long long o_sl,
                           int out_len, int batch, int dim, int seqlen, int dstate, int dtype,
-                          void* workspace, long long workspace_bytes, vm_stream_t stream);
+                          int segments, void* workspace, long long workspace_bytes,
+                          vm_stream_t stream);
 
-/* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape. */
-long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int dstate);
+/* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape and
+ * segment request (0 = the cost model's choice). */
+long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int dstate,
+                                            int segments);
 
 /*
  * One-token scan step on `state` (updated in place, own dtype; fp32 math).
@@ -131,6 +135,7 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
  * e_pad <= 128); wdt_pad: (dim, r_pad) with columns >= r zero (r_pad 32 or 64).  Rows
  * with step >= seqlen are written as 0.  conv state as vm_causal_conv1d_fwd (width <= 4).
  * dim % 64 == 0, seqlen >= 1.
+ * dt == NULL skips dt_proj (conv + x_proj only; wdt_pad may then be NULL too).
  * dt_softplus != 0: `dt` receives the scan's activated step instead,
  *   delta = softplus(float(bf16(dt)) + dt_bias[d])  (dt_bias nullable = 0), rounded to bf16
  *   — selective_scan_fn's delta_bias / delta_softplus prologue (mamba_simple.py:30-106),
@@ -147,22 +152,6 @@ int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                      const float* dt_bias, int dt_softplus,
                      int out_len, int batch, int dim, int seqlen, int width, int dtype,
                      vm_stream_t stream);
-
-/*
- * out_proj GEMM + the next block's fused residual add + RMSNorm / LayerNorm
- * (mamba_simple.py:445-446 then videomamba.py:152-166 / mamba-ssm rms_norm_fn, prenorm):
- *   hidden = bf16(y @ w_out^T);  s = hidden + residual (fp32);  out = bf16(norm(s) * w + b)
- *   residual_out = s.
- * y: (rows, k) bf16, row stride y_sl; w_out: (n, k) bf16 (nn.Linear weight, contiguous);
- * residual / residual_out: (rows, n) fp32, contiguous, nullable, may alias; out: (rows, n)
- * bf16.  norm_bias nullable (RMSNorm ignores it); is_rms selects RMSNorm.
- * k % 32 == 0, n % 64 == 0, n <= 768.
- */
-int vm_out_proj_add_norm_fwd(const void* y, long long y_sl, const void* w_out,
-                             const float* residual, const float* norm_weight,
-                             const float* norm_bias, void* out, float* residual_out,
-                             long long rows, int n, int k, float eps, int is_rms,
-                             vm_stream_t stream);
 
 /*
  * One-token conv step: shift conv_state left by one, append x, dot with weight (+bias),

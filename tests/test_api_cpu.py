@@ -255,7 +255,7 @@ def test_abi_rejects_bad_arguments_without_gpu():
     lib = _lib.load()
     rc = lib.vm_selective_scan_fwd(*([None, 0, 0, 0] * 2), None, *([None, 0, 0, 0] * 2),
                                    None, None, 0, 0, 0, None, 0, None, 0, 0, 0, None, 0, 0, 0,
-                                   None, 0, 0, 0, 0, 1, 1, 1, 16, 0, None, 0, None)
+                                   None, 0, 0, 0, 0, 1, 1, 1, 16, 0, 0, None, 0, None)
     assert rc == -1
     assert b"null required pointer" in lib.vm_last_error()
     rc = lib.vm_add_norm_fwd(None, 0, None, 0, None, None, None, 0, None, 0, 1, 8, 1e-5, 1, None)
@@ -265,7 +265,31 @@ def test_abi_rejects_bad_arguments_without_gpu():
 def test_scan_workspace_query_without_gpu():
     lib = _lib.load()
     # small batch, long sequence: the segmented token-major form wants scratch
-    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 16) > 0
+    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 16, 0) > 0
     # a chip-filling batch runs single-pass
-    assert lib.vm_selective_scan_workspace_bytes(64, 1152, 3137, 16) == 0
-    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 17) == 0
+    assert lib.vm_selective_scan_workspace_bytes(64, 1152, 3137, 16, 0) == 0
+    assert lib.vm_selective_scan_workspace_bytes(1, 1152, 3137, 17, 0) == 0
+    # an explicit segment request (the ABI's only configuration argument) is honoured
+    one = lib.vm_selective_scan_workspace_bytes(2, 64, 100, 16, 1)
+    four = lib.vm_selective_scan_workspace_bytes(2, 64, 100, 16, 4)
+    assert one == 0 and four == 2 * 4 * 64 * (2 * 16 + 1) * 4
+
+
+def test_library_reads_no_environment():
+    """The C library has no configuration channel besides its arguments:
+    no getenv in any product source."""
+    csrc = os.path.join(ROOT, "videomamba_amd", "csrc")
+    for name in os.listdir(csrc):
+        if name.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(csrc, name)).read(), name
+
+
+def test_options_override_and_validation():
+    from videomamba_amd import options
+    assert options.get().mixer_layout == "auto" and options.get().scan_segments == 0
+    with options.override(mixer_layout="tm", scan_segments=8) as o:
+        assert options.get() is o and o.scan_segments == 8
+    assert options.get().mixer_layout == "auto"
+    with pytest.raises(ValueError):
+        with options.override(mixer_layout="xx"):
+            pass

@@ -15,6 +15,7 @@ import torch
 import video_mamba
 from conftest import load_golden
 from oracle import videomamba_oracle as orc
+from videomamba_amd import options
 from videomamba_amd.mamba_simple import Mamba
 from videomamba_amd.videomamba import PretrainVideoMamba, create_block
 
@@ -32,11 +33,11 @@ def _close(a, b, tol):
 
 
 @pytest.fixture(params=["cm", "tm"])
-def layout(request, monkeypatch):
+def layout(request):
     """Both mixer layouts (channel-major + time-parallel scan, token-major +
-    channel-per-lane scan) must match the same fixtures; VM_MIXER_LAYOUT forces one."""
-    monkeypatch.setenv("VM_MIXER_LAYOUT", request.param)
-    return request.param
+    channel-per-lane scan) must match the same fixtures; options.mixer_layout forces one."""
+    with options.override(mixer_layout=request.param):
+        yield request.param
 
 
 def _load(module, npz, name, dt):
@@ -369,7 +370,8 @@ def test_ti_8f_fp32_matches_oracle(layout):
 
 def test_m_16f_bf16_streaming_chunks_match_full_and_fp32(layout):
     """VideoMamba-M (d576, depth 32) 16x224^2 bf16: 2 chunks of 8 frames with carried
-    fp32 state == one full pass; and the bf16 pass tracks an fp32 pass of the same weights."""
+    fp32 state == one full pass within the north star's 1e-4 relative; and the bf16 pass
+    tracks an fp32 pass of the same weights (5e-2: bf16 rounding through 32 layers)."""
     torch.manual_seed(0)
     model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, add_pool_norm=False)
     model = model.to(DEV).eval()
@@ -384,13 +386,13 @@ def test_m_16f_bf16_streaming_chunks_match_full_and_fp32(layout):
         c2, st = mb(xb[:, :, 8:], ssm_state=st, temporal_pos_offset=8)
     stitched = torch.cat([c1, c2], 1).float()
     rel = ((stitched - full.float()).norm() / full.float().norm()).item()
-    assert rel < 1e-2, rel
+    assert rel < 1e-4, rel
     rel32 = ((full.float() - full32).norm() / full32.norm()).item()
     assert rel32 < 5e-2, rel32
     assert torch.isfinite(full.float()).all()
 
 
-def test_large_batch_selects_token_major_and_matches_channel_major(monkeypatch):
+def test_large_batch_selects_token_major_and_matches_channel_major():
     """The automatic layout choice: a chip-filling batch runs token-major; its output
     equals the channel-major run of the same model (bf16, M geometry, 2 frames)."""
     from videomamba_amd.mamba_simple import mixer_layout
@@ -404,19 +406,23 @@ def test_large_batch_selects_token_major_and_matches_channel_major(monkeypatch):
     x = torch.randn(big, 3, 2, 224, 224, device=DEV).to(torch.bfloat16)
     with torch.no_grad():
         auto = model(x)
-        monkeypatch.setenv("VM_MIXER_LAYOUT", "cm")
-        cm = model(x)
+        with options.override(mixer_layout="cm"):
+            cm = model(x)
     rel = ((auto.float() - cm.float()).norm() / cm.float().norm()).item()
     assert rel < 1e-2, rel
 
 
 @pytest.mark.parametrize("d_model,L,split", [(96, 301, 130), (64, 70, 3), (288, 1000, 999)])
-def test_fused_conv_proj_mixer_bf16_matches_oracle_and_unfused(d_model, L, split, monkeypatch):
+def test_fused_conv_proj_mixer_bf16_matches_oracle_and_unfused(d_model, L, split):
     """Token-major bf16 mixer with the fused conv+x_proj+dt_proj kernel (D % 64 == 0):
     vs the oracle's bf16 restatement and vs the unfused token-major path, full and two
     chunks with carried (conv_state, ssm_state) — including a 3-token first chunk (the conv
     halo reaches into the state) and a 1-token second chunk."""
-    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
+    with options.override(mixer_layout="tm"):
+        _fused_conv_proj_mixer(d_model, L, split)
+
+
+def _fused_conv_proj_mixer(d_model, L, split):
     torch.manual_seed(d_model)
     m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0)
     with torch.no_grad():
@@ -432,8 +438,8 @@ def test_fused_conv_proj_mixer_bf16_matches_oracle_and_unfused(d_model, L, split
         o1, (c1, s1) = m(xd[:, :split], return_state=True)
         c1_0, s1_0 = c1.clone(), s1.clone()  # s1 is updated in place by the next chunk
         o2, (c2, s2) = m(xd[:, split:], state=(c1, s1), return_state=True)
-        monkeypatch.setenv("VM_FUSED_CONV_PROJ", "0")
-        unfused = m(xd)
+        with options.override(fused_conv_proj=False):
+            unfused = m(xd)
     _close(full, ref, 5e-2)
     rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
     assert rel(full, unfused) < 1e-2
@@ -476,34 +482,175 @@ def test_graph_replay_matches_eager_streaming(layout, pool, add_pool_norm, dt):
                 torch.testing.assert_close(s1, s2, rtol=0, atol=0)
 
 
-# ------------------------------------------------------------------ concurrent batch slices
-@pytest.mark.parametrize("streams", ["2", "3"])
-def test_multistream_batch_slices_match_single_stream(streams, monkeypatch):
-    """VM_BATCH_STREAMS>1 (videomamba.py _layers_multistream): batch slices on concurrent
-    HIP streams give bit-identical features and carried state to the one-stream loop, for
-    the stateless and the full-state streaming paths (token-major forced so the slicing
-    engages at a small model)."""
-    monkeypatch.setenv("VM_MIXER_LAYOUT", "tm")
-    torch.manual_seed(0)
-    model = _small_model(img_size=32, patch_size=16, depth=3, embed_dim=32, fused_add_norm=True,
-                         rms_norm=True, residual_in_fp32=True, num_frames=4,
-                         add_pool_norm=False).to(DEV, torch.bfloat16).eval()
-    x = torch.randn(5, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
+# ------------------------------------------------------------------ BASELINE configs C2 / C4 / C5
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def _m_model(frames, seed=0, depth=32, add_pool_norm=False):
+    torch.manual_seed(seed)
+    model = PretrainVideoMamba(depth=depth, embed_dim=576, num_frames=frames,
+                               add_pool_norm=add_pool_norm)
     with torch.no_grad():
-        monkeypatch.setenv("VM_BATCH_STREAMS", "1")
-        ref = model(x)
-        st_ref = model.allocate_state(5, dtype=torch.bfloat16, device=DEV)
-        c1_ref, st_ref = model(x[:, :, :2], ssm_state=st_ref)
-        c2_ref, st_ref = model(x[:, :, 2:], ssm_state=st_ref, temporal_pos_offset=2)
-        monkeypatch.setenv("VM_BATCH_STREAMS", streams)
-        assert model._stream_slices(5, None) is not None
-        got = model(x)
-        st = model.allocate_state(5, dtype=torch.bfloat16, device=DEV)
-        c1, st = model(x[:, :, :2], ssm_state=st)
-        c2, st = model(x[:, :, 2:], ssm_state=st, temporal_pos_offset=2)
-    torch.cuda.synchronize()
-    for a, b in ((got, ref), (c1, c1_ref), (c2, c2_ref)):
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    return model.to(DEV).to(torch.bfloat16).eval()
+
+
+def test_c2_ti_8f_bf16_full_sequence_matches_oracle():
+    """C2 (BASELINE.json configs[1]): VideoMamba-Ti (d192, depth 24) 8x224^2 bf16,
+    full-sequence forward at B=1 on the HIP path vs the oracle's bf16 restatement on the
+    same weights and clip (bf16 at the reference's rounding points, fp32 math).
+    Tolerance: relative L2 norm <= 1e-2 on x_vis and x_pool (single-ulp bf16 flips where
+    the fp32 accumulation orders differ propagate through 24 layers); every element within
+    5e-2 abs + 5e-2 rel."""
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=24, embed_dim=192, num_frames=8).eval()
+    with torch.no_grad():
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    model = model.to(torch.bfloat16)
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(1, 3, 8, 224, 224, generator=g).to(torch.bfloat16)
+    cfg = dict(img_size=224, patch_size=16, depth=24, kernel_size=1, num_frames=8,
+               fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+               pool_type="cls+avg", norm_epsilon=1e-5, d_state=16, d_conv=4)
+    torch.set_num_threads(16)
+    ref_v, ref_p, _ = orc.encoder_forward(p, cfg, x)
+    model = model.to(DEV)
+    with torch.no_grad():
+        xv, xp = model(x.to(DEV))
+    assert xv.dtype == torch.bfloat16 and xv.shape == ref_v.shape
+    assert _rel(xv.cpu(), ref_v) <= 1e-2, _rel(xv.cpu(), ref_v)
+    assert _rel(xp.cpu(), ref_p) <= 1e-2, _rel(xp.cpu(), ref_p)
+    torch.testing.assert_close(xv.float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
+
+
+def test_c4_m_32f_chunked_equals_full_and_token_major_batch():
+    """C4 clip shape (VideoMamba-M 32x224^2 bf16, num_frames=32): 2 x 16-frame chunks
+    with a carried fp32 state == one 32-frame pass within 1e-4 relative, at B=1
+    (channel-major mixer) and at B=72 (token-major mixer: the chip-filling batch runs the
+    bench's kernels, fused conv_proj + channel-per-lane scan); clip 0 of the B=72 batch ==
+    its B=1 run within 1e-2 (different scan kernels, bf16 rounding flips)."""
+    from videomamba_amd.mamba_simple import mixer_layout
+    model = _m_model(32)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    outs = {}
+    for bsz in (1, 72):
+        x = torch.randn(bsz, 3, 32, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+        if bsz == 72:
+            x[0] = x1[0]
+            assert mixer_layout(bsz, 1152, torch.device(DEV)) == "tm"
+        else:
+            x1 = x
+            assert mixer_layout(bsz, 1152, torch.device(DEV)) == "cm"
+        with torch.no_grad():
+            full = model(x)
+            st = model.allocate_state(bsz, dtype=torch.float32)
+            c1, st = model(x[:, :, :16], ssm_state=st, temporal_pos_offset=0)
+            c2, st = model(x[:, :, 16:], ssm_state=st, temporal_pos_offset=16)
+        stitched = torch.cat([c1, c2], 1)
+        assert _rel(stitched, full) < 1e-4, (bsz, _rel(stitched, full))
+        assert torch.isfinite(full.float()).all()
+        outs[bsz] = full[:1]
+        del x, full, c1, c2, st, stitched
+    assert _rel(outs[72], outs[1]) < 1e-2, _rel(outs[72], outs[1])
+
+
+def test_c5_long_video_chunk64_streaming_matches_full():
+    """C5 at reduced chunk count: VideoMamba-M built with num_frames=1024 (so the temporal
+    embedding is sliced, never interpolated: SURVEY F7), 4 x chunk64 streamed with a
+    carried fp32 state (L = 12,545 then 12,544 per chunk) vs one 256-frame forward
+    (L = 50,177), B=1.  North-star tolerance: < 1e-4 relative on the last chunk's tokens
+    (and on every chunk)."""
+    model = _m_model(1024)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(1, 3, 256, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        full = model(x)
+        st = model.allocate_state(1, dtype=torch.float32)
+        chunks = []
+        for c in range(4):
+            out, st = model(x[:, :, 64 * c:64 * (c + 1)], ssm_state=st, temporal_pos_offset=64 * c)
+            chunks.append(out)
+    assert chunks[0].shape[1] == 12545 and chunks[3].shape[1] == 12544
+    assert full.shape[1] == 50177
+    last = full[:, -12544:]
+    assert _rel(chunks[3], last) < 1e-4, _rel(chunks[3], last)
+    assert _rel(torch.cat(chunks, 1), full) < 1e-4
+    assert torch.isfinite(full.float()).all()
+
+
+@pytest.mark.parametrize("segments", [1, 0])
+def test_m_mixer_token_major_bench_kernels_match_oracle(segments):
+    """The bench's exact mixer kernels at VideoMamba-M width (d_model 576: D = 1152,
+    R = 36, N = 16, bf16): token-major layout, fused conv + x_proj + dt_proj, and the
+    channel-per-lane scan reading z inside xz and B|C inside x_dbl with one scalar load
+    (scan_seq_kernel<bf16, ..., BC1>); segments=1 is the single-pass form the B=336 bench
+    runs, 0 the cost model's choice at this batch.  vs the oracle's bf16 mixer (same
+    rounding points), full sequence and two stateful chunks.  Tolerance 5e-2 abs+rel per
+    element, 1e-2 relative norm."""
+    torch.manual_seed(11)
+    m = Mamba(d_model=576, d_state=16, d_conv=4, expand=2, layer_idx=0)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.add_(0.01 * torch.randn_like(prm))
+    m = m.to(torch.bfloat16).to(DEV).eval()
+    p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 1000, 576).to(torch.bfloat16)
+    torch.set_num_threads(16)
+    ref = orc.mamba_mixer(p, "", x, d_state=16, d_conv=4)
+    r1, (rc1, rs1) = orc.mamba_mixer(p, "", x[:, :601], d_state=16, d_conv=4, return_state=True)
+    r2, _ = orc.mamba_mixer(p, "", x[:, 601:], d_state=16, d_conv=4, state=(rc1, rs1),
+                            return_state=True)
+    xd = x.to(DEV)
+    with options.override(mixer_layout="tm", scan_segments=segments), torch.no_grad():
+        full = m(xd)
+        st = m.allocate_state(2, dtype=torch.float32)
+        o1, st = m(xd[:, :601], state=st, return_state=True)
+        o2, st = m(xd[:, 601:], state=st, return_state=True)
+    _close(full, ref, 5e-2)
+    assert _rel(full.cpu(), ref) < 1e-2
+    assert _rel(torch.cat([o1, o2], 1).cpu(), torch.cat([r1, r2], 1)) < 1e-2
+    assert _rel(torch.cat([o1, o2], 1), full) < 1e-4
+
+
+def test_streaming_state_contract_in_place_ssm_fresh_conv():
+    """The streaming contract (streaming.py docs): with ``state=(conv, ssm)``
+    the returned ssm state IS the caller's tensor, updated in place (the reference's
+    fallback aliases it), and the returned conv state is a new tensor; the caller's conv
+    state is left untouched.  A caller that wants to branch a stream clones first."""
+    m = Mamba(d_model=32, d_state=16, d_conv=4, layer_idx=0).to(DEV).eval()
+    x = torch.randn(2, 40, 32, device=DEV)
+    conv, ssm = m.allocate_state(2)
+    conv0, ssm0 = conv.clone(), ssm.clone()
+    with torch.no_grad():
+        _, (c1, s1) = m(x, state=(conv, ssm), return_state=True)
+    assert s1 is ssm and not torch.equal(ssm, ssm0)
+    assert c1 is not conv and torch.equal(conv, conv0)
+
+
+def test_graph_replay_survives_workspace_growth_and_weight_reload():
+    """StreamingChunkGraph owns its scan workspace and re-captures after a parameter
+    change: capture at B=1 (token-major, segmented scan forced so the workspace is live),
+    run an eager B=4 forward that would grow a shared scratch buffer, reload modified
+    weights with load_state_dict, then replay == the eager stateful forward."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    torch.manual_seed(0)
+    model = _small_model(img_size=32, patch_size=16, depth=2, embed_dim=64, fused_add_norm=True,
+                         rms_norm=True, residual_in_fp32=True, num_frames=4, pool_type="avg",
+                         add_pool_norm=True).to(DEV).eval()
+    x = torch.randn(1, 3, 2, 32, 32, device=DEV)
+    with options.override(mixer_layout="tm", scan_segments=3):
+        runner = StreamingChunkGraph(model, batch=1, frames=2, height=32, width=32)
+        with torch.no_grad():
+            runner.run(x, temporal_pos_offset=0)
+            model(torch.randn(4, 3, 4, 32, 32, device=DEV))  # eager, bigger workspace
+            sd = {k: v + 0.01 * torch.randn_like(v) if v.is_floating_point() else v
+                  for k, v in model.state_dict().items()}
+            model.load_state_dict(sd)
+            runner.reset_state()
+            got = runner.run(x, temporal_pos_offset=0)
+            state = model.allocate_state(1, device=DEV)
+            want = model(x, ssm_state=state, temporal_pos_offset=0)
+    for a, b in zip(got, want[:-1]):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
-    for (ca, sa), (cb, sb) in zip(st, st_ref):
-        torch.testing.assert_close(ca, cb, rtol=0, atol=0)
-        torch.testing.assert_close(sa, sb, rtol=0, atol=0)

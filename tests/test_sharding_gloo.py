@@ -61,3 +61,98 @@ def test_gloo_world2_shards_clock_and_gather():
     assert all(o[2] == 2.0 for o in out)          # max over ranks
     for o in out:                                 # every rank sees the global pooled batch
         assert torch.equal(torch.tensor(o[3]), x * 2)
+
+
+def _bench_stub(extra):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--stub-cpu", "--gpus", "2", "--steps", "4",
+           "--warmup", "1"] + extra
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_control_flow_world2_weak_scaling():
+    """bench.py's own N=2 path under torchrun (gloo, encoder stubbed): ranks from the env,
+    a fixed batch per rank (C3, weak scaling), barrier-bracketed timing whose clock is the
+    slowest rank's (rank 1 sleeps 4 ms per step), one JSON line from rank 0."""
+    line = _bench_stub([])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["per_gpu_batch"] == 336 and line["config"]["global_batch"] == 672
+    assert line["ms_per_step"] >= 4.0  # the slower rank sets the step time
+    want = 672 * 16 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
+    assert abs(line["value"] - want) / want < 1e-3
+    assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
+
+
+def test_bench_control_flow_world2_global_batch_split():
+    """--global-batch (C4): one global batch split by shard_range — 5 clips on 2 ranks is
+    3 + 2; scaling is strong and value counts the global batch once."""
+    line = _bench_stub(["--config", "m32", "--global-batch", "5"])
+    assert line["scaling"] == "strong" and line["config"]["global_batch"] == 5
+    assert line["config"]["per_gpu_batch"] == 3  # rank 0's shard
+    want = 5 * 32 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
+    assert abs(line["value"] - want) / want < 1e-3
+
+
+def _encoder_shard_worker(rank, world, port, q):
+    """One rank of the batch-sharded encoder: its contiguous clip range through the HIP
+    encoder on cuda:0, then the pooled-feature all-gather (gloo, so CPU tensors)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from videomamba_amd.videomamba import PretrainVideoMamba
+        torch.manual_seed(0)
+        model = PretrainVideoMamba(img_size=64, patch_size=16, depth=3, embed_dim=64,
+                                   num_frames=4).eval()
+        x = torch.randn(4, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
+        local = shard_batch(x, world, rank)
+        with torch.no_grad():
+            xv, xp = model.to("cuda:0")(local.to("cuda:0"))
+        pooled = gather_pooled(xp.cpu())
+        q.put((rank, local.shape[0], xv.cpu(), pooled))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_encoder_batch_sharded_world2_matches_single_process():
+    """SURVEY §8e on hardware we have: 2 fresh processes (gloo, both on cuda:0) each run
+    their shard of a 4-clip batch through the HIP encoder and all-gather x_pool.  Every
+    rank's features equal the single-process forward of the same shard bit for bit, and the
+    gathered x_pool equals the single-process forward of the whole batch (1e-5: the
+    library GEMMs may pick other kernels for a different batch size)."""
+    from videomamba_amd.videomamba import PretrainVideoMamba
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_encoder_shard_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=300) for _ in range(world)), key=lambda o: o[0])
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(img_size=64, patch_size=16, depth=3, embed_dim=64,
+                               num_frames=4).eval().to("cuda:0")
+    x = torch.randn(4, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        xv_all, xp_all = model(x.to("cuda:0"))
+        for rank, n, xv, pooled in out:
+            a, b = shard_range(4, world, rank)
+            assert n == b - a
+            xv_ref, _ = model(x[a:b].to("cuda:0"))
+            assert torch.equal(xv, xv_ref.cpu())
+            assert pooled.shape == xp_all.shape
+            torch.testing.assert_close(pooled, xp_all.cpu(), rtol=1e-5, atol=1e-5)
+    assert torch.equal(out[0][3], out[1][3])  # every rank holds the same gathered batch

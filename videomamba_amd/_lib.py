@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _P = c_void_p
 _LL = c_longlong
@@ -41,9 +41,9 @@ _SIGNATURES = {
          _P, _I, _LL, _LL,        # h_last
          _P, _LL, _LL, _LL, _I,   # out, out_len
          _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
-         _P, _LL,                 # workspace, workspace_bytes
+         _I, _P, _LL,             # segments, workspace, workspace_bytes
          _P], _I),
-    "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I], _LL),
+    "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_state_update": (
         [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
          _P, _LL, _I, _I, _I, _I, _P], _I),
@@ -57,8 +57,6 @@ _SIGNATURES = {
          _P, _LL, _LL, _P, _LL, _LL, _P, _LL, _LL,  # u, x_dbl, dt
          _P, _I,                                  # dt bias, dt softplus
          _I, _I, _I, _I, _I, _I, _P], _I),
-    "vm_out_proj_add_norm_fwd": (
-        [_P, _LL, _P, _P, _P, _P, _P, _P, _LL, _I, _I, ctypes.c_float, _I, _P], _I),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_add_norm_fwd": (

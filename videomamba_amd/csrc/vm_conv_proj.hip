@@ -90,9 +90,6 @@ __device__ __forceinline__ bf16_t dt_out(float acc, float bias) {
   return v;
 }
 
-template <int SW = 16, int NW = 4, bool SPD = false>
-__device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
-                                         int row0, int lane, int wave);
 template <bool SPD>
 __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
                                               bf16_t* sU, int row0, int lane, int wave);
@@ -259,88 +256,8 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
   }
 }
 
-// dt_proj for one 64-token tile: A = x_dbl[:, :R] (zero-padded to r_pad) in sA,
-// wave = 64-column blocks wave, wave+NW, ...; outputs staged per wave in sU and stored as
-// 128-byte row segments, SW bytes per lane-store.
-template <int SW, int NW, bool SPD>
-__device__ __forceinline__ void dt_phase(const ConvProjParams& p, const bf16_t* sA, bf16_t* sU,
-                                         int row0, int lane, int wave) {
-  const int D = p.dim;
-  const int ksteps = p.r_pad / 32;
-  bf16x8 af[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      af[i][ks] = *reinterpret_cast<const bf16x8*>(
-          &sA[(i * 16 + (lane & 15)) * kCPPad + ks * 32 + (lane >> 4) * 8]);
-  bf16_t* stg = sU + wave * kCPTok * kCPPad;
-  for (int cb = wave; cb * 64 < D; cb += NW) {
-    float bj[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bj[j] = SPD && p.dtb ? p.dtb[cb * 64 + j * 16 + (lane & 15)] : 0.0f;
-    f32x4 d[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) d[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = cb * 64 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks < ksteps) {
-          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
-              p.wdt + (long long)n * p.r_pad + ks * 32 + (lane >> 4) * 8);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            d[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bv, d[i][j], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          stg[(i * 16 + (lane >> 4) * 4 + e) * kCPPad + j * 16 + (lane & 15)] =
-              dt_out<SPD>(d[i][j][e], bj[j]);
-    // the wave reads back its own staging tile: 64 rows x 128 B
-    if constexpr (SW == 16) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int lr = it * 8 + (lane >> 3), q = lane & 7;
-        const int row = row0 + lr;
-        const uint4 val = *reinterpret_cast<const uint4*>(&stg[lr * kCPPad + q * 8]);
-        if (row < p.rows)
-          *reinterpret_cast<uint4*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 8) = val;
-      }
-    } else if constexpr (SW == 8) {
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int lr = it * 4 + (lane >> 4), q = lane & 15;
-        const int row = row0 + lr;
-        const uint2 val = *reinterpret_cast<const uint2*>(&stg[lr * kCPPad + q * 4]);
-        if (row < p.rows)
-          *reinterpret_cast<uint2*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 4) = val;
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < 32; ++it) {
-        const int lr = it * 2 + (lane >> 5), q = lane & 31;
-        const int row = row0 + lr;
-        const uint32_t val = *reinterpret_cast<const uint32_t*>(&stg[lr * kCPPad + q * 2]);
-        if (row < p.rows)
-          *reinterpret_cast<uint32_t*>(p.dt + (long long)row * p.dt_sl + cb * 64 + q * 2) = val;
-      }
-    }
-  }
-}
-
-
-// dt_proj inside conv_proj (DT): as dt_phase, but each 64-column block in two 32-row
-// halves, so the per-wave staging is 32 rows and the fused kernel keeps conv_proj's LDS
+// dt_proj inside conv_proj (DT): wave = 64-column blocks wave, wave+4, ...; each block in
+// two 32-row halves, so the per-wave staging is 32 rows and the fused kernel keeps conv_proj's LDS
 // budget (3 workgroups per CU) and half the accumulators.
 template <bool SPD>
 __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf16_t* sA,
@@ -421,26 +338,6 @@ __global__ __launch_bounds__(256) void conv_state_out_kernel(const ConvProjParam
   }
 }
 
-// dt = x_dbl[:, :R] @ W_dt^T for 64-token tiles (the split form of conv_proj_kernel<true>).
-// NW waves share a tile's 64-column blocks (D = 1152: 18 blocks, 3 per wave at NW = 6).
-template <int SW = 16, int NW = 4, bool SPD = false>
-__global__ __launch_bounds__(64 * NW) void dt_proj_kernel(const ConvProjParams p) {
-  __shared__ __attribute__((aligned(16))) bf16_t sA[kCPTok * kCPPad];
-  __shared__ __attribute__((aligned(16))) bf16_t sU[NW * kCPTok * kCPPad];
-  const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * kCPTok;
-  for (int idx = tid; idx < kCPTok * kCPPad / 8; idx += 64 * NW)
-    *reinterpret_cast<uint4*>(&sA[idx * 8]) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  for (int idx = tid; idx < kCPTok * p.r; idx += 64 * NW) {
-    const int lr = idx / p.r, k = idx - lr * p.r;
-    const int row = row0 + lr;
-    sA[lr * kCPPad + k] = row < p.rows ? p.xdbl[(long long)row * p.xd_sl + k] : bf16_t(0);
-  }
-  __syncthreads();
-  dt_phase<SW, NW, SPD>(p, sA, sU, row0, tid & 63, tid >> 6);
-}
-
 }  // namespace vm
 
 using namespace vm;
@@ -456,27 +353,27 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
                                 void* dt, long long dt_sb, long long dt_sl,
                                 const float* dt_bias, int dt_softplus, int out_len, int batch, int dim, int seqlen, int width, int dtype,
                                 vm_stream_t stream) {
-  if (!xz || !conv_weight || !wx_pad || !wdt_pad || !u || !xdbl || !dt) {
+  if (!xz || !conv_weight || !wx_pad || !u || !xdbl || (dt && !wdt_pad)) {
     vmhost::set_error("vm_conv_proj_fwd: null required pointer");
     return VM_E_INVALID;
   }
   if (dtype != VM_DTYPE_BF16 || batch < 0 || dim <= 0 || dim % kCPCh != 0 || seqlen < 1 ||
       out_len < seqlen || width < 1 || width > 4 || e < 1 || e_pad % 16 != 0 || e_pad < e ||
-      e_pad > kCPMaxNB * 16 || r < 1 || r > e || (r_pad != 32 && r_pad != 64) || r_pad < r ||
+      e_pad > kCPMaxNB * 16 || r < 1 || r > e || (dt && ((r_pad != 32 && r_pad != 64) || r_pad < r)) ||
       (cs_in && !vmhost::dtype_ok(cs_in_dtype)) || (cs_out && !vmhost::dtype_ok(cs_out_dtype))) {
     vmhost::set_error("vm_conv_proj_fwd: unsupported shape (bf16, dim %% 64 == 0, width <= 4, "
                       "R + 2N <= 128, R <= 64, seqlen >= 1)");
     return VM_E_INVALID;
   }
   if (!vmhost::aligned16(xz) || !vmhost::aligned16(u) || !vmhost::aligned16(wx_pad) ||
-      !vmhost::aligned16(wdt_pad) || !vmhost::aligned16(dt) || xz_sb % 8 || xz_sl % 8 ||
+      (dt && !vmhost::aligned16(wdt_pad)) || (dt && !vmhost::aligned16(dt)) || xz_sb % 8 || xz_sl % 8 ||
       u_sb % 8 || u_sl % 8 || dt_sl % 8 || out_len % 2 || e % 2 || xd_sl % 2 ||
       (reinterpret_cast<uintptr_t>(xdbl) & 3) || dim > 8192) {
     vmhost::set_error("vm_conv_proj_fwd: xz / u / dt / weights need 16-byte aligned rows, "
                       "x_dbl 4-byte aligned, even out_len and e, dim <= 8192");
     return VM_E_INVALID;
   }
-  if (u_sb != out_len * u_sl || xd_sb != out_len * xd_sl || dt_sb != out_len * dt_sl) {
+  if (u_sb != out_len * u_sl || xd_sb != out_len * xd_sl || (dt && dt_sb != out_len * dt_sl)) {
     vmhost::set_error("vm_conv_proj_fwd: u / x_dbl / dt must be batch-contiguous "
                       "(sb == out_len * sl)");
     return VM_E_INVALID;
@@ -502,10 +399,9 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   dim3 grid((p.rows + kCPTok - 1) / kCPTok);
   const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // dt_proj runs inside conv_proj (half-tile dt phase, same LDS budget); VM_CONV_PROJ_SPLIT=1
-  // runs it as its own kernel instead (bit-identical output)
-  const char* split = getenv("VM_CONV_PROJ_SPLIT");
-  const bool fused_dt = !(split && atoi(split) == 1);
+  // dt_proj runs inside conv_proj (half-tile dt phase, same LDS budget); dt == nullptr
+  // skips it (conv + x_proj only: a consumer that projects dt itself)
+  const bool fused_dt = dt != nullptr;
   const bool spd = dt_softplus != 0;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
   switch (e_pad / 16) {  // x_proj output blocks
@@ -519,9 +415,6 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     VM_CP_CASE(5) VM_CP_CASE(6) VM_CP_CASE(7) VM_CP_CASE(8)
 #undef VM_CP_CASE
   }
-  // conv + x_proj at lower register pressure, then dt_proj from x_dbl
-  if (!fused_dt && spd) hipLaunchKernelGGL((dt_proj_kernel<16, 4, true>), grid, dim3(256), 0, st, p);
-  else if (!fused_dt) hipLaunchKernelGGL((dt_proj_kernel<16, 4>), grid, dim3(256), 0, st, p);
   if (cs_out)
     hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
   return vmhost::launch_status("vm_conv_proj_fwd");

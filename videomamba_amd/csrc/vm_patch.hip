@@ -435,16 +435,16 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch % 8 == 0 && width % 8 == 0 &&
                        p.K % 8 == 0 && vmhost::aligned16(video) && vmhost::aligned16(weight);
-  const char* pv = getenv("VM_PATCH_KERNEL");  // A/B: "1" 64x64 tiles, "2" 64x192 tiles
   const bool wide_ok = mfma_ok && patch == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
                        out_sb % 8 == 0 && vmhost::aligned16(out) && vmhost::aligned16(spos) &&
-                       vmhost::aligned16(tpos) && !(pv && atoi(pv) == 1);
+                       vmhost::aligned16(tpos);
   // the 128-token LDS-staged tiles pay off on chip-filling batches; small ones keep more,
-  // smaller workgroups (B = 1: 147 of 64 x 192 against 75 of 128 x 192)
-  if (wide_ok && !(pv && atoi(pv) == 2) && p.M >= 32768) {
+  // smaller workgroups (B = 1: 147 of 64 x 192 against 75 of 128 x 192).  All three MFMA
+  // kernels accumulate in the same k order and round at the same points (bit-identical).
+  if (wide_ok && p.M >= 32768) {
     dim3 grid((p.M + kGT - 1) / kGT, embed / kGN);
     hipLaunchKernelGGL(patch_gemm_kernel, grid, dim3(256), 0, s, p);
-  } else if (wide_ok) {  // VM_PATCH_KERNEL=2: the 64x192 register-fragment kernel
+  } else if (wide_ok) {  // the 64x192 register-fragment kernel
     dim3 grid((p.M + kPT - 1) / kPT, embed / kPN);
     hipLaunchKernelGGL(patch_mfma16_kernel, grid, dim3(256), 0, s, p);
   } else if (mfma_ok) {

@@ -26,11 +26,12 @@ struct ScanParams {
 
 // Token-major path (vm_scan_seq.hip).  Workspace for the time-segmented form, in bytes;
 // 0 when the single-pass form is chosen.  `segments` receives the chosen segment count.
-size_t seq_workspace_bytes(int batch, int dim, int seqlen, int* segments);
+// segments: 0 = cost model, > 0 forced.
+size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen);
 // Launch; `workspace` must hold seq_workspace_bytes() (or be larger).  Returns false when
 // the operands do not fit the token-major kernels (the caller reports the error).
 bool seq_supported(const ScanParams& p, int dtype);
-void seq_launch(const ScanParams& p, int dtype, void* workspace, size_t workspace_bytes,
-                hipStream_t s);
+void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
+                size_t workspace_bytes, hipStream_t s);
 
 }  // namespace vm

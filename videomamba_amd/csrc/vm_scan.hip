@@ -1,25 +1,21 @@
-// Selective scan (forward) and one-token state update for gfx950.
+// Channel-major selective scan (forward) and the one-token state update for gfx950.
 //
 // Replaces mamba-ssm's selective_scan_fn / selective_state_update as called by the
 // reference at models/videomamba/mamba_simple.py:122-172 and :483-494; the math is
 // _selective_scan_ref (mamba_simple.py:30-106): fp32 internally, softplus threshold 20,
 // output rounded to the input dtype, state carried in fp32.
 //
-// Work decomposition (MI355X-first, not a translation of the CUDA kernel):
-//   * a wave holds CPW = 64/LPC channels; within a channel LPC lanes cover LPC*K
-//     consecutive timesteps (K per lane, sequential inside the lane);
-//   * a workgroup = NW waves = NW*CPW channels of one batch row; it sweeps the sequence
-//     in blocks of LPC*K timesteps, carrying h per (channel, state) in the first lane of
-//     each channel's lane row;
-//   * per state n: each lane folds its K steps into an (a, b) pair, the pairs are
-//     combined across the LPC lanes with a DPP Hillis-Steele scan (row_shr 1/2/4/8,
-//     row_bcast 15/31 for 64-lane rows), the carry enters as the first lane's initial b,
-//     and each lane re-sweeps its K steps from its exclusive prefix to emit y;
-//   * B_t / C_t (shared by every channel of the batch row) are staged once per block in
-//     LDS as fp32 and read with ds_read_b128; u / delta / z / out are read with 16-byte
-//     vector loads along the contiguous sequence axis.
-// Per (element, state) the VALU cost is 2 exp-equivalents + ~6 FMA-class ops; the
-// scan adds ~(4*steps+3)/K per element-state.
+// This file holds the time-parallel kernel for channel-major operands (unit step stride;
+// the small-batch mixer layout) and the ABI entry points, which route token-major operands
+// (unit channel stride) to vm_scan_seq.hip.  Measured-loser variants of round 1 (v1-v4, the
+// time-split form) live in tools/probes/scan_variants_r01.hip and are not built.
+//
+// scan_v5_kernel: one wave per channel row; lane l covers K consecutive steps of a
+// 64*K-step block.  Per state n: a lane-local fold of its K steps into (a, b), a DPP
+// Hillis-Steele scan over the 64 lanes (row_shr 1/2/4/8, row_bcast 15/31) whose range
+// products are exp2 of delta prefix sums (state-independent, off the serial chain), the
+// block carry entering at lane 0, and a re-sweep emitting y.  B_t / C_t rows are staged
+// per block in LDS as fp32.
 
 #include <stdlib.h>
 
@@ -28,655 +24,10 @@
 namespace vm {
 
 template <int CTRL, int ROWMASK = 0xf>
-__device__ __forceinline__ float dpp_f(float old, float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v),
-                                                    CTRL, ROWMASK, 0xf, false));
-}
-
-// One Hillis-Steele step of the (a, b) composition  (a_l,b_l) o (a,b) = (a_l a, a b_l + b)
-// with the left operand taken from the lane selected by DPP control CTRL.
-template <int CTRL, int ROWMASK = 0xf, bool NEED_A = true>
-__device__ __forceinline__ void scan_step(float& a, float& b) {
-  const float bl = dpp_f<CTRL, ROWMASK>(0.0f, b);
-  if (NEED_A) {
-    const float al = dpp_f<CTRL, ROWMASK>(1.0f, a);
-    b = fmaf(a, bl, b);
-    a = a * al;
-  } else {
-    b = fmaf(a, bl, b);
-  }
-}
-
-// Inclusive scan over LPC lanes (16 or 64); only b is needed afterwards.
-template <int LPC>
-__device__ __forceinline__ void pair_scan(float a, float& b) {
-  scan_step<0x111>(a, b);  // row_shr:1
-  scan_step<0x112>(a, b);  // row_shr:2
-  scan_step<0x114>(a, b);  // row_shr:4
-  if (LPC == 16) {
-    scan_step<0x118, 0xf, false>(a, b);  // row_shr:8
-  } else {
-    scan_step<0x118>(a, b);               // row_shr:8
-    scan_step<0x142, 0xa>(a, b);          // row_bcast:15 -> rows 1,3
-    scan_step<0x143, 0xc, false>(a, b);   // row_bcast:31 -> rows 2,3
-  }
-}
-
-// Exclusive shift by one lane inside the LPC-lane row; the row's first lane gets `first`.
-template <int LPC>
-__device__ __forceinline__ float excl_shift(float first, float b) {
-  return LPC == 16 ? dpp_f<0x111>(first, b) : dpp_f<0x138>(first, b);  // row_shr:1 / wave_shr:1
-}
-
-// Move the row's last-lane value to the row's first lane (row_ror:1 / wave_ror:1).
-template <int LPC>
-__device__ __forceinline__ float last_to_first(float v) {
-  return LPC == 16 ? dpp_f<0x121>(0.0f, v) : dpp_f<0x13C>(0.0f, v);
-}
-
-template <typename T, int K>
-__device__ __forceinline__ void load_k(const T* row, int t0, int seqlen, bool vec, float (&v)[K]) {
-  if (vec && t0 + K <= seqlen) {
-#pragma unroll
-    for (int j = 0; j < K; j += 8) {
-      float w[8];
-      load8(row + t0 + j, w);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[j + i] = w[i];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = (t0 + k < seqlen) ? to_f32(row[t0 + k]) : 0.0f;
-  }
-}
-
-template <typename T, int K>
-__device__ __forceinline__ void store_k(T* row, int t0, int seqlen, bool vec, const float (&v)[K]) {
-  if (vec && t0 + K <= seqlen) {
-#pragma unroll
-    for (int j = 0; j < K; j += 8) {
-      float w[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) w[i] = v[j + i];
-      store8(row + t0 + j, w);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (t0 + k < seqlen) row[t0 + k] = from_f32<T>(v[k]);
-  }
-}
-
-template <typename T, int K, int LPC, int NW>
-__global__ __launch_bounds__(64 * NW) void scan_fwd_kernel(const ScanParams p) {
-  constexpr int CPW = 64 / LPC;   // channels per wave
-  constexpr int TB = LPC * K;     // timesteps per block
-  __shared__ __attribute__((aligned(16))) float sBC[2 * kMaxN * TB];
-  float* sB = sBC;
-  float* sC = sBC + kMaxN * TB;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int rl = lane & (LPC - 1);        // lane inside the channel's row
-  const int b = blockIdx.y;
-  const int d_raw = (blockIdx.x * NW + wave) * CPW + lane / LPC;
-  const bool active = d_raw < p.dim;
-  const int d = active ? d_raw : p.dim - 1;
-  const int N = p.dstate;
-  const int L = p.seqlen;
-
-  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
-  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
-  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
-  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
-  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
-  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
-
-  float A2[kMaxN], carry[kMaxN];
-#pragma unroll
-  for (int n = 0; n < kMaxN; ++n) {
-    A2[n] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
-    carry[n] = (n < N && p.h0 && rl == 0)
-                   ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
-  }
-  const float Dv = p.D ? p.D[d] : 0.0f;
-  const float bias = p.dbias ? p.dbias[d] : 0.0f;
-  const bool vx = p.vec_x != 0;
-
-  const int LO = p.out_len;  // columns [L, LO) are written as 0
-  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
-    // ---- stage B/C for this block (fp32 in LDS) ----
-    __syncthreads();
-    const int chunks = 2 * N * (TB / 8);
-    for (int idx = tid; idx < chunks; idx += 64 * NW) {
-      const int row = idx / (TB / 8);
-      const int c8 = idx - row * (TB / 8);
-      const bool isC = row >= N;
-      const int n = isC ? row - N : row;
-      const T* src = isC ? Cb + n * p.c_sn : Bb + n * p.b_sn;
-      float* dst = (isC ? sC : sB) + n * TB + c8 * 8;
-      const int t = t_blk + c8 * 8;
-      float w[8];
-      if (p.vec_bc && t + 8 <= L) {
-        load8(src + t, w);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
-      }
-      *reinterpret_cast<float4*>(dst) = make_float4(w[0], w[1], w[2], w[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(w[4], w[5], w[6], w[7]);
-    }
-    __syncthreads();
-
-    // ---- per-lane elementwise prologue ----
-    const int t0 = t_blk + rl * K;
-    float dl[K], du[K], y[K];
-    {
-      float uv[K], dv[K];
-      load_k<T, K>(urow, t0, L, vx, uv);
-      load_k<T, K>(drow, t0, L, vx, dv);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float dd = dv[k] + bias;
-        if (p.softplus) dd = softplus(dd);
-        dd = (t0 + k < L) ? dd : 0.0f;  // padded steps are the identity (a=1, b=0)
-        dl[k] = dd;
-        du[k] = dd * uv[k];
-        y[k] = Dv * uv[k];
-      }
-    }
-    float sd = 0.0f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) sd += dl[k];
-
-    // ---- scan over states ----
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n) {
-      if (n < N) {
-        const float* bs = sB + n * TB + rl * K;
-        const float* cs = sC + n * TB + rl * K;
-        float a[K], bb[K];
-        float fold = 0.0f;
-#pragma unroll
-        for (int k = 0; k < K; k += 4) {
-          const float4 bq = *reinterpret_cast<const float4*>(bs + k);
-          const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            a[k + i] = __builtin_amdgcn_exp2f(dl[k + i] * A2[n]);
-            bb[k + i] = du[k + i] * bv[i];
-            fold = fmaf(a[k + i], fold, bb[k + i]);
-          }
-        }
-        const float aa = __builtin_amdgcn_exp2f(sd * A2[n]);
-        // carry enters as the initial state of the row's first lane
-        fold = fmaf(aa, carry[n], fold);
-        pair_scan<LPC>(aa, fold);
-        float h = excl_shift<LPC>(carry[n], fold);
-#pragma unroll
-        for (int k = 0; k < K; k += 4) {
-          const float4 cq = *reinterpret_cast<const float4*>(cs + k);
-          const float cv[4] = {cq.x, cq.y, cq.z, cq.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            h = fmaf(a[k + i], h, bb[k + i]);
-            y[k + i] = fmaf(h, cv[i], y[k + i]);
-          }
-        }
-        const float nc = last_to_first<LPC>(fold);
-        carry[n] = (rl == 0) ? nc : 0.0f;
-      }
-    }
-
-    // ---- gate and store ----
-    if (zrow) {
-      float zv[K];
-      load_k<T, K>(zrow, t0, L, vx, zv);
-#pragma unroll
-      for (int k = 0; k < K; ++k) y[k] *= silu(zv[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
-    if (active) store_k<T, K>(orow, t0, LO, vx, y);
-  }
-
-  if (p.hl && active && rl == 0) {
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n)
-      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[n]);
-  }
-}
-
-// --------------------------------------------------------------------- scan v3
-// Throughput path.  One wave = one channel row (b, d); lanes over time, K steps per lane,
-// blocks of 64*K steps; a workgroup = NW channels of one batch row sharing the B/C
-// staging.  Per block the per-lane delta sums and their 64-lane prefix structure are
-// computed once; per state the Hillis-Steele (a, b) scan then needs only
-//     b += exp2(A * S_range) * dpp_shift(b)
-// where S_range (sum of delta over the lanes the current pair already covers) is
-// state-independent, so the exps sit off the serial DPP chain and invalid DPP sources
-// read 0 (bound_ctrl) with no "old"-value moves.  G states are interleaved per pass
-// (G independent fold / scan / sweep chains).  B/C are staged per block in LDS as fp32
-// in a [state][K/4][lane][4] layout: every ds_read_b128 is 64 consecutive 16-byte words.
-template <int CTRL, int ROWMASK = 0xf>
 __device__ __forceinline__ float dppz(float v) {  // invalid source lanes read 0
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, true));
 }
 
-template <typename T, int K, int G, int NW, int ABL = 0>
-__global__ __launch_bounds__(64 * NW) void scan_v3_kernel(const ScanParams p) {
-  // ABL (timing-only ablations): 1 no DPP scan, 2 no exp, 4 no B/C staging, 8 no x loads
-  constexpr int TB = 64 * K;
-  constexpr int KQ = K / 4;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sB = smem;                  // [kMaxN][KQ][64][4]
-  float* sC = smem + kMaxN * TB;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.y;
-  const int d_raw = blockIdx.x * NW + wave;
-  const bool active = d_raw < p.dim;
-  const int d = active ? d_raw : p.dim - 1;
-  const int N = p.dstate;
-  const int L = p.seqlen;
-  const int LO = p.out_len;
-  const bool vx = p.vec_x != 0;
-
-  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
-  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
-  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
-  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
-  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
-  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
-
-  float A2[kMaxN], carry[kMaxN];  // wave-uniform
-#pragma unroll
-  for (int n = 0; n < kMaxN; ++n) {
-    A2[n] = (n < N) ? p.A[d * N + n] * kLog2e : 0.0f;
-    carry[n] = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) : 0.0f;
-  }
-  const float Dv = p.D ? p.D[d] : 0.0f;
-  const float bias = p.dbias ? p.dbias[d] : 0.0f;
-
-  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
-    // ---- stage B/C (fp32, lane-interleaved) ----
-    __syncthreads();
-    const int chunks = (ABL & 4) ? 0 : 2 * N * (TB / 8);
-    for (int idx = tid; idx < chunks; idx += 64 * NW) {
-      const int row = idx / (TB / 8);
-      const int c8 = idx - row * (TB / 8);
-      const bool isC = row >= N;
-      const int n = isC ? row - N : row;
-      const T* src = isC ? Cb + n * p.c_sn : Bb + n * p.b_sn;
-      const int t = t_blk + c8 * 8;
-      float w[8];
-      if (p.vec_bc && t + 8 <= L) {
-        load8(src + t, w);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w[j] = (t + j < L) ? to_f32(src[t + j]) : 0.0f;
-      }
-      // block-relative step r = c8*8 + j -> lane r/K, k = r%K
-      float* base = (isC ? sC : sB) + n * TB;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int r = c8 * 8 + 4 * q;
-        const int ln = r / K, k = r - ln * K;
-        *reinterpret_cast<float4*>(base + ((k >> 2) * 64 + ln) * 4) =
-            make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-      }
-    }
-    if (!(ABL & 4)) __syncthreads();
-
-    // ---- per-lane prologue ----
-    const int t0 = t_blk + lane * K;
-    float dl[K], du[K], y[K];
-    {
-      float uv[K], dv[K];
-      if (ABL & 8) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) { uv[k] = 0.001f * (t0 + k); dv[k] = -4.0f + 0.0001f * k; }
-      } else {
-        load_k<T, K>(urow, t0, L, vx, uv);
-        load_k<T, K>(drow, t0, L, vx, dv);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float dd = dv[k] + bias;
-        if (p.softplus) dd = softplus(dd);
-        dd = (t0 + k < L) ? dd : 0.0f;
-        dl[k] = dd;
-        du[k] = dd * uv[k];
-        y[k] = Dv * uv[k];
-      }
-    }
-    // delta range sums for the scan steps (state independent)
-    float sd = 0.0f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) sd += dl[k];
-    float prow = sd;
-    float s1, s2, s4, s8;
-    {
-      float t = dppz<0x111>(prow); s1 = prow;            prow += t;
-      t = dppz<0x112>(prow);       s2 = prow;            prow += t;
-      t = dppz<0x114>(prow);       s4 = prow;            prow += t;
-      t = dppz<0x118>(prow);       s8 = prow;            prow += t;
-    }
-    // s1 = sd, s2 = sum of lanes (i-1, i], s4 = (i-3, i], s8 = (i-7, i] within the row
-    const float srow = prow;                 // row-inclusive prefix: range before bcast15
-    const float shalf = prow + dppz<0x142, 0xa>(prow);  // half-inclusive: range before bcast31
-
-    // ---- states, G at a time ----
-#pragma unroll
-    for (int n0 = 0; n0 < kMaxN; n0 += G) {
-      if (n0 < N) {
-        float a[G][K], bb[G][K], fold[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int n = n0 + g;
-          const float* bs = sB + n * TB + lane * 4;
-          fold[g] = 0.0f;
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq) {
-            const float4 q = *reinterpret_cast<const float4*>(bs + kq * 256);
-            const float bv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int k = kq * 4 + i;
-              a[g][k] = (ABL & 2) ? fmaf(dl[k], A2[n], 1.0f) : __builtin_amdgcn_exp2f(dl[k] * A2[n]);
-              bb[g][k] = du[k] * bv[i];
-              fold[g] = fmaf(a[g][k], fold[g], bb[g][k]);
-            }
-          }
-        }
-        // carry enters the wave at lane 0
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int n = n0 + g;
-          const float aa = __builtin_amdgcn_exp2f(sd * A2[n]);
-          if (lane == 0) fold[g] = fmaf(aa, carry[n], fold[g]);
-        }
-        // 64-lane inclusive scan of b; a-products from the delta range sums
-#pragma unroll
-        for (int g = 0; g < (ABL & 1 ? 0 : G); ++g) {
-          const int n = n0 + g;
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(s1 * A2[n]), dppz<0x111>(fold[g]), fold[g]);
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(s2 * A2[n]), dppz<0x112>(fold[g]), fold[g]);
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(s4 * A2[n]), dppz<0x114>(fold[g]), fold[g]);
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(s8 * A2[n]), dppz<0x118>(fold[g]), fold[g]);
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(srow * A2[n]), dppz<0x142, 0xa>(fold[g]), fold[g]);
-          fold[g] = fmaf(__builtin_amdgcn_exp2f(shalf * A2[n]), dppz<0x143, 0xc>(fold[g]), fold[g]);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int n = n0 + g;
-          float h = dppz<0x138>(fold[g]);  // wave_shr:1: exclusive prefix (lane 0 reads 0)
-          if (lane == 0) h = carry[n];
-          carry[n] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[g]), 63));
-          const float* cs = sC + n * TB + lane * 4;
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq) {
-            const float4 q = *reinterpret_cast<const float4*>(cs + kq * 256);
-            const float cv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int k = kq * 4 + i;
-              h = fmaf(a[g][k], h, bb[g][k]);
-              y[k] = fmaf(h, cv[i], y[k]);
-            }
-          }
-        }
-      }
-    }
-
-    if (zrow) {
-      float zv[K];
-      load_k<T, K>(zrow, t0, L, vx, zv);
-#pragma unroll
-      for (int k = 0; k < K; ++k) y[k] *= silu(zv[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
-    if (active && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y);
-  }
-
-  if (p.hl && active && lane == 0) {
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n)
-      if (n < N) store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype, carry[n]);
-  }
-}
-
-template <typename T, int K, int G, int NW, int ABL = 0>
-static void launch_v3(const ScanParams& p, hipStream_t s) {
-  const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
-  dim3 grid((p.dim + NW - 1) / NW, p.batch);
-  hipLaunchKernelGGL((scan_v3_kernel<T, K, G, NW, ABL>), grid, dim3(64 * NW), lds, s, p);
-}
-
-// --------------------------------------------------------------------- scan v4
-// Production throughput path.  gfx950 issues a wave64 fp32 VALU op in ~4 cycles, so the
-// fp32 peak needs packed math: the states are processed in pairs held in float2
-// (v_pk_mul_f32 / v_pk_fma_f32), two independent pair-chains per pass (P).  The rest is
-// v3's structure: one wave per channel row, lanes over time (K steps per lane), blocks
-// of 64*K steps, B/C staged per block in LDS as fp32 laid out [pair][K/2][lane][4]
-// (4 = two steps x two states: one conflict-free ds_read_b128 per two steps), 64-lane
-// DPP scan of b with the range products E_o built recursively from the neighbours'
-// products (E_2o = E_o * shift_o(E_o)) plus two exps for the row/half spans.
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 exp2v(f2 x) {
-  return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-}
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-template <int CTRL, int ROWMASK = 0xf>
-__device__ __forceinline__ f2 dppz2(f2 v) { return f2{dppz<CTRL, ROWMASK>(v.x), dppz<CTRL, ROWMASK>(v.y)}; }
-
-template <typename T, int K, int P, int NW>
-__global__ __launch_bounds__(64 * NW) void scan_v4_kernel(const ScanParams p) {
-  constexpr int TB = 64 * K;
-  constexpr int K2 = K / 2;
-  constexpr int NP = kMaxN / 2;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sB = smem;                 // [NP][K2][64][4]
-  float* sC = smem + kMaxN * TB;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.y;
-  const int d_raw = blockIdx.x * NW + wave;
-  const bool active = d_raw < p.dim;
-  const int d = active ? d_raw : p.dim - 1;
-  const int N = p.dstate;
-  const int NPr = (N + 1) >> 1;
-  const int L = p.seqlen;
-  const int LO = p.out_len;
-  const bool vx = p.vec_x != 0;
-
-  const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + d * p.u_sd;
-  const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + d * p.dl_sd;
-  const T* zrow = p.z ? static_cast<const T*>(p.z) + b * p.z_sb + d * p.z_sd : nullptr;
-  T* orow = static_cast<T*>(p.out) + b * p.o_sb + d * p.o_sd;
-  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
-  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
-
-  f2 A2[NP], carry[NP];  // wave-uniform
-#pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const int n0 = 2 * q, n1 = 2 * q + 1;
-    A2[q] = f2{n0 < N ? p.A[d * N + n0] * kLog2e : 0.0f, n1 < N ? p.A[d * N + n1] * kLog2e : 0.0f};
-    const long long hb = b * p.h0_sb + d * p.h0_sd;
-    carry[q] = f2{(n0 < N && p.h0) ? load_dyn(p.h0, hb + n0, p.h0_dtype) : 0.0f,
-                  (n1 < N && p.h0) ? load_dyn(p.h0, hb + n1, p.h0_dtype) : 0.0f};
-  }
-  const float Dv = p.D ? p.D[d] : 0.0f;
-  const float bias = p.dbias ? p.dbias[d] : 0.0f;
-
-  for (int t_blk = 0; t_blk < LO; t_blk += TB) {
-    // ---- stage B/C: thread = (B|C, state pair, 8-step chunk) ----
-    __syncthreads();
-    const int chunks = 2 * NPr * (TB / 8);
-    for (int idx = tid; idx < chunks; idx += 64 * NW) {
-      const int row = idx / (TB / 8);
-      const int c8 = idx - row * (TB / 8);
-      const bool isC = row >= NPr;
-      const int q = isC ? row - NPr : row;
-      const T* src = isC ? Cb : Bb;
-      const long long sn = isC ? p.c_sn : p.b_sn;
-      const int t = t_blk + c8 * 8;
-      float w0[8], w1[8];
-      const bool has1 = 2 * q + 1 < N;
-      if (p.vec_bc && t + 8 <= L) {
-        load8(src + (2 * q) * sn + t, w0);
-        if (has1) load8(src + (2 * q + 1) * sn + t, w1);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          w0[j] = (t + j < L) ? to_f32(src[(2 * q) * sn + t + j]) : 0.0f;
-          w1[j] = (has1 && t + j < L) ? to_f32(src[(2 * q + 1) * sn + t + j]) : 0.0f;
-        }
-      }
-      if (!has1) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w1[j] = 0.0f;
-      }
-      const int r = c8 * 8;           // block-relative first step of the chunk
-      const int ln = r / K, kb = r - ln * K;
-      float* base = (isC ? sC : sB) + q * K2 * 256;
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const int k2 = (kb + j) >> 1;
-        *reinterpret_cast<float4*>(base + (k2 * 64 + ln) * 4) =
-            make_float4(w0[j], w1[j], w0[j + 1], w1[j + 1]);
-      }
-    }
-    __syncthreads();
-
-    // ---- per-lane prologue ----
-    const int t0 = t_blk + lane * K;
-    float dl[K], du[K];
-    f2 y2[K];
-    {
-      float uv[K], dv[K];
-      load_k<T, K>(urow, t0, L, vx, uv);
-      load_k<T, K>(drow, t0, L, vx, dv);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float dd = dv[k] + bias;
-        if (p.softplus) dd = softplus_fast(dd);
-        dd = (t0 + k < L) ? dd : 0.0f;
-        dl[k] = dd;
-        du[k] = dd * uv[k];
-        y2[k] = f2{Dv * uv[k], 0.0f};
-      }
-    }
-    float sd = 0.0f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) sd += dl[k];
-    float srow = sd;
-    srow += dppz<0x111>(srow);
-    srow += dppz<0x112>(srow);
-    srow += dppz<0x114>(srow);
-    srow += dppz<0x118>(srow);                         // row-inclusive delta sum
-    const float shalf = srow + dppz<0x142, 0xa>(srow);  // half-inclusive delta sum
-
-    // ---- state pairs, P per pass ----
-#pragma unroll
-    for (int q0 = 0; q0 < NP; q0 += P) {
-      if (q0 < NPr) {
-        f2 a[P][K], bb[P][K], fold[P];
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-          const int q = q0 + j;
-          const float* bs = sB + q * K2 * 256 + lane * 4;
-          fold[j] = f2{0.0f, 0.0f};
-#pragma unroll
-          for (int k2 = 0; k2 < K2; ++k2) {
-            const float4 v = *reinterpret_cast<const float4*>(bs + k2 * 256);
-            const f2 bv[2] = {f2{v.x, v.y}, f2{v.z, v.w}};
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const int k = 2 * k2 + i;
-              a[j][k] = exp2v(A2[q] * dl[k]);
-              bb[j][k] = bv[i] * du[k];
-              fold[j] = fma2(a[j][k], fold[j], bb[j][k]);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-          const int q = q0 + j;
-          const f2 e1 = exp2v(A2[q] * sd);  // product over the lane's own steps
-          if (lane == 0) fold[j] = fma2(e1, carry[q], fold[j]);
-          const f2 e2 = e1 * dppz2<0x111>(e1);
-          const f2 e4 = e2 * dppz2<0x112>(e2);
-          const f2 e8 = e4 * dppz2<0x114>(e4);
-          fold[j] = fma2(e1, dppz2<0x111>(fold[j]), fold[j]);
-          fold[j] = fma2(e2, dppz2<0x112>(fold[j]), fold[j]);
-          fold[j] = fma2(e4, dppz2<0x114>(fold[j]), fold[j]);
-          fold[j] = fma2(e8, dppz2<0x118>(fold[j]), fold[j]);
-          fold[j] = fma2(exp2v(A2[q] * srow), dppz2<0x142, 0xa>(fold[j]), fold[j]);
-          fold[j] = fma2(exp2v(A2[q] * shalf), dppz2<0x143, 0xc>(fold[j]), fold[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-          const int q = q0 + j;
-          f2 h = dppz2<0x138>(fold[j]);  // exclusive prefix
-          if (lane == 0) h = carry[q];
-          carry[q] = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[j].x), 63)),
-                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fold[j].y), 63))};
-          const float* cs = sC + q * K2 * 256 + lane * 4;
-#pragma unroll
-          for (int k2 = 0; k2 < K2; ++k2) {
-            const float4 v = *reinterpret_cast<const float4*>(cs + k2 * 256);
-            const f2 cv[2] = {f2{v.x, v.y}, f2{v.z, v.w}};
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const int k = 2 * k2 + i;
-              h = fma2(a[j][k], h, bb[j][k]);
-              y2[k] = fma2(h, cv[i], y2[k]);
-            }
-          }
-        }
-      }
-    }
-
-    float y[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) y[k] = y2[k].x + y2[k].y;
-    if (zrow) {
-      float zv[K];
-      load_k<T, K>(zrow, t0, L, vx, zv);
-#pragma unroll
-      for (int k = 0; k < K; ++k) y[k] *= silu_fast(zv[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) y[k] = (t0 + k < L) ? y[k] : 0.0f;
-    if (active && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y);
-  }
-
-  if (p.hl && active && lane == 0) {
-    const long long hb = b * p.hl_sb + d * p.hl_sd;
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      if (2 * q < N) store_dyn(p.hl, hb + 2 * q, p.hl_dtype, carry[q].x);
-      if (2 * q + 1 < N) store_dyn(p.hl, hb + 2 * q + 1, p.hl_dtype, carry[q].y);
-    }
-  }
-}
-
-template <typename T, int K, int P, int NW>
-static void launch_v4(const ScanParams& p, hipStream_t s) {
-  const size_t lds = 2 * kMaxN * 64 * K * sizeof(float);
-  dim3 grid((p.dim + NW - 1) / NW, p.batch);
-  hipLaunchKernelGGL((scan_v4_kernel<T, K, P, NW>), grid, dim3(64 * NW), lds, s, p);
-}
-
-// --------------------------------------------------------------------- scan v5
 // Scalar-math successor of v4 (measured on gfx950: v_pk_fma_f32 costs ~2x v_fma_f32 per
 // wave instruction, so packing buys nothing; v_exp_f32 ~3x).  One state per pass, K
 // steps per lane with any even K (K=10 covers L=3137 in 5 blocks of 640 at 98% lane
@@ -1065,182 +416,6 @@ static void launch_v5_auto(const ScanParams& p, hipStream_t s) {
   else launch_v5<T, 8, 8>(p, s);
 }
 
-// --------------------------------------------------------------------- time-split scan
-// Scan v2 (the production path).  A workgroup owns NC channels of one batch row and the
-// WHOLE sequence: S waves (S <= 8) each cover 64*K consecutive timesteps, K per lane.
-// Per state n:
-//   1. each lane folds its K steps of every channel into (a, b) pairs (zero carry),
-//      a 64-lane DPP scan gives the in-wave inclusive b, and lane 63 publishes the wave
-//      total b to LDS (double-buffered by state parity);
-//   2. one workgroup barrier;
-//   3. each wave composes the totals of the waves before it onto the block carry (the
-//      wave products are exp2(A*sum(delta)), from per-wave delta sums published once per
-//      super-block), gets its lanes' carry-in as exp2(A*prefix_delta)*carry + b_excl,
-//      and re-sweeps its K steps emitting y += C*h.
-// B_t / C_t rows are read straight from L2 with 16-byte loads and shared by the NC
-// channels of the wave.  Sequences longer than 8*64*K run as super-blocks with the
-// block carry composed through all S waves.
-template <typename T, int K>
-__device__ __forceinline__ void load_row_k(const T* row, int t0, int L, bool vec, float (&v)[K]) {
-  load_k<T, K>(row, t0, L, vec, v);
-}
-
-__device__ __forceinline__ float wave_incl_sum(float v) {
-  v += dpp_f<0x111>(0.0f, v);
-  v += dpp_f<0x112>(0.0f, v);
-  v += dpp_f<0x114>(0.0f, v);
-  v += dpp_f<0x118>(0.0f, v);
-  v += dpp_f<0x142, 0xa>(0.0f, v);
-  v += dpp_f<0x143, 0xc>(0.0f, v);
-  return v;
-}
-
-template <typename T, int K, int NC>
-__global__ __launch_bounds__(512) void scan_tw_kernel(const ScanParams p, const int S) {
-  constexpr int TW = 64 * K;
-  __shared__ float s_sdw[NC][8];
-  __shared__ float s_bt[2][NC][8];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b = blockIdx.y;
-  const int N = p.dstate;
-  const int L = p.seqlen;
-  const int LO = p.out_len;
-  const int SB = S * TW;
-  const bool vx = p.vec_x != 0;
-  const bool vbc = p.vec_bc != 0;
-
-  int dch[NC];
-  bool act[NC];
-  float A2[NC][kMaxN], carry[NC][kMaxN], Dv[NC], bias[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int dr = blockIdx.x * NC + c;
-    act[c] = dr < p.dim;
-    dch[c] = act[c] ? dr : p.dim - 1;
-    Dv[c] = p.D ? p.D[dch[c]] : 0.0f;
-    bias[c] = p.dbias ? p.dbias[dch[c]] : 0.0f;
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n) {
-      A2[c][n] = (n < N) ? p.A[dch[c] * N + n] * kLog2e : 0.0f;
-      carry[c][n] = (n < N && p.h0)
-          ? load_dyn(p.h0, b * p.h0_sb + dch[c] * p.h0_sd + n, p.h0_dtype) : 0.0f;
-    }
-  }
-  const T* Bb = static_cast<const T*>(p.B) + b * p.b_sb;
-  const T* Cb = static_cast<const T*>(p.C) + b * p.c_sb;
-
-  for (int t_sb = 0; t_sb < LO; t_sb += SB) {
-    const int t0 = t_sb + wave * TW + lane * K;
-    const bool more = t_sb + SB < L;  // another super-block follows: keep the block carry
-    float dl[NC][K], du[NC][K], y[NC][K], sd[NC], psd_ex[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const T* urow = static_cast<const T*>(p.u) + b * p.u_sb + dch[c] * p.u_sd;
-      const T* drow = static_cast<const T*>(p.delta) + b * p.dl_sb + dch[c] * p.dl_sd;
-      float uv[K], dv[K];
-      load_k<T, K>(urow, t0, L, vx, uv);
-      load_k<T, K>(drow, t0, L, vx, dv);
-      sd[c] = 0.0f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float dd = dv[k] + bias[c];
-        if (p.softplus) dd = softplus(dd);
-        dd = (t0 + k < L) ? dd : 0.0f;
-        dl[c][k] = dd;
-        du[c][k] = dd * uv[k];
-        y[c][k] = Dv[c] * uv[k];
-        sd[c] += dd;
-      }
-      const float incl = wave_incl_sum(sd[c]);
-      psd_ex[c] = incl - sd[c];
-      if (lane == 63) s_sdw[c][wave] = incl;
-    }
-
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n) {
-      if (n < N) {
-        float bv[K];
-        load_k<T, K>(Bb + n * p.b_sn, t0, L, vbc, bv);
-        float a[NC][K], bb[NC][K], fold[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          fold[c] = 0.0f;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            a[c][k] = __builtin_amdgcn_exp2f(dl[c][k] * A2[c][n]);
-            bb[c][k] = du[c][k] * bv[k];
-            fold[c] = fmaf(a[c][k], fold[c], bb[c][k]);
-          }
-          const float aa = __builtin_amdgcn_exp2f(sd[c] * A2[c][n]);
-          pair_scan<64>(aa, fold[c]);
-          if (lane == 63) s_bt[n & 1][c][wave] = fold[c];
-        }
-        __syncthreads();
-        float cv[K];
-        load_k<T, K>(Cb + n * p.c_sn, t0, L, vbc, cv);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          // carry entering this wave: compose the totals of the earlier waves
-          float hc = carry[c][n];
-          float nxt = 0.0f;
-          const int upto = more ? S : wave;
-          for (int w = 0; w < upto; ++w) {
-            const float e = __builtin_amdgcn_exp2f(A2[c][n] * s_sdw[c][w]);
-            const float v = fmaf(e, hc, s_bt[n & 1][c][w]);
-            hc = (w < wave) ? v : hc;
-            nxt = v;
-          }
-          if (more) carry[c][n] = nxt;
-          const float bex = dpp_f<0x138>(0.0f, fold[c]);  // wave_shr:1 -> exclusive b
-          float h = fmaf(__builtin_amdgcn_exp2f(A2[c][n] * psd_ex[c]), hc, bex);
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            h = fmaf(a[c][k], h, bb[c][k]);
-            y[c][k] = fmaf(h, cv[k], y[c][k]);
-          }
-          // the final state is the last wave's last lane after the sweep
-          if (!more && p.hl && act[c] && wave == S - 1 && lane == 63)
-            store_dyn(p.hl, b * p.hl_sb + dch[c] * p.hl_sd + n, p.hl_dtype, h);
-        }
-      }
-    }
-
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (p.z) {
-        const T* zrow = static_cast<const T*>(p.z) + b * p.z_sb + dch[c] * p.z_sd;
-        float zv[K];
-        load_k<T, K>(zrow, t0, L, vx, zv);
-#pragma unroll
-        for (int k = 0; k < K; ++k) y[c][k] *= silu(zv[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) y[c][k] = (t0 + k < L) ? y[c][k] : 0.0f;
-      T* orow = static_cast<T*>(p.out) + b * p.o_sb + dch[c] * p.o_sd;
-      if (act[c] && t0 < LO) store_k<T, K>(orow, t0, LO, vx, y[c]);
-    }
-    __syncthreads();  // s_sdw is rewritten by the next super-block
-  }
-  if (L == 0 && p.hl && wave == 0 && lane == 0) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (act[c])
-        for (int n = 0; n < N; ++n)
-          store_dyn(p.hl, b * p.hl_sb + dch[c] * p.hl_sd + n, p.hl_dtype, carry[c][n]);
-  }
-}
-
-template <typename T, int K, int NC>
-static void launch_tw(const ScanParams& p, hipStream_t s) {
-  constexpr int TW = 64 * K;
-  int S = (p.out_len + TW - 1) / TW;
-  S = S < 1 ? 1 : (S > 8 ? 8 : S);
-  dim3 grid((p.dim + NC - 1) / NC, p.batch);
-  hipLaunchKernelGGL((scan_tw_kernel<T, K, NC>), grid, dim3(64 * S), 0, s, p, S);
-}
-
 // --------------------------------------------------------------------- one-token step
 struct StepParams {
   void* state; const void* x; const void* dt; const float* A; const void* B; const void* C;
@@ -1274,58 +449,10 @@ __global__ __launch_bounds__(256) void state_update_kernel(const StepParams p) {
   static_cast<T*>(p.out)[b * p.o_sb + d] = from_f32<T>(y);
 }
 
-template <typename T, int K, int LPC, int NW>
-static void launch_scan(const ScanParams& p, hipStream_t s) {
-  constexpr int CPW = 64 / LPC;
-  dim3 grid((p.dim + NW * CPW - 1) / (NW * CPW), p.batch);
-  hipLaunchKernelGGL((scan_fwd_kernel<T, K, LPC, NW>), grid, dim3(64 * NW), 0, s, p);
-}
-
-// VM_SCAN_VARIANT selects an alternative kernel for A/B timing and cross-checks
-// (read per call so tests can sweep it); 0 = production choice.
-static int scan_variant() {
-  const char* e = getenv("VM_SCAN_VARIANT");
-  return e ? atoi(e) : 0;
-}
 
 template <typename T>
 static void dispatch_scan(const ScanParams& p, hipStream_t s) {
-  switch (scan_variant()) {
-    case 1: launch_scan<T, 8, 64, 4>(p, s); break;     // v1: channel-serial blocks
-    case 2: launch_scan<T, 16, 16, 4>(p, s); break;
-    case 3: launch_tw<T, 16, 1>(p, s); break;          // time-split, 1 channel x K=16
-    case 4: launch_tw<T, 8, 1>(p, s); break;
-    case 5: launch_tw<T, 8, 2>(p, s); break;           // time-split, 2 channels x K=8
-    case 6: launch_v3<T, 8, 1, 8>(p, s); break;
-    case 7: launch_v3<T, 8, 2, 4>(p, s); break;
-    case 8: launch_v3<T, 16, 2, 4>(p, s); break;
-    case 21: launch_v3<T, 8, 1, 8, 1>(p, s); break;   // ablations (timing only, wrong output)
-    case 22: launch_v3<T, 8, 1, 8, 2>(p, s); break;
-    case 24: launch_v3<T, 8, 1, 8, 4>(p, s); break;
-    case 28: launch_v3<T, 8, 1, 8, 8>(p, s); break;
-    case 29: launch_v3<T, 8, 1, 8, 15>(p, s); break;
-    case 23: launch_v3<T, 8, 1, 8, 3>(p, s); break;
-    case 9: launch_v3<T, 8, 2, 8>(p, s); break;
-    case 10: launch_v4<T, 8, 2, 8>(p, s); break;
-    case 11: launch_v4<T, 8, 1, 4>(p, s); break;
-    case 12: launch_v4<T, 16, 1, 4>(p, s); break;
-    case 13: launch_v4<T, 8, 1, 8>(p, s); break;      // v4: packed state pairs
-    case 14: launch_v5<T, 10, 8>(p, s); break;
-    case 15: launch_v5<T, 8, 4>(p, s); break;
-    case 16: launch_v5<T, 16, 4>(p, s); break;
-    case 17: launch_v5<T, 8, 8>(p, s); break;
-    case 18: launch_v5<T, 10, 8>(p, s, 0); break;     // v5 K=10 without the pipelined form
-    case 19: launch_v5<T, 10, 8>(p, s, 1); break;     // v5 K=10 pipelined at any grid (bf16)
-    case 30: launch_v5_split<T, 10, 10, 2>(p, s); break;  // states split over 2 waves
-    case 31: launch_v5_split<T, 10, 12, 2>(p, s); break;
-    case 32: launch_v5_split<T, 10, 16, 2>(p, s); break;
-    case 33: launch_v5_split<T, 10, 16, 4>(p, s); break;  // ... over 4 waves
-    case 34: launch_v5_split<T, 10, 12, 4>(p, s); break;
-    case 35: launch_v5_split<T, 8, 16, 4>(p, s); break;
-    case 36: launch_v5_split<T, 8, 8, 2>(p, s); break;   // 80 KB LDS: two workgroups per CU
-    case 37: launch_v5_split<T, 8, 6, 2>(p, s); break;
-    default: launch_v5_auto<T>(p, s); break;          // v5: scalar, K chosen per L
-  }
+  launch_v5_auto<T>(p, s);
 }
 
 }  // namespace vm
@@ -1344,7 +471,7 @@ extern "C" int vm_selective_scan_fwd(
     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
     void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
     int batch, int dim, int seqlen, int dstate, int dtype,
-    void* workspace, long long workspace_bytes, vm_stream_t stream) {
+    int segments, void* workspace, long long workspace_bytes, vm_stream_t stream) {
   if (!u || !delta || !A || !B || !C || !out) {
     vmhost::set_error("vm_selective_scan_fwd: null required pointer");
     return VM_E_INVALID;
@@ -1372,9 +499,9 @@ extern "C" int vm_selective_scan_fwd(
   p.softplus = delta_softplus; p.h0_dtype = h0_dtype; p.hl_dtype = hl_dtype;
   hipStream_t s = static_cast<hipStream_t>(stream);
   // Token-major operands (channel stride 1): channel-per-lane sequential kernels.
-  if (seq_supported(p, dtype) && scan_variant() == 0) {
-    seq_launch(p, dtype, workspace, workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0,
-               s);
+  if (seq_supported(p, dtype)) {
+    seq_launch(p, dtype, segments, workspace,
+               workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0, s);
     return vmhost::launch_status("vm_selective_scan_fwd");
   }
   // Channel-major operands (step stride 1): time-parallel kernels.
@@ -1397,9 +524,9 @@ extern "C" int vm_selective_scan_fwd(
 }
 
 extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen,
-                                                       int dstate) {
+                                                       int dstate, int segments) {
   if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN) return 0;
-  return static_cast<long long>(seq_workspace_bytes(batch, dim, seqlen, nullptr));
+  return static_cast<long long>(seq_workspace_bytes(batch, dim, seqlen, segments, nullptr));
 }
 
 extern "C" int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long long s_sd,

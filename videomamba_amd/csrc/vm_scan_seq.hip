@@ -441,167 +441,6 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 }
 
-// Two adjacent channels per lane (bf16, 16 states, B/C as scalar loads; opt-in, see
-// seq_two_channels for the measurement): one 4-byte load
-// or store moves both channels' u / delta / z / y, and the per-step fixed work (B/C unpack
-// on the scalar unit, waits, loop) is shared by two recurrences whose exp / FMA chains
-// interleave.  Same math and segment modes as scan_seq_kernel.
-template <int MODE, bool SP, bool HZ>
-__global__ __launch_bounds__(128) void scan_seq2_kernel(const ScanParams p, const SeqWork w) {
-  typedef __attribute__((address_space(4))) const uint32_t* cptr;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = blockIdx.x * 2 + wave;  // 128-channel group
-  if (g * 128 >= p.dim) return;         // no barriers in this kernel
-  const int seg = blockIdx.y;
-  const int b = blockIdx.z;
-  const int L = p.seqlen;
-  const int t_beg = seg * w.seg_len;
-  const int t_end = min(L, t_beg + w.seg_len);
-  const int d0 = __builtin_amdgcn_readfirstlane(g * 128);
-  const int dA = d0 + 2 * lane;
-  const bool active = dA < p.dim;       // dim is even: dA + 1 < dim as well
-  const int d = active ? dA : p.dim - 2;
-  const long long ws_row = (static_cast<long long>(b) * w.S + seg) * p.dim + d;
-
-  float A2[2][kMaxN], h[2][kMaxN], Dv[2], bias[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n) {
-      A2[c][n] = p.A[(d + c) * kMaxN + n] * kLog2e;
-      float h_init = 0.0f;
-      if constexpr (MODE == 0) {
-        if (p.h0) h_init = load_dyn(p.h0, b * p.h0_sb + (d + c) * p.h0_sd + n, p.h0_dtype);
-      }
-      if constexpr (MODE == 2) h_init = w.hin[(ws_row + c) * kMaxN + n];
-      h[c][n] = h_init;
-    }
-    Dv[c] = p.D ? p.D[d + c] : 0.0f;
-    bias[c] = p.dbias ? p.dbias[d + c] : 0.0f;
-  }
-  const int voff = (d - d0) * 2;
-  const int voff_st = active ? voff : kSeqDead;
-  const auto ur = uniform_rsrc(static_cast<const bf16_t*>(p.u) + b * p.u_sb + d0);
-  const auto dr_ = uniform_rsrc(static_cast<const bf16_t*>(p.delta) + b * p.dl_sb + d0);
-  const auto zr = uniform_rsrc(HZ ? static_cast<const bf16_t*>(p.z) + b * p.z_sb + d0
-                                  : static_cast<const bf16_t*>(p.u));
-  const auto orr = uniform_rsrc(static_cast<bf16_t*>(p.out) + b * p.o_sb + d0);
-  const int us = static_cast<int>(p.u_sl) * 2, ds = static_cast<int>(p.dl_sl) * 2;
-  const int zs = static_cast<int>(p.z_sl) * 2, os = static_cast<int>(p.o_sl) * 2;
-  const bf16_t* Bq = static_cast<const bf16_t*>(p.B) + b * p.b_sb;
-  const bf16_t* Cq = static_cast<const bf16_t*>(p.C) + b * p.c_sb;
-  uint32_t bcw[2][16];  // [step parity][B words 0..7 | C words 8..15]
-  auto bc_load = [&](int t, uint32_t (&dst)[16]) {
-    const cptr bp = (cptr)(Bq + static_cast<long long>(t) * p.b_sl);
-    const cptr cp = (cptr)(Cq + static_cast<long long>(t) * p.c_sl);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      dst[i] = bp[i];
-      if constexpr (MODE != 1) dst[8 + i] = cp[i];
-    }
-  };
-
-  __builtin_amdgcn_s_waitcnt(0);  // drain the parameter loads (see scan_seq_kernel)
-  const int tlast = L > 0 ? L - 1 : 0;
-  const int nsteps = t_end - t_beg;
-  uint32_t ru[kPF], rd[kPF], rz[kPF];
-  if (nsteps > 0) {
-#pragma unroll
-    for (int j = 0; j < kPF; ++j) {
-      const int t = min(t_beg + j, tlast);
-      ru[j] = __builtin_amdgcn_raw_buffer_load_b32(ur, voff, t * us, 0);
-      rd[j] = __builtin_amdgcn_raw_buffer_load_b32(dr_, voff, t * ds, 0);
-      rz[j] = HZ && MODE != 1 ? __builtin_amdgcn_raw_buffer_load_b32(zr, voff, t * zs, 0) : 0u;
-    }
-    bc_load(t_beg, bcw[0]);
-  }
-
-  float sdel[2] = {0.0f, 0.0f};
-  for (int tg = t_beg; tg < t_end; tg += kPF) {
-#pragma unroll
-    for (int j = 0; j < kPF; ++j) {
-      const int t = tg + j;
-      const uint32_t wu = ru[j], wd = rd[j], wz = rz[j];
-      {
-        const int tn = min(t + kPF, tlast);
-        ru[j] = __builtin_amdgcn_raw_buffer_load_b32(ur, voff, tn * us, 0);
-        rd[j] = __builtin_amdgcn_raw_buffer_load_b32(dr_, voff, tn * ds, 0);
-        if (HZ && MODE != 1) rz[j] = __builtin_amdgcn_raw_buffer_load_b32(zr, voff, tn * zs, 0);
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
-      bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);   // keep the loads at the step head
-      const bool live = t < t_end;
-      const float uv[2] = {__uint_as_float(wu << 16), __uint_as_float(wu & 0xffff0000u)};
-      const float dv[2] = {__uint_as_float(wd << 16), __uint_as_float(wd & 0xffff0000u)};
-      float dl[2], du[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        float x = dv[c] + bias[c];
-        if (SP) x = softplus_fast(x);
-        dl[c] = live ? x : 0.0f;
-        du[c] = dl[c] * uv[c];
-      }
-      const uint32_t (&cw)[16] = bcw[j & 1];
-      if constexpr (MODE == 1) {
-#pragma unroll
-        for (int n = 0; n < kMaxN; ++n) {
-          const float Bn = __uint_as_float((n & 1) ? (cw[n >> 1] & 0xffff0000u) : (cw[n >> 1] << 16));
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-            h[c][n] = fmaf(__builtin_amdgcn_exp2f(dl[c] * A2[c][n]), h[c][n], du[c] * Bn);
-        }
-        sdel[0] += dl[0];
-        sdel[1] += dl[1];
-      } else {
-        float y[2] = {Dv[0] * uv[0], Dv[1] * uv[1]};
-#pragma unroll
-        for (int n = 0; n < kMaxN; ++n) {
-          const uint32_t wb = cw[n >> 1], wc = cw[8 + (n >> 1)];
-          const float Bn = __uint_as_float((n & 1) ? (wb & 0xffff0000u) : (wb << 16));
-          const float Cn = __uint_as_float((n & 1) ? (wc & 0xffff0000u) : (wc << 16));
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            h[c][n] = fmaf(__builtin_amdgcn_exp2f(dl[c] * A2[c][n]), h[c][n], du[c] * Bn);
-            y[c] = fmaf(h[c][n], Cn, y[c]);
-          }
-        }
-        if (HZ) {
-          y[0] *= silu_fast(__uint_as_float(wz << 16));
-          y[1] *= silu_fast(__uint_as_float(wz & 0xffff0000u));
-        }
-        const uint32_t packed = static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
-                                (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16);
-        __builtin_amdgcn_raw_buffer_store_b32(packed, orr, live ? voff_st : kSeqDead, t * os, 0);
-      }
-    }
-  }
-
-  if constexpr (MODE == 1) {
-    if (active) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-#pragma unroll
-        for (int n = 0; n < kMaxN; ++n) w.hend[(ws_row + c) * kMaxN + n] = h[c][n];
-        w.sdel[ws_row + c] = sdel[c];
-      }
-    }
-  } else {
-    if (t_end >= L && active) {
-      if (p.hl) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int n = 0; n < kMaxN; ++n)
-            store_dyn(p.hl, b * p.hl_sb + (d + c) * p.hl_sd + n, p.hl_dtype, h[c][n]);
-      }
-      for (int t = L; t < p.out_len; ++t)
-        __builtin_amdgcn_raw_buffer_store_b32(0u, orr, voff, t * os, 0);
-    }
-  }
-}
-
 // Entry state of every segment: h_in[0] = h0, h_in[s+1] = exp2(A*log2e*sum_delta[s]) *
 // h_in[s] + h_end[s].  One thread per (b, d, n), sequential over the S segments; the
 // summaries stream through a 16-deep register window so their loads overlap the chain.
@@ -643,8 +482,6 @@ __global__ __launch_bounds__(256) void scan_seq_carry_kernel(const ScanParams p,
 
 // B/C as scalar loads: 16 states, unit state stride, every row 4-byte aligned.
 static bool seq_sgpr_bc(const ScanParams& p, int es) {
-  const char* e = getenv("VM_SCAN_SGPR");
-  if (e && atoi(e) == 0) return false;
   auto ok = [&](const void* ptr, long long sb, long long sn, long long sl) {
     return sn == 1 && (reinterpret_cast<uintptr_t>(ptr) & 3) == 0 && (sb * es) % 4 == 0 &&
            (sl * es) % 4 == 0;
@@ -654,49 +491,19 @@ static bool seq_sgpr_bc(const ScanParams& p, int es) {
          span * p.b_sl < (1ll << 31) && span * p.c_sl < (1ll << 31);
 }
 
-// Packed state pairs (PK) on the SGPR-B/C path; VM_SCAN_PK=0 selects the scalar form.
-static bool seq_packed() {
-  const char* e = getenv("VM_SCAN_PK");
-  return !(e && atoi(e) == 0);
-}
-
-// Two channels per lane: opt-in (VM_SCAN_CPL=2).  Measured on MI355X at D=1152, L=3137,
-// B=224: 4.23 ms vs 2.95 ms for one channel per lane (half the waves, and the doubled
-// per-wave chains did not recover the lost occupancy), so the default stays at one.
-static bool seq_two_channels(const ScanParams& p, int es, int segs) {
-  (void)segs;
-  const char* e = getenv("VM_SCAN_CPL");
-  return e && atoi(e) == 2 && es == 2 && p.dim % 2 == 0 && seq_sgpr_bc(p, es) &&
-         (reinterpret_cast<uintptr_t>(p.u) & 3) == 0 && (reinterpret_cast<uintptr_t>(p.delta) & 3) == 0 &&
-         (reinterpret_cast<uintptr_t>(p.out) & 3) == 0 &&
-         (p.z == nullptr || (reinterpret_cast<uintptr_t>(p.z) & 3) == 0) &&
-         p.u_sb % 2 == 0 && p.dl_sb % 2 == 0 && p.o_sb % 2 == 0 && (p.z == nullptr || p.z_sb % 2 == 0) &&
-         p.u_sl % 2 == 0 && p.dl_sl % 2 == 0 && p.o_sl % 2 == 0 && (p.z == nullptr || p.z_sl % 2 == 0);
-}
-
 template <typename T, int MODE, bool SP, bool HZ>
 static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hipStream_t s) {
-  if constexpr (sizeof(T) == 2) {
-    if (seq_two_channels(p, 2, segs)) {
-      const int g2 = (p.dim + 127) / 128;
-      dim3 grid((g2 + 1) / 2, segs, p.batch);
-      hipLaunchKernelGGL((scan_seq2_kernel<MODE, SP, HZ>), grid, dim3(128), 0, s, p, w);
-      return;
-    }
-  }
   const int groups = (p.dim + 63) / 64;
   dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
   if (seq_sgpr_bc(p, sizeof(T))) {
+    // BC1: C directly follows B in one row (the mixer's x_dbl): one scalar load for both
     const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
                      static_cast<const T*>(p.C) == static_cast<const T*>(p.B) + kMaxN;
-    if (seq_packed() && bc1)
+    if (bc1)
       hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true, true>), grid,
                          dim3(64 * kSeqNW), 0, s, p, w);
-    else if (seq_packed())
-      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true>), grid,
-                         dim3(64 * kSeqNW), 0, s, p, w);
     else
-      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, false>), grid,
+      hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true>), grid,
                          dim3(64 * kSeqNW), 0, s, p, w);
   } else {
     hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, false, false>), grid,
@@ -755,20 +562,20 @@ static int choose_segments(int batch, int dim, int seqlen) {
   return best;
 }
 
-// VM_SCAN_SEGMENTS (read per call) forces the segment count — tests and sweeps.
-static int segments_for(int batch, int dim, int seqlen) {
-  const char* e = getenv("VM_SCAN_SEGMENTS");
-  if (e && atoi(e) > 0) {
-    int S = atoi(e) < kMaxSeg ? atoi(e) : kMaxSeg;
+// segments > 0 (an explicit ABI argument: tests and sweeps) forces the segment count;
+// 0 lets the cost model choose.
+static int segments_for(int batch, int dim, int seqlen, int segments) {
+  if (segments > 0) {
+    int S = segments < kMaxSeg ? segments : kMaxSeg;
     if (S > seqlen) S = seqlen > 0 ? seqlen : 1;
     return S;
   }
   return choose_segments(batch, dim, seqlen);
 }
 
-size_t seq_workspace_bytes(int batch, int dim, int seqlen, int* segments) {
-  const int S = segments_for(batch, dim, seqlen);
-  if (segments) *segments = S;
+size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen) {
+  const int S = segments_for(batch, dim, seqlen, segments);
+  if (chosen) *chosen = S;
   if (S <= 1) return 0;
   return static_cast<size_t>(batch) * S * dim * (2 * kMaxN + 1) * sizeof(float);
 }
@@ -783,10 +590,10 @@ bool seq_supported(const ScanParams& p, int dtype) {
          (p.z == nullptr || fits(p.z_sl));
 }
 
-void seq_launch(const ScanParams& p, int dtype, void* workspace, size_t workspace_bytes,
-                hipStream_t s) {
+void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
+                size_t workspace_bytes, hipStream_t s) {
   int S = 1;
-  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, &S);
+  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
   SeqWork w{};
   if (S > 1 && workspace && workspace_bytes >= need) {
     const size_t states = static_cast<size_t>(p.batch) * S * p.dim * kMaxN;

@@ -6,41 +6,61 @@ the results for this package's shapes on gfx950 ship in ``tuning/tunableop_gfx95
 and are loaded read-only, so a fresh process uses the tuned kernels with no tuning cost.
 Shapes missing from the file fall back to the library heuristic.
 
-    VM_GEMM_TUNING=0    leave TunableOp alone
-    VM_GEMM_TUNING=tune record new shapes into the results file (slow; run on the target)
+Scope: TunableOp is a process-wide switch in PyTorch, so this module turns it on only
+around the mixer's own GEMM calls (:func:`tuned`) and restores the caller's setting
+afterwards — other GEMMs in the user's process are untouched.  It stays off when
+``torch.are_deterministic_algorithms_enabled()`` (the determinism contract) or when
+``options.gemm_tuning == "off"``; ``"tune"`` records new shapes into the results file.
 """
 
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
 
+from . import options
+
 RESULTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning",
                        "tunableop_gfx950.csv")
-_done = False
+_loaded = {"mode": None}
 
 
-def enable_tuned_gemms() -> bool:
-    """Idempotent.  Returns True when TunableOp is active for this process."""
-    global _done
-    if _done:
-        return torch.cuda.tunable.is_enabled()
-    _done = True
-    mode = os.getenv("VM_GEMM_TUNING", "1").lower()
-    if mode in ("0", "off", "false", "no") or not torch.cuda.is_available():
+def _prepare(mode: str) -> bool:
+    """Load the results file once per mode; False when TunableOp cannot be used."""
+    if _loaded["mode"] == mode:
+        return True
+    if not torch.cuda.is_available():
         return False
+    tun = torch.cuda.tunable
     tune = mode == "tune"
     if not tune and not os.path.exists(RESULTS):
         return False
-    tun = torch.cuda.tunable
-    os.makedirs(os.path.dirname(RESULTS), exist_ok=True)
     tun.set_filename(RESULTS, insert_device_ordinal=False)
-    tun.enable(True)
-    tun.tuning_enable(tune)
     if tune:
-        tun.set_max_tuning_duration(int(os.getenv("VM_GEMM_TUNING_MS", "60")))
-        tun.set_max_tuning_iterations(int(os.getenv("VM_GEMM_TUNING_ITERS", "20")))
+        os.makedirs(os.path.dirname(RESULTS), exist_ok=True)
+        tun.set_max_tuning_duration(60)
+        tun.set_max_tuning_iterations(20)
     else:
         tun.read_file(RESULTS)
+    _loaded["mode"] = mode
     return True
+
+
+@contextlib.contextmanager
+def tuned():
+    """Run the enclosed GEMMs with the shipped TunableOp results (see module doc)."""
+    mode = options.get().gemm_tuning
+    if mode == "off" or torch.are_deterministic_algorithms_enabled() or not _prepare(mode):
+        yield False
+        return
+    tun = torch.cuda.tunable
+    was_on, was_tuning = tun.is_enabled(), tun.tuning_is_enabled()
+    tun.enable(True)
+    tun.tuning_enable(mode == "tune")
+    try:
+        yield True
+    finally:
+        tun.tuning_enable(was_tuning)
+        tun.enable(was_on)

@@ -20,6 +20,13 @@ chunk kind (first chunk with CLS, continuation chunk without) into a ``torch.cud
 Semantics are the eager path's (same kernels, same rounding points); tests check replay
 against eager chunk by chunk.  Masks and keep_temporal pooling are not graph-captured
 (use the eager forward for those).
+
+Lifetimes.  A graph replays raw device pointers, so everything it touches is pinned for
+its lifetime: the runner owns the scan's scratch workspace (no shared cache can grow and
+free it under the graph), and it records every parameter's (data_ptr, version) at
+capture.  When the model's parameters change (``load_state_dict``, an in-place edit, a
+``.to()``), the next ``run`` drops the stale graphs and captures again, so a replay never
+reads weight caches that the eager path has since replaced.
 """
 
 from __future__ import annotations
@@ -28,6 +35,8 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 from torch import Tensor
+
+from . import kernels as K
 
 __all__ = ["StreamingChunkGraph"]
 
@@ -51,6 +60,8 @@ class StreamingChunkGraph:
             (c, s) for c, s in model.allocate_state(batch, dtype=self.dtype, device=self.device)]
         self._graphs: Dict[bool, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self._pool = None
+        self._param_key = None
+        self._ws = None  # scan scratch owned by the captured graphs
 
     # ------------------------------------------------------------------ state
     @property
@@ -82,16 +93,33 @@ class StreamingChunkGraph:
         gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
         return m._pool(self.static_x, x_vis, None, False, has_cls, self.tt, gh * gw)
 
+    def _params_key(self):
+        return tuple((t.data_ptr(), t._version, t.dtype, t.device)
+                     for t in list(self.model.parameters()) + list(self.model.buffers()))
+
+    def _workspace(self) -> Tensor:
+        """Scan scratch sized for the largest token-major scan of a chunk (every layer has
+        the same shape); allocated once per capture set and owned by this runner."""
+        m = self.model
+        gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
+        L = self.tt * gh * gw + 1
+        need = max(K.scan_workspace_bytes(self.batch, mx.d_inner, L, mx.d_state)
+                   for mx in m._mixers())
+        if self._ws is None or self._ws.numel() < max(need, 1):
+            self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+        return self._ws
+
     def _capture(self, has_cls: bool):
         saved = [(c.clone(), s.clone()) for c, s in self._state]
+        ws = self._workspace()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.no_grad(), torch.cuda.stream(side):
+        with torch.no_grad(), torch.cuda.stream(side), K.scan_workspace_override(ws):
             for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
                 self._body(has_cls)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool):
+        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scan_workspace_override(ws):
             outs = self._body(has_cls)
         self._pool = g.pool()
         self.load_state(saved)  # warm-up passes advanced the state: restore it
@@ -113,6 +141,11 @@ class StreamingChunkGraph:
                                              dtype=self.dtype, device=self.device)
         self.static_tpos.copy_(tpos)
         self.static_x.copy_(x)
+        key = self._params_key()
+        if key != self._param_key:  # parameters changed since capture: capture again
+            self._graphs.clear()
+            self._pool = None
+            self._param_key = key
         if has_cls not in self._graphs:
             self._capture(has_cls)
         g, outs = self._graphs[has_cls]

@@ -24,7 +24,7 @@ from typing import Optional, Tuple
 import torch
 from torch import Tensor
 
-from . import _lib
+from . import _lib, options
 
 _DT = {torch.float32: _lib.VM_DTYPE_F32, torch.bfloat16: _lib.VM_DTYPE_BF16}
 
@@ -96,13 +96,36 @@ def _channel_contig(t: Optional[Tensor]) -> Optional[Tensor]:
 
 # --------------------------------------------------------------------------- raw launchers
 _WORKSPACE = {}
+_WS_OVERRIDE = [None]
 
 
-def scan_workspace(device: torch.device, nbytes: int) -> Optional[Tensor]:
-    """Per-device scratch for the time-segmented token-major scan (grown, never shrunk)."""
+class scan_workspace_override:
+    """Within the block every token-major scan uses ``buf`` (a uint8 device tensor owned
+    by the caller) instead of the per-stream cache — how a captured HIP graph keeps its
+    scratch alive and fixed for its lifetime (graphs.StreamingChunkGraph)."""
+
+    def __init__(self, buf: Tensor):
+        self.buf = buf
+
+    def __enter__(self):
+        self.prev = _WS_OVERRIDE[0]
+        _WS_OVERRIDE[0] = self.buf
+        return self.buf
+
+    def __exit__(self, *exc):
+        _WS_OVERRIDE[0] = self.prev
+        return False
+
+
+def scan_workspace(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
+    """Scratch for the time-segmented token-major scan, one buffer per (device, stream),
+    grown and never shrunk.  When it grows, the old buffer is released back to the
+    caching allocator on that same stream, so work already queued there finishes first.
+    Captured HIP graphs own their workspace (graphs.StreamingChunkGraph) and never
+    reach this cache."""
     if nbytes <= 0:
         return None
-    key = (device.type, device.index)
+    key = (device.type, device.index, stream)
     buf = _WORKSPACE.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -110,17 +133,32 @@ def scan_workspace(device: torch.device, nbytes: int) -> Optional[Tensor]:
     return buf
 
 
+def scan_workspace_bytes(batch: int, dim: int, seqlen: int, dstate: int,
+                         segments: Optional[int] = None) -> int:
+    seg = options.get().scan_segments if segments is None else segments
+    return int(_lib.load().vm_selective_scan_workspace_bytes(batch, dim, seqlen, dstate, seg))
+
+
 def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, softplus,
              h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen, dstate, dtype,
-             stream):
+             stream, workspace: Optional[Tensor] = None):
     """Strides are (batch, channel|state, step) element strides; either every
-    u/delta/z/out channel stride is 1 (token-major) or every step stride is 1."""
+    u/delta/z/out channel stride is 1 (token-major) or every step stride is 1.
+    ``workspace`` (a uint8 device buffer) replaces the per-stream scratch cache."""
     lib = _lib.load()
+    seg = int(options.get().scan_segments)
     ws_bytes = 0
     ws = None
+    if workspace is None:
+        workspace = _WS_OVERRIDE[0]
     if u_s[1] == 1:
-        ws_bytes = int(lib.vm_selective_scan_workspace_bytes(batch, dim, seqlen, dstate))
-        ws = scan_workspace(u.device, ws_bytes)
+        ws_bytes = scan_workspace_bytes(batch, dim, seqlen, dstate, seg)
+        if workspace is not None:
+            if workspace.numel() < ws_bytes:
+                raise ValueError(f"scan workspace too small: {workspace.numel()} < {ws_bytes}")
+            ws = workspace
+        else:
+            ws = scan_workspace(u.device, int(stream), ws_bytes)
     rc = lib.vm_selective_scan_fwd(
         _p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
         _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
@@ -128,7 +166,7 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
         _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
         _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
         _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate, dtype,
-        _p(ws), ws_bytes, stream)
+        seg, _p(ws), ws_bytes, stream)
     _lib.check(rc, "vm_selective_scan_fwd")
 
 
@@ -151,28 +189,19 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
     """Fused token-major conv1d + SiLU -> x_proj -> dt_proj (bf16).  *_s = (batch, step)
     element strides of the token-major buffers; wx_pad (e_pad, D) / wdt_pad (D, r_pad) are
     zero-padded copies of the projection weights.  dt_softplus: `dt` receives the scan's
-    activated step softplus(dt + dt_bias32) instead (the scan then runs without them)."""
+    activated step softplus(dt + dt_bias32) instead (the scan then runs without them).
+    dt=None skips dt_proj (conv + x_proj only; wdt_pad may be None)."""
     lib = _lib.load()
     rc = lib.vm_conv_proj_fwd(
         _p(xz), xz_s[0], xz_s[1], _p(cw32), _p(cb32),
         _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
         _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
-        _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad), r, wdt_pad.shape[1],
-        _p(u), u_s[0], u_s[1], _p(xdbl), xd_s[0], xd_s[1], _p(dt), dt_s[0], dt_s[1],
+        _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad), r,
+        wdt_pad.shape[1] if wdt_pad is not None else 0,
+        _p(u), u_s[0], u_s[1], _p(xdbl), xd_s[0], xd_s[1], _p(dt),
+        dt_s[0] if dt is not None else 0, dt_s[1] if dt is not None else 0,
         _p(dt_bias32), int(dt_softplus), out_len, batch, dim, seqlen, width, dtype_code(u.dtype), stream)
     _lib.check(rc, "vm_conv_proj_fwd")
-
-
-def out_norm_raw(y, y_sl, w_out, residual, nw32, nb32, out, residual_out, rows, eps, is_rms,
-                 stream):
-    """out_proj GEMM + residual add + RMSNorm/LayerNorm in one launch (bf16 y / w_out,
-    fp32 residual); see vm_out_proj_add_norm_fwd."""
-    lib = _lib.load()
-    n, k = w_out.shape
-    rc = lib.vm_out_proj_add_norm_fwd(_p(y), y_sl, _p(w_out), _p(residual), _p(nw32), _p(nb32),
-                                      _p(out), _p(residual_out), rows, n, k, float(eps),
-                                      int(is_rms), stream)
-    _lib.check(rc, "vm_out_proj_add_norm_fwd")
 
 
 def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_rms, stream):

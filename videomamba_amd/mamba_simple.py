@@ -44,43 +44,19 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from . import kernels as K
-from .gemm_tuning import enable_tuned_gemms
+from . import options
+from .gemm_tuning import tuned
 from .layers import round_up, warn_if_grad
 
-# Cross-stream GEMM ordering.  When PretrainVideoMamba issues batch slices on concurrent
-# streams (videomamba._layers_multistream) two library GEMMs must never run at the same
-# time: hipBLASLt's stream-K kernels spin on partial-tile flags of their own workgroups
-# (and share the handle's workspace), so two of them co-resident can wait on each other
-# forever (measured: a hang at B=336 with two streams).  While ``serial_gemms`` is on,
-# every token-major GEMM waits for the previously issued GEMM of any other stream; the
-# scan / conv / norm kernels of one slice still overlap the GEMMs of the other.
-_GEMM_ORDER = {"on": 0, "last": None}
-
-
-class serial_gemms:
-    def __enter__(self):
-        _GEMM_ORDER["on"] += 1
-        return self
-
-    def __exit__(self, *exc):
-        _GEMM_ORDER["on"] -= 1
-        if _GEMM_ORDER["on"] == 0:
-            _GEMM_ORDER["last"] = None
-        return False
-
-
 def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
-    if not _GEMM_ORDER["on"]:
+    """A projection GEMM of the mixer (library GEMM with the shipped tuning results)."""
+    with tuned():
         return F.linear(x, w, b)
-    cur = torch.cuda.current_stream(x.device)
-    last = _GEMM_ORDER["last"]
-    if last is not None and last[0] != cur.cuda_stream:
-        cur.wait_event(last[1])
-    out = F.linear(x, w, b)
-    ev = torch.cuda.Event()
-    ev.record(cur)
-    _GEMM_ORDER["last"] = (cur.cuda_stream, ev)
-    return out
+
+
+def _matmul(a: Tensor, b: Tensor) -> Tensor:
+    with tuned():
+        return torch.matmul(a, b)
 
 
 _CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP "
@@ -92,9 +68,9 @@ def mixer_layout(batch: int, d_inner: int, device: torch.device) -> str:
     least ~1.25 waves per SIMD, else "cm" (channel-major, time-parallel scan).  Measured
     at D=1152, L=3137 (profiles/): the time-parallel kernel costs ~24 us per clip-layer at
     any batch, the channel-per-lane one ~1.6 ms flat up to 2 waves/SIMD (15 us per
-    clip-layer at B=112).  VM_MIXER_LAYOUT=tm|cm overrides."""
-    forced = os.getenv("VM_MIXER_LAYOUT", "").lower()
-    if forced in ("tm", "cm"):
+    clip-layer at B=112).  ``options.mixer_layout`` ("tm" | "cm") overrides."""
+    forced = options.get().mixer_layout
+    if forced != "auto":
         return forced
     simds = 4 * torch.cuda.get_device_properties(device).multi_processor_count
     waves = batch * ((d_inner + 63) // 64)
@@ -200,7 +176,7 @@ class Mamba(nn.Module):
         return (hn.dtype == torch.bfloat16 and seqlen >= 1 and self.d_inner % 64 == 0
                 and self.d_conv <= 4 and E <= 128 and self.dt_rank <= 64
                 and self.x_proj.bias is None and self.dt_proj.weight.dtype == torch.bfloat16
-                and os.getenv("VM_FUSED_CONV_PROJ", "1") != "0")
+                and options.get().fused_conv_proj)
 
     # ------------------------------------------------------------------ core
     def _forward_padded(self, hn: Tensor, seqlen: int, *, conv_state_in: Optional[Tensor] = None,
@@ -208,7 +184,6 @@ class Mamba(nn.Module):
                         h_last: Optional[Tensor] = None) -> Tensor:
         """hn: (B, Lp, C) contiguous, rows >= seqlen zero.  Returns (B, Lp, C) with rows
         >= seqlen zero.  States are read/written by the kernels (see module doc)."""
-        enable_tuned_gemms()
         if mixer_layout(hn.shape[0], self.d_inner, hn.device) == "tm":
             return self._forward_padded_tm(hn, seqlen, conv_state_in, conv_state_out, h0, h_last)
         Bsz, Lp, C = hn.shape
@@ -220,7 +195,7 @@ class Mamba(nn.Module):
         rows = (Lp, n)  # (batch stride, channel stride) of a (ch, B*Lp) buffer
         rows3 = (Lp, n, 1)  # + step stride
 
-        xz = torch.matmul(self.in_proj.weight, hn.view(n, C).t())  # (2D, B*Lp)
+        xz = _matmul(self.in_proj.weight, hn.view(n, C).t())  # (2D, B*Lp)
         if self.in_proj.bias is not None:
             xz += self.in_proj.bias.to(xz.dtype)[:, None]
         x, z = xz[:Dm], xz[Dm:]
@@ -231,15 +206,15 @@ class Mamba(nn.Module):
                    conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
                    if conv_state_out is not None else (0, 0),
                    u, rows3, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
-        x_dbl = torch.matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
-        dt = torch.matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
+        x_dbl = _matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
+        dt = _matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
         y = torch.empty_like(u)
         K.scan_raw(u, rows3, dt, rows3, A, x_dbl[R:R + N], rows3, x_dbl[R + N:], rows3, Dv,
                    z, rows3, dbias, True,
                    h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
                    h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
                    y, rows3, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
-        out = torch.matmul(y.t(), self.out_proj.weight.t())  # (B*Lp, C)
+        out = _matmul(y.t(), self.out_proj.weight.t())  # (B*Lp, C)
         if self.out_proj.bias is not None:
             out += self.out_proj.bias.to(out.dtype)
         return out.view(Bsz, Lp, C)
@@ -261,22 +236,17 @@ class Mamba(nn.Module):
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
                  if conv_state_out is not None else (0, 0))
-        scan_bias, scan_softplus = dbias, True
         if self._fused_conv_proj_ok(hn, seqlen):
-            # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip).
-            # VM_DELTA_IN_CONV_PROJ=1 moves the scan's delta activation softplus(dt + bias)
-            # into its dt epilogue: measured a wash at B = 336 (scan -222 us, conv_proj
-            # +385 us per layer, profiles/r01f_delta_placement.txt), so it stays in the scan
+            # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip).  The scan
+            # keeps the delta activation softplus(dt + bias): moved into conv_proj's dt
+            # epilogue it measured a wash at B = 336 (scan -222 us, conv_proj +385 us per
+            # layer, profiles/r01f_delta_placement.txt)
             wx_pad, wdt_pad = self._padded_proj_weights()
             x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
             dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
-            pre = os.getenv("VM_DELTA_IN_CONV_PROJ", "0") == "1"
             K.conv_proj_raw(xz, s_xz[::2], cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                             wx_pad, E, wdt_pad, R, u, s_u[::2], x_dbl, (Lp * E, E), dt,
-                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream,
-                            dt_bias32=dbias if pre else None, dt_softplus=pre)
-            if pre:
-                scan_bias, scan_softplus = None, False
+                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream)
         else:
             K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                        u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
@@ -284,7 +254,7 @@ class Mamba(nn.Module):
             dt = _linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
         y = torch.empty_like(u)
         K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
-                   xz[:, Dm:], s_xz, scan_bias, scan_softplus,
+                   xz[:, Dm:], s_xz, dbias, True,
                    h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
                    h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
                    y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)

@@ -1,0 +1,82 @@
+"""Host-side selection knobs of the HIP path — the only configuration channel there is.
+
+The C library reads no environment: every choice it makes beyond the operands' shapes
+and layouts arrives as an explicit ABI argument (today: the token-major scan's segment
+count).  Above it, the Python host picks the mixer layout and a few paths from this one
+documented options object; tests and sweeps change them with :func:`override`.
+
+    mixer_layout     "auto" (default) | "tm" | "cm".  "auto": token-major (channel-per-lane
+                     scan) when batch x 64-channel groups fills ~1.25 waves per SIMD, else
+                     channel-major (time-parallel scan); see mamba_simple.mixer_layout.
+    scan_segments    0 (default) = the library's cost model; > 0 forces the token-major
+                     scan's time-segment count (vm_selective_scan_fwd ``segments``).
+    fused_conv_proj  True (default): bf16 token-major mixers run conv1d + x_proj + dt_proj
+                     as one kernel (vm_conv_proj_fwd); False: conv kernel + library GEMMs.
+    gemm_tuning      "on" (default): the mixer's projection GEMMs use the shipped TunableOp
+                     results (gemm_tuning.py), enabled only around those calls; "off": the
+                     library heuristic; "tune": record new shapes (slow, offline).
+                     Initialised from ``VM_GEMM_TUNING`` when that is set (the tuning
+                     script's switch); nothing else is read from the environment.
+
+Options are process-global (not thread-local): the model is driven from one host thread.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import dataclasses
+import os
+from typing import Iterator
+
+__all__ = ["Options", "get", "override"]
+
+_LAYOUTS = ("auto", "tm", "cm")
+_TUNING = ("on", "off", "tune")
+
+
+@dataclasses.dataclass
+class Options:
+    mixer_layout: str = "auto"
+    scan_segments: int = 0
+    fused_conv_proj: bool = True
+    gemm_tuning: str = "on"
+
+    def validate(self) -> None:
+        if self.mixer_layout not in _LAYOUTS:
+            raise ValueError(f"mixer_layout must be one of {_LAYOUTS}, got {self.mixer_layout!r}")
+        if int(self.scan_segments) < 0:
+            raise ValueError("scan_segments must be >= 0")
+        if self.gemm_tuning not in _TUNING:
+            raise ValueError(f"gemm_tuning must be one of {_TUNING}, got {self.gemm_tuning!r}")
+
+
+def _initial() -> Options:
+    o = Options()
+    env = os.environ.get("VM_GEMM_TUNING", "").strip().lower()
+    if env in ("0", "off", "false", "no"):
+        o.gemm_tuning = "off"
+    elif env == "tune":
+        o.gemm_tuning = "tune"
+    return o
+
+
+_OPTS = _initial()
+
+
+def get() -> Options:
+    """The live options object (read by the mixer on every call)."""
+    return _OPTS
+
+
+@contextlib.contextmanager
+def override(**changes) -> Iterator[Options]:
+    """Temporarily change options: ``with override(mixer_layout="tm"): ...``."""
+    global _OPTS
+    old = _OPTS
+    new = dataclasses.replace(old, **changes)
+    new.validate()
+    _OPTS = new
+    try:
+        yield new
+    finally:
+        _OPTS = old

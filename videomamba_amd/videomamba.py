@@ -18,7 +18,6 @@ tokens (``Block.forward`` itself is kept for callers that use blocks directly).
 from __future__ import annotations
 
 import logging
-import os
 import math
 from functools import partial
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union, cast
@@ -30,7 +29,7 @@ from torch import Tensor
 
 from . import kernels as K
 from .layers import DropPath, RMSNorm, round_up, to_2tuple, trunc_normal_, warn_if_grad
-from .mamba_simple import InferenceParamsLike, Mamba, mixer_layout, serial_gemms
+from .mamba_simple import InferenceParamsLike, Mamba
 from .streaming import (STREAMING_CONTRACT_VERSION, ForwardReturnSemantics, StateShape,
                         forward_return_semantics as _return_semantics)
 
@@ -470,96 +469,6 @@ class PretrainVideoMamba(nn.Module):
         return K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms, out=out,
                        owner=self.norm)
 
-    def _stream_slices(self, batch: int, ssm_state):
-        """Batch slices for concurrent streams, or None.  Opt-in (``VM_BATCH_STREAMS=n``):
-        large token-major batches are cut into n slices whose layer loops are issued on
-        their own HIP streams, interleaved layer by layer, so that the VALU-bound scan of
-        one slice could overlap the HBM/MFMA-bound kernels of another.  Measured on MI355X
-        at M-16f B=336 (profiles/r01c_streams_probe.txt): 1 stream 385 ms/step, 2 streams
-        457, 3 streams 496 — the library GEMMs are stream-K kernels that assume the whole
-        chip (two of them co-resident deadlock, hence mamba_simple.serial_gemms; beside a
-        scan they stall), so the default stays at one stream.  Every slice must still fill
-        the chip on its own (token-major layout); full (conv, ssm) state containers and the
-        stateless path are supported (legacy ssm-only state runs on one stream)."""
-        n = int(os.getenv("VM_BATCH_STREAMS", "1"))
-        if n <= 1 or batch < n:
-            return None
-        if ssm_state is not None:
-            first = self._get_layer_state(ssm_state, 0)
-            if not (isinstance(first, (list, tuple)) and len(first) == 2):
-                return None
-        dev = self.patch_embed.proj.weight.device
-        per = batch // n
-        if mixer_layout(per, self.layers[0].mixer.d_inner, dev) != "tm":
-            return None
-        cuts = [batch * i // n for i in range(n + 1)]
-        return [(cuts[i], cuts[i + 1]) for i in range(n)]
-
-    def _side_streams(self, n: int, device):
-        key = (device.index, n)
-        cache = self.__dict__.setdefault("_vm_streams", {})
-        if key not in cache:
-            cache[key] = [torch.cuda.Stream(device) for _ in range(n)]
-        return cache[key]
-
-    def _layers_multistream(self, h, L, ssm_state, slices):
-        """_run_layers + final norm per batch slice, each slice on its own stream."""
-        dev = h.device
-        main = torch.cuda.current_stream(dev)
-        streams = self._side_streams(len(slices), dev)
-        out = torch.empty_like(h)
-
-        def slice_state(b0, b1):
-            if ssm_state is None:
-                return None
-            if isinstance(ssm_state, dict):
-                return {k: (v[0][b0:b1], v[1][b0:b1]) for k, v in ssm_state.items()}
-            return [(c[b0:b1], s[b0:b1]) for c, s in ssm_state]
-
-        hs = [h[b0:b1] for b0, b1 in slices]
-        res = [None] * len(slices)
-        sts = [slice_state(b0, b1) for b0, b1 in slices]
-        news = [None] * len(slices)
-        tuple_out = False
-        for st in streams:
-            st.wait_stream(main)
-        # layer-interleaved issue order so the streams progress together; library GEMMs of
-        # different slices are ordered (mamba_simple.serial_gemms), everything else overlaps
-        with serial_gemms():
-            for idx, layer in enumerate(self.layers):
-                for s, stream in enumerate(streams):
-                    with torch.cuda.stream(stream):
-                        st = sts[s]
-                        if st is None:
-                            hs[s], res[s], _ = layer.forward_padded(hs[s], res[s], L)
-                            continue
-                        ls = st[idx] if not isinstance(st, dict) else st.get(idx)
-                        hs[s], res[s], ns = layer.forward_padded(hs[s], res[s], L,
-                                                                 state=tuple(ls),
-                                                                 return_state=True)
-                        if news[s] is None:
-                            news[s] = {} if isinstance(st, dict) else [None] * len(self.layers)
-                        news[s][idx] = ns
-        for s, (b0, b1) in enumerate(slices):
-            with torch.cuda.stream(streams[s]):
-                self._final_norm(hs[s], res[s], out=out[b0:b1])
-        for st in streams:
-            main.wait_stream(st)
-        new_states = None
-        if ssm_state is not None:
-            tuple_out = isinstance(ssm_state, tuple)
-            keys = list(ssm_state.keys()) if isinstance(ssm_state, dict) else range(len(self.layers))
-            merged = {} if isinstance(ssm_state, dict) else [None] * len(self.layers)
-            for k in keys:
-                c_full, s_full = ssm_state[k]
-                conv = torch.cat([news[s][k][0] for s in range(len(slices))], 0)
-                parts = [news[s][k][1] for s in range(len(slices))]
-                in_place = all(parts[s].data_ptr() == s_full[b0:b1].data_ptr()
-                               for s, (b0, b1) in enumerate(slices))
-                merged[k] = (conv, s_full if in_place else torch.cat(parts, 0))
-            new_states = merged
-        return out, new_states, tuple_out
-
     # ------------------------------------------------------------------ forward
     def _embed(self, x: Tensor, has_cls: bool, temporal_pos_offset: int, tpos=None):
         """Patch embed + positional adds (+ CLS row) into a zero-padded (B, Lp, C) buffer.
@@ -608,12 +517,8 @@ class PretrainVideoMamba(nn.Module):
             h = torch.zeros((Bsz, round_up(L), self.embed_dim), dtype=h.dtype, device=h.device)
             h[:, :L] = gathered
 
-        slices = self._stream_slices(Bsz, ssm_state)
-        if slices is not None:
-            out, new_states, tuple_out = self._layers_multistream(h, L, ssm_state, slices)
-        else:
-            h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state)
-            out = self._final_norm(h, residual)
+        h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state)
+        out = self._final_norm(h, residual)
         x_vis = out[:, :L].contiguous()
 
         if new_states is not None and isinstance(new_states, list):
