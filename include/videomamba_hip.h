@@ -15,6 +15,8 @@
  *   vm_causal_conv1d_update    <- causal_conv1d_update  (mamba_simple.py:468-474)
  *   vm_conv_proj_fwd           <- causal_conv1d_fn + x_proj + dt_proj, fused, token-major
  *                                 (mamba_simple.py:381-416)
+ *   vm_conv_proj_cm_fwd        <- the same three steps on the channel-major small-batch
+ *                                 layout (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
@@ -136,6 +138,9 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
  * with step >= seqlen are written as 0.  conv state as vm_causal_conv1d_fwd (width <= 4).
  * dim % 64 == 0, seqlen >= 1.
  * dt == NULL skips dt_proj (conv + x_proj only; wdt_pad may then be NULL too).
+ * batch <= 8 runs a split-K form (fixed 128-channel splits of the x_proj reduction, so
+ * every token's bits are independent of the sequence length) that needs `workspace` of
+ * vm_conv_proj_workspace_bytes() bytes; larger batches need none (NULL, 0).
  * dt_softplus != 0: `dt` receives the scan's activated step instead,
  *   delta = softplus(float(bf16(dt)) + dt_bias[d])  (dt_bias nullable = 0), rounded to bf16
  *   — selective_scan_fn's delta_bias / delta_softplus prologue (mamba_simple.py:30-106),
@@ -151,7 +156,36 @@ int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                      void* dt, long long dt_sb, long long dt_sl,
                      const float* dt_bias, int dt_softplus,
                      int out_len, int batch, int dim, int seqlen, int width, int dtype,
-                     vm_stream_t stream);
+                     void* workspace, long long workspace_bytes, vm_stream_t stream);
+
+/* Scratch bytes vm_conv_proj_fwd needs for this shape (0 above the split-K batch). */
+long long vm_conv_proj_workspace_bytes(int batch, int out_len, int dim, int e);
+
+/*
+ * Channel-major mixer middle (bf16, small batches; the (D, B*L) layout of
+ * mamba_simple.py:333-416):  u = silu(conv1d([conv_state_in | x])) -> x_dbl = W_x @ u ->
+ * dt = W_dt @ x_dbl[:r], each rounded to bf16 (the reference's rounding points).
+ * x: the first `dim` rows of xz, row stride x_sd, columns = batch * out_len tokens (batch b's
+ * steps at columns b*out_len + t, unit stride).  u, dt: (dim, batch*out_len) row strides
+ * u_sd / dt_sd; x_dbl: (e, batch*out_len) row stride xd_sd.  Columns with t >= seqlen are
+ * written as 0.  wx_pad / wdt_pad / conv weights and state as vm_conv_proj_fwd.
+ * The x_proj reduction over channels runs in a fixed split order (fp32 partials in
+ * `workspace`, vm_conv_proj_cm_workspace_bytes() bytes), so every token's outputs are
+ * independent of the sequence length and batch (chunked == full-sequence, bitwise).
+ * dim % 64 == 0, out_len % 8 == 0, seqlen >= 1, width <= 4.
+ */
+int vm_conv_proj_cm_fwd(const void* xz, long long x_sd, const float* conv_weight,
+                        const float* conv_bias,
+                        const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
+                        void* cs_out, int cs_out_dtype, long long cso_sb, long long cso_sd,
+                        const void* wx_pad, int e, int e_pad, const void* wdt_pad, int r,
+                        int r_pad, void* u, long long u_sd, void* xdbl, long long xd_sd,
+                        void* dt, long long dt_sd, int out_len, int batch, int dim,
+                        int seqlen, int width, void* workspace, long long workspace_bytes,
+                        vm_stream_t stream);
+
+/* Scratch bytes vm_conv_proj_cm_fwd needs for this shape (its x_proj partials). */
+long long vm_conv_proj_cm_workspace_bytes(int batch, int out_len, int dim, int e);
 
 /*
  * One-token conv step: shift conv_state left by one, append x, dot with weight (+bias),

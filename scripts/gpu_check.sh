@@ -14,6 +14,6 @@ run() {  # run <name> <timeout-s> <cmd...>
 }
 STEPS=${STEPS:-smoke,tests,bench}
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *tests* ]] && run gpu_tests 1200 python -m pytest tests -m gpu -q --timeout 400 ${PYTEST_ARGS:-}
-[[ $STEPS == *bench* ]] && run bench 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3}
+[[ $STEPS == *tests* ]] && run gpu_tests ${TEST_TMO:-900} python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+[[ $STEPS == *bench* ]] && run bench 600 python -u bench.py ${BENCH_ARGS:---steps 10 --warmup 3}
 exit 0

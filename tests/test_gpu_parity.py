@@ -468,7 +468,7 @@ def test_conv_proj_delta_softplus_epilogue():
     torch.manual_seed(5)
     m = Mamba(d_model=96, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
     Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
-    Bsz, L = 3, 301
+    Bsz, L = 9, 301  # batch > 8: the softplus epilogue lives in the wide (non-split-K) kernel
     Lp = (L + 7) // 8 * 8
     n = Bsz * Lp
     xz = torch.randn(n, 2 * Dm, device=DEV).to(torch.bfloat16)
@@ -494,3 +494,50 @@ def test_conv_proj_delta_softplus_epilogue():
     assert (got > 0).all()
     err = ((got - want).abs() / want).max().item()
     assert err <= 2.0 ** -8, err
+
+
+@pytest.mark.parametrize("d_model", [576, 96])
+def test_conv_proj_split_k_matches_wide_kernel(d_model):
+    """vm_conv_proj_fwd runs the split-K form (fixed 128-channel splits of the x_proj
+    reduction, vm_conv_proj_sk.hip) for batch <= 8 and the one-workgroup-per-64-rows kernel
+    above.  The same clip through both: u bit-identical (same conv arithmetic), x_dbl and dt
+    within one bf16 rounding of each other (the fp32 reduction orders differ), both vs the
+    oracle's conv and the fp32 projections of the kernel's own u.  d_model 96 -> D = 192
+    covers a half-width last split (64 channels)."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(d_model)
+    m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    _, _, _, cw, cb = m._fp32_params()
+    wx_pad, wdt_pad = m._padded_proj_weights()
+    st = torch.cuda.current_stream().cuda_stream
+    L = 777
+    Lp = (L + 7) // 8 * 8
+    outs = []
+    xz9 = torch.randn(9, Lp, 2 * Dm, device=DEV).to(torch.bfloat16)
+    xz9[:, L:] = 0
+    cs9 = torch.randn(9, Dm, W, device=DEV).to(torch.bfloat16)
+    for bsz in (9, 1):
+        n = bsz * Lp
+        xz = xz9[:bsz].reshape(n, 2 * Dm).contiguous()
+        cs = cs9[:bsz].contiguous()
+        u = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+        xd = torch.empty(n, E, device=DEV, dtype=torch.bfloat16)
+        dt = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+        K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, (Dm * W, W), None, (0, 0),
+                        wx_pad, E, wdt_pad, R, u, (Lp * Dm, Dm), xd, (Lp * E, E), dt,
+                        (Lp * Dm, Dm), Lp, bsz, Dm, L, W, st)
+        outs.append((u[:Lp], xd[:Lp], dt[:Lp]))
+    torch.cuda.synchronize()
+    (u9, xd9, dt9), (u1, xd1, dt1) = outs
+    assert torch.equal(u9, u1)
+    assert not u1[L:].float().abs().any() and not dt1[L:].float().abs().any()
+    ulp = lambda t: t.float().abs() * 2.0 ** -7 + 1e-6  # noqa: E731
+    assert ((xd9.float() - xd1.float()).abs() <= ulp(xd1)).all()
+    want_xd = F.linear(u1.float(), m.x_proj.weight.float())
+    assert ((xd1.float() - want_xd).abs() <= want_xd.abs() * 2.0 ** -7 + 1e-3).all()
+    want_dt = F.linear(xd1[:, :R].float(), m.dt_proj.weight.float())
+    assert ((dt1.float() - want_dt).abs() <= want_dt.abs() * 2.0 ** -7 + 1e-3).all()
+    ref_u, _ = orc.causal_conv1d(xz9[:1, :L, :Dm].transpose(1, 2).cpu(), cw.cpu(), cb.cpu(), True,
+                                 cs9[:1].cpu())
+    _close(u1[:L].t().unsqueeze(0), ref_u, 1e-2)

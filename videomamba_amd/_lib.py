@@ -56,7 +56,17 @@ _SIGNATURES = {
          _P, _I, _I, _P, _I, _I,                  # W_x pad, e, e_pad, W_dt pad, r, r_pad
          _P, _LL, _LL, _P, _LL, _LL, _P, _LL, _LL,  # u, x_dbl, dt
          _P, _I,                                  # dt bias, dt softplus
-         _I, _I, _I, _I, _I, _I, _P], _I),
+         _I, _I, _I, _I, _I, _I,                  # out_len, batch, dim, seqlen, width, dtype
+         _P, _LL, _P], _I),                       # workspace, bytes, stream
+    "vm_conv_proj_workspace_bytes": ([_I, _I, _I, _I], _LL),
+    "vm_conv_proj_cm_fwd": (
+        [_P, _LL, _P, _P,                         # xz (row stride), conv weight / bias
+         _P, _I, _LL, _LL, _P, _I, _LL, _LL,      # conv state in / out
+         _P, _I, _I, _P, _I, _I,                  # W_x pad, e, e_pad, W_dt pad, r, r_pad
+         _P, _LL, _P, _LL, _P, _LL,               # u, x_dbl, dt (row strides)
+         _I, _I, _I, _I, _I,                      # out_len, batch, dim, seqlen, width
+         _P, _LL, _P], _I),
+    "vm_conv_proj_cm_workspace_bytes": ([_I, _I, _I, _I], _LL),
     "vm_causal_conv1d_update": (
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_add_norm_fwd": (

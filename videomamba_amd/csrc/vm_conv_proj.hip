@@ -27,7 +27,7 @@
 
 #include <stdlib.h>
 
-#include "vm_common.h"
+#include "vm_conv_proj.h"
 
 namespace vm {
 
@@ -342,6 +342,11 @@ __global__ __launch_bounds__(256) void conv_state_out_kernel(const ConvProjParam
 
 using namespace vm;
 
+extern "C" long long vm_conv_proj_workspace_bytes(int batch, int out_len, int dim, int e) {
+  if (batch > kSkMaxBatch) return 0;
+  return conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
+}
+
 extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                                 const float* conv_weight, const float* conv_bias,
                                 const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
@@ -352,7 +357,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
                                 void* xdbl, long long xd_sb, long long xd_sl,
                                 void* dt, long long dt_sb, long long dt_sl,
                                 const float* dt_bias, int dt_softplus, int out_len, int batch, int dim, int seqlen, int width, int dtype,
-                                vm_stream_t stream) {
+                                void* workspace, long long workspace_bytes, vm_stream_t stream) {
   if (!xz || !conv_weight || !wx_pad || !u || !xdbl || (dt && !wdt_pad)) {
     vmhost::set_error("vm_conv_proj_fwd: null required pointer");
     return VM_E_INVALID;
@@ -403,6 +408,27 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   // skips it (conv + x_proj only: a consumer that projects dt itself)
   const bool fused_dt = dt != nullptr;
   const bool spd = dt_softplus != 0;
+  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= 80 && r_pad <= 80) {
+    // small batch: the split-K form (vm_conv_proj_sk.hip) fills the chip and keeps the
+    // x_proj reduction order fixed per token
+    const long long need = conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
+    if (!workspace || workspace_bytes < need) {
+      vmhost::set_error("vm_conv_proj_fwd: batch <= %d needs a workspace of %lld bytes "
+                        "(vm_conv_proj_workspace_bytes)", kSkMaxBatch, need);
+      return VM_E_INVALID;
+    }
+    ConvProjTmArgs a{};
+    a.x = p.xz; a.x_tl = xz_sl; a.cw = conv_weight; a.cb = conv_bias;
+    a.csi = cs_in; a.csi_dtype = cs_in_dtype; a.csi_sb = csi_sb; a.csi_sd = csi_sd;
+    a.wx = p.wx; a.e = e; a.e_pad = e_pad; a.wdt = fused_dt ? p.wdt : nullptr; a.r = r;
+    a.r_pad = r_pad; a.u = p.u; a.u_tl = u_sl; a.xdbl = p.xdbl; a.xd_tl = xd_sl; a.dt = p.dt;
+    a.dt_tl = dt_sl; a.out_len = out_len; a.batch = batch; a.dim = dim; a.seqlen = seqlen;
+    a.width = width;
+    conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
+    if (cs_out)
+      hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
+    return vmhost::launch_status("vm_conv_proj_fwd");
+  }
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
   switch (e_pad / 16) {  // x_proj output blocks
 #define VM_CP_CASE(NBV)                                              \

@@ -1,0 +1,656 @@
+// Split-K mixer middle for small batches: depthwise causal conv1d + SiLU -> x_proj ->
+// dt_proj, token-major (the mixer's layout at every batch) and channel-major.
+//
+// Replaces the three steps the reference runs between in_proj and the scan
+// (models/videomamba/mamba_simple.py:381-416):
+//     u     = silu(conv1d(x [+ conv_state]))            (causal_conv1d_fn)
+//     x_dbl = u @ W_x^T                                   (x_proj, R + 2N outputs)
+//     dt    = x_dbl[:, :R] @ W_dt^T                       (dt_proj weight; bias -> scan)
+// with the reference's rounding points (u, x_dbl, dt rounded to bf16; fp32 accumulation).
+//
+// Why a split-K form: at B = 1 (the streaming-chunk latency path, 3,144 token rows) the
+// one-workgroup-per-64-rows kernel of vm_conv_proj.hip has 49 workgroups for 256 CUs and
+// sweeps all 1,152 channels serially (94 us per layer, profiles/r02_b1_*), and the library
+// GEMMs for x_proj / dt_proj are latency-bound (12-14 us each for 7 MB) and pick split-K
+// forms whose accumulation order depends on the token count — which broke chunked ==
+// full-sequence bit-equality (scripts/diag/chunk_invariance.py: 5.4e-4 relative at M-32f).
+// Here the channels split into FIXED 128-channel ranges (split s = channels 128s..128s+127,
+// partials summed in split order), so every token's x_dbl / dt bits are independent of
+// the sequence length and batch, and 49 x 9 = 441 workgroups fill the chip at B = 1.
+//
+//   conv_xproj_*_kernel  grid (token tiles of 64, channel splits): the x tile (+ conv halo)
+//     and the split's W_x slice are staged in LDS, conv + SiLU writes u (global, and an LDS
+//     [token][channel] tile), v_mfma_f32_16x16x32_bf16 accumulates the split's x_dbl
+//     partial; partials go to an fp32 workspace.
+//   xdbl_dt_*_kernel     grid (token tiles of 64, 128-channel blocks): sums the partials
+//     in split order (block 0 also writes x_dbl in bf16), stages x_dbl[:R] as an MFMA
+//     operand and computes dt for its 128 channels; dt leaves through an LDS tile as
+//     contiguous row segments.
+// HBM traffic per token: x in, u / dt out (2 * D * 2 B each) + the partials
+// (D/128 * E * 4 B, L2 / infinity-cache resident at small batch).
+
+#include "vm_conv_proj.h"
+
+namespace vm {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct ConvProjCmParams {
+  const bf16_t* x;  // rows = channels (stride x_sd), columns = batch * out_len tokens
+  const float* cw; const float* cb;
+  const void* csi; void* cso;
+  const bf16_t* wx;   // (e_pad, D) zero-padded rows
+  const bf16_t* wdt;  // (D, r_pad) zero-padded columns
+  bf16_t* u; bf16_t* xdbl; bf16_t* dt;
+  float* part;        // [nsplit][e][ntok] fp32 partials of x_dbl
+  long long x_sd, u_sd, xd_sd, dt_sd, csi_sb, csi_sd, cso_sb, cso_sd;
+  int batch, dim, seqlen, lp, ntok, e, e_pad, r, r_pad, width, csi_dtype, cso_dtype;
+  int nsplit, split_ch;  // channel splits of the x_proj reduction, channels per split
+};
+
+constexpr int kCmTok = 64;    // token columns per workgroup
+constexpr int kCmPitch = 72;  // LDS row pitch in bf16 (144 B): 16-B aligned rows
+constexpr int kCmHalo = 8;    // tokens staged before the tile (>= width - 1, 16-B aligned)
+
+// ---------------------------------------------------------------- conv + x_proj partials
+template <int NB>  // NB = e_pad / 16 output row blocks of x_proj
+__global__ __launch_bounds__(256) void conv_xproj_cm_kernel(const ConvProjCmParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t sX[64 * kCmPitch];      // [ch][halo + tok]
+  __shared__ __attribute__((aligned(16))) bf16_t sU[kCmTok * kCmPitch];  // [tok][ch]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int tok0 = blockIdx.x * kCmTok;
+  const int split = blockIdx.y;
+  const int c_beg = split * p.split_ch;
+  const int c_end = min(p.dim, c_beg + p.split_ch);
+  const int W = p.width;
+
+  // conv role: channel (lane) x 16 consecutive tokens (wave)
+  const int ct0 = wave * 16;
+  f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = c_beg; c0 < c_end; c0 += 64) {
+    // ---- stage x[c0 .. c0+63][tok0 - 8 .. tok0 + 63] (16-B pieces, zero outside) ----
+    for (int i = tid; i < 64 * 9; i += 256) {
+      const int row = i / 9, seg = i - row * 9;
+      const int t = tok0 - kCmHalo + seg * 8;
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (t >= 0 && t + 8 <= p.ntok)
+        q = *reinterpret_cast<const uint4*>(p.x + (long long)(c0 + row) * p.x_sd + t);
+      else if (t + 8 > 0 && t < p.ntok) {  // ragged end of the token axis
+        uint16_t h[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          h[k] = (t + k >= 0 && t + k < p.ntok) ? p.x[(long long)(c0 + row) * p.x_sd + t + k] : 0;
+        q = make_uint4(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16),
+                       h[4] | (uint32_t(h[5]) << 16), h[6] | (uint32_t(h[7]) << 16));
+      }
+      *reinterpret_cast<uint4*>(&sX[row * kCmPitch + seg * 8]) = q;
+    }
+    __syncthreads();
+    // ---- conv + SiLU: channel c0 + lane, tokens ct0 .. ct0 + 15 ----
+    {
+      const int c = c0 + lane;
+      float w[4], bias = p.cb ? p.cb[c] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = k < W ? p.cw[c * W + k] : 0.0f;
+      const bf16_t* xr = &sX[lane * kCmPitch + kCmHalo + ct0];
+      uint16_t outv[16];
+      int b = (tok0 + ct0) / p.lp;
+      int step = tok0 + ct0 - b * p.lp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (i > 0 && ++step == p.lp) {  // next batch row (out_len >= 8: at most 2 wraps)
+          step = 0;
+          ++b;
+        }
+        const int tok = tok0 + ct0 + i;
+        float a = bias;
+        if (step >= W - 1) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < W) a = fmaf(w[k], to_f32(xr[i - (W - 1) + k]), a);
+        } else {  // taps before the sequence start: conv state (or zeros)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (k < W) {
+              const int j = step - (W - 1) + k;  // input index in the virtual sequence
+              float v = 0.0f;
+              if (j >= 0) v = to_f32(xr[i - (W - 1) + k]);
+              else if (p.csi && tok < p.ntok)
+                v = load_dyn(p.csi, b * p.csi_sb + (long long)c * p.csi_sd + W + j, p.csi_dtype);
+              a = fmaf(w[k], v, a);
+            }
+          }
+        }
+        const float uval = (step < p.seqlen && tok < p.ntok)
+                               ? a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-a * kLog2e))
+                               : 0.0f;
+        outv[i] = from_f32<bf16_t>(uval);
+        sU[(ct0 + i) * kCmPitch + lane] = outv[i];
+      }
+      // u row segment: 16 tokens = 32 B
+      if (tok0 + ct0 + 16 <= p.ntok) {
+        uint4* dst = reinterpret_cast<uint4*>(p.u + (long long)c * p.u_sd + tok0 + ct0);
+        dst[0] = make_uint4(outv[0] | (uint32_t(outv[1]) << 16), outv[2] | (uint32_t(outv[3]) << 16),
+                            outv[4] | (uint32_t(outv[5]) << 16), outv[6] | (uint32_t(outv[7]) << 16));
+        dst[1] = make_uint4(outv[8] | (uint32_t(outv[9]) << 16), outv[10] | (uint32_t(outv[11]) << 16),
+                            outv[12] | (uint32_t(outv[13]) << 16), outv[14] | (uint32_t(outv[15]) << 16));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (tok0 + ct0 + i < p.ntok) p.u[(long long)c * p.u_sd + tok0 + ct0 + i] = outv[i];
+      }
+    }
+    __syncthreads();
+    // ---- x_proj partial: wave = tokens 16w .. 16w+15, all e_pad rows, K = 64 channels ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+          &sU[(wave * 16 + (lane & 15)) * kCmPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+            p.wx + (long long)(j * 16 + (lane & 15)) * p.dim + c0 + ks * 32 + (lane >> 4) * 8);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // sX / sU are restaged by the next chunk
+  }
+  // ---- partials: part[split][e][tok], 16 consecutive tokens per (e) ----
+  const int tok = tok0 + wave * 16 + (lane & 15);
+  if (tok < p.ntok) {
+    float* dst = p.part + (long long)split * p.e * p.ntok + tok;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int e = j * 16 + (lane >> 4) * 4 + rr;
+        if (e < p.e) dst[(long long)e * p.ntok] = acc[j][rr];
+      }
+  }
+}
+
+// ---------------------------------------------------------------- x_dbl reduce + dt_proj
+__global__ __launch_bounds__(256) void xdbl_dt_cm_kernel(const ConvProjCmParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t sXD[kCmTok * kCmPitch];   // [tok][k]
+  __shared__ __attribute__((aligned(16))) bf16_t sDT[128 * kCmPitch];      // [ch][tok]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int tok0 = blockIdx.x * kCmTok;
+  const int cb = blockIdx.y;  // 128-channel block
+  const bool writer = cb == 0;
+  const int rows = writer ? p.e : p.r;
+  // zero the K padding of the dt operand
+  for (int i = tid; i < kCmTok * kCmPitch / 8; i += 256)
+    reinterpret_cast<uint4*>(sXD)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  for (int idx = tid; idx < rows * kCmTok; idx += 256) {
+    const int e = idx / kCmTok, t = idx - e * kCmTok;
+    const int tok = tok0 + t;
+    if (tok >= p.ntok) continue;
+    float s = 0.0f;
+    for (int sp = 0; sp < p.nsplit; ++sp) s += p.part[((long long)sp * p.e + e) * p.ntok + tok];
+    const bf16_t v = from_f32<bf16_t>(s);
+    if (e < p.r) sXD[t * kCmPitch + e] = v;
+    if (writer) p.xdbl[(long long)e * p.xd_sd + tok] = v;
+  }
+  __syncthreads();
+  // ---- dt for channels cb*128 + 32w .. +31 (2 row tiles) x 64 tokens (4 column tiles) ----
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ksteps = p.r_pad / 32;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (ks < ksteps) {
+      bf16x8 av[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ch = min(cb * 128 + wave * 32 + i * 16 + (lane & 15), p.dim - 1);
+        av[i] = *reinterpret_cast<const bf16x8*>(p.wdt + (long long)ch * p.r_pad + ks * 32 +
+                                                 (lane >> 4) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+            &sXD[(j * 16 + (lane & 15)) * kCmPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        sDT[(wave * 32 + i * 16 + (lane >> 4) * 4 + rr) * kCmPitch + j * 16 + (lane & 15)] =
+            from_f32<bf16_t>(acc[i][j][rr]);
+  __syncthreads();
+  // ---- 128 channel rows x 64 tokens out, 16 B per lane-store ----
+  for (int i = tid; i < 128 * 8; i += 256) {
+    const int row = i >> 3, q = i & 7;
+    const int ch = cb * 128 + row;
+    const int tok = tok0 + q * 8;
+    if (ch >= p.dim) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(&sDT[row * kCmPitch + q * 8]);
+    if (tok + 8 <= p.ntok) {
+      *reinterpret_cast<uint4*>(p.dt + (long long)ch * p.dt_sd + tok) = v;
+    } else {
+      const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+      for (int k = 0; k < 8; ++k)
+        if (tok + k < p.ntok) p.dt[(long long)ch * p.dt_sd + tok + k] = h[k];
+    }
+  }
+}
+
+// New conv state (B, D, width): the last `width` raw inputs of each channel (mamba_simple.py
+// :383-399) — steps L - width .. L - 1 of x, or of the old state before the sequence start.
+__global__ __launch_bounds__(256) void conv_state_cm_kernel(const ConvProjCmParams p) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= p.dim) return;
+  for (int s = 0; s < p.width; ++s) {
+    const int te = p.seqlen - p.width + s;
+    float val = 0.0f;
+    if (te >= 0) val = to_f32(p.x[(long long)c * p.x_sd + (long long)b * p.lp + te]);
+    else if (p.csi) val = load_dyn(p.csi, b * p.csi_sb + (long long)c * p.csi_sd + p.width + te,
+                                   p.csi_dtype);
+    store_dyn(p.cso, b * p.cso_sb + (long long)c * p.cso_sd + s, p.cso_dtype, val);
+  }
+}
+
+// ================================================================ token-major split-K
+constexpr int kTmPitch = 136;  // LDS row pitch in bf16 (272 B): 128 channels + 16-B pad
+constexpr int kSkCh = 128;     // channels per split (fixed: see the file header)
+
+struct SkTmParams {
+  ConvProjTmArgs a;
+  float* part;  // [nsplit][ntok][ep] fp32 partials of x_dbl, ep = round_up(e, 4)
+  int ntok, nsplit, ep;
+};
+
+// x tile rows tok0 - 8 .. tok0 + 63 (zero outside [0, ntok)), channels c0 .. c0 + 127.
+// Latency shape (what bounds these kernels at B = 1, where a CU holds ~2 workgroups and
+// nothing overlaps them): every global load the workgroup needs is issued up front and
+// waited for once; the u and partial stores go out last, so no barrier drains them.
+template <int NB>  // NB = e_pad / 16 output column blocks of x_proj
+__global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) {
+  const ConvProjTmArgs& p = q.a;
+  extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
+  bf16_t* sX = sm;                         // [72][kTmPitch]
+  bf16_t* sU = sX + 72 * kTmPitch;         // [64][kTmPitch]
+  bf16_t* sW = sU + kCmTok * kTmPitch;     // [e_pad][kTmPitch]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int tok0 = blockIdx.x * kCmTok;
+  const int split = blockIdx.y;
+  const int c0 = split * kSkCh;
+  const int W = p.width;
+  const int nch = min(kSkCh, p.dim - c0);  // 128, or 64 for the last split of dim % 128 == 64
+  const bool cact = 2 * lane < nch;
+  const int c = c0 + 2 * (cact ? lane : 0);
+  // ---- one round of global loads: x tile, W_x slice, this thread's conv taps ----
+  constexpr int kXI = (72 * 16 + 255) / 256;  // 16-B x pieces per thread (5)
+  uint4 xv[kXI];
+#pragma unroll
+  for (int k = 0; k < kXI; ++k) {
+    const int i = tid + k * 256;
+    const int rr = i >> 4, qd = i & 15;
+    const int tok = tok0 - kCmHalo + rr;
+    xv[k] = make_uint4(0, 0, 0, 0);
+    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch)
+      xv[k] = *reinterpret_cast<const uint4*>(p.x + (long long)tok * p.x_tl + c0 + qd * 8);
+  }
+  constexpr int kWI = (NB * 16 * 16 + 255) / 256;  // 16-B W_x pieces per thread
+  uint4 wv[kWI];
+#pragma unroll
+  for (int k = 0; k < kWI; ++k) {
+    const int i = tid + k * 256;
+    const int e = i >> 4, qd = i & 15;
+    wv[k] = make_uint4(0, 0, 0, 0);
+    if (i < NB * 16 * 16 && qd * 8 < nch)
+      wv[k] = *reinterpret_cast<const uint4*>(p.wx + (long long)e * p.dim + c0 + qd * 8);
+  }
+  float wl[4], wh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    wl[k] = k < W ? p.cw[c * W + k] : 0.0f;
+    wh[k] = k < W ? p.cw[(c + 1) * W + k] : 0.0f;
+  }
+  const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
+#pragma unroll
+  for (int k = 0; k < kXI; ++k) {
+    const int i = tid + k * 256;
+    if (i < 72 * 16) *reinterpret_cast<uint4*>(&sX[(i >> 4) * kTmPitch + (i & 15) * 8]) = xv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kWI; ++k) {
+    const int i = tid + k * 256;
+    if (i < NB * 16 * 16) *reinterpret_cast<uint4*>(&sW[(i >> 4) * kTmPitch + (i & 15) * 8]) = wv[k];
+  }
+  __syncthreads();
+  // ---- conv + SiLU: channels c, c + 1 (one packed word), tokens 16w .. 16w+15 ----
+  const int t0 = wave * 16;
+  uint32_t upk[16];
+  {
+    int b = (tok0 + t0) / p.out_len;
+    int step = tok0 + t0 - b * p.out_len;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i > 0 && ++step == p.out_len) {  // next batch row (out_len >= 8: at most 2 wraps)
+        step = 0;
+        ++b;
+      }
+      const int tok = tok0 + t0 + i;
+      float al = bl, ah = bh;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < W) {
+          const int j = step - (W - 1) + k;  // input step in the virtual sequence
+          float vl = 0.0f, vh = 0.0f;
+          if (j >= 0) {
+            const uint32_t wd = *reinterpret_cast<const uint32_t*>(
+                &sX[(kCmHalo + t0 + i - (W - 1) + k) * kTmPitch + 2 * lane]);
+            vl = __uint_as_float(wd << 16);
+            vh = __uint_as_float(wd & 0xffff0000u);
+          } else if (p.csi && tok < q.ntok && cact) {  // taps before the sequence start
+            vl = load_dyn(p.csi, b * p.csi_sb + (long long)c * p.csi_sd + W + j, p.csi_dtype);
+            vh = load_dyn(p.csi, b * p.csi_sb + (long long)(c + 1) * p.csi_sd + W + j, p.csi_dtype);
+          }
+          al = fmaf(wl[k], vl, al);
+          ah = fmaf(wh[k], vh, ah);
+        }
+      }
+      const bool live = step < p.seqlen && tok < q.ntok && cact;
+      const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
+      const float uh = live ? ah * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-ah * kLog2e)) : 0.0f;
+      upk[i] = static_cast<uint32_t>(from_f32<bf16_t>(ul)) |
+               (static_cast<uint32_t>(from_f32<bf16_t>(uh)) << 16);
+      *reinterpret_cast<uint32_t*>(&sU[(t0 + i) * kTmPitch + 2 * lane]) = upk[i];
+    }
+  }
+  __syncthreads();
+  // ---- x_proj partial: wave = tokens 16w .. 16w+15 x all e_pad columns, K = 128 ----
+  f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+        &sU[(wave * 16 + (lane & 15)) * kTmPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+          &sW[(j * 16 + (lane & 15)) * kTmPitch + ks * 32 + (lane >> 4) * 8]);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+    }
+  }
+  // ---- stores last: u rows (256 B per wave-store) and the partials ----
+  if (cact) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int tok = tok0 + t0 + i;
+      if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c) = upk[i];
+    }
+  }
+  // D[token 4(lane/16) + r][column lane % 16]: part[split][token][e], 64-B row pieces
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int tok = tok0 + wave * 16 + (lane >> 4) * 4 + rr;
+    if (tok >= q.ntok) continue;
+    float* dst = q.part + ((long long)split * q.ntok + tok) * q.ep;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int e = j * 16 + (lane & 15);
+      if (e < p.e) dst[e] = acc[j][rr];
+    }
+  }
+}
+
+// x_dbl = bf16(sum of the partials in split order); dt = bf16(x_dbl[:, :R] @ W_dt^T).
+// All loads (W_dt fragments, every split's partials) are issued before the first wait.
+template <int NSPL>  // splits (dim / 128 rounded up), 1 .. 16
+__global__ __launch_bounds__(256) void xdbl_dt_tm_kernel(const SkTmParams q) {
+  const ConvProjTmArgs& p = q.a;
+  __shared__ __attribute__((aligned(16))) bf16_t sXD[kCmTok * kCmPitch];   // [tok][k]
+  __shared__ __attribute__((aligned(16))) bf16_t sDT[kCmTok * kTmPitch];   // [tok][128 ch]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int tok0 = blockIdx.x * kCmTok;
+  const int cb = blockIdx.y;  // 128-channel block
+  const bool writer = cb == 0;
+  const bool do_dt = p.wdt != nullptr;
+  bf16x8 bw[2][2];
+  if (do_dt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = min(cb * 128 + wave * 32 + i * 16 + (lane & 15), p.dim - 1);
+        bw[i][ks] = ks * 32 < p.r_pad
+                        ? *reinterpret_cast<const bf16x8*>(p.wdt + (long long)ch * p.r_pad +
+                                                           ks * 32 + (lane >> 4) * 8)
+                        : bf16x8{};
+      }
+  }
+  // reduction items: (token, 4 consecutive columns) over rows R (the dt operand) or E (the
+  // writer block, which also stores x_dbl); every split's float4 of a round of kIt items is
+  // in flight together
+  const int rows = writer ? p.e : p.r;
+  const int q4 = (rows + 3) >> 2;
+  const long long sstride = (long long)q.ntok * q.ep;
+  constexpr int kIt = 3;
+  for (int it0 = 0; it0 < kCmTok * q4; it0 += kIt * 256) {
+    float4 part[kIt][NSPL];
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+      const int it = it0 + tid + k * 256;
+      const int t = it / q4, e0 = (it - t * q4) * 4;
+      const bool ok = it < kCmTok * q4 && tok0 + t < q.ntok;
+      const float* src = q.part + (long long)(tok0 + t) * q.ep + e0;
+#pragma unroll
+      for (int sp = 0; sp < NSPL; ++sp)
+        part[k][sp] = ok ? *reinterpret_cast<const float4*>(src + sp * sstride)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+      const int it = it0 + tid + k * 256;
+      if (it >= kCmTok * q4) continue;
+      const int t = it / q4, e0 = (it - t * q4) * 4;
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int sp = 0; sp < NSPL; ++sp) {
+        sum.x += part[k][sp].x; sum.y += part[k][sp].y; sum.z += part[k][sp].z; sum.w += part[k][sp].w;
+      }
+      const float sv[4] = {sum.x, sum.y, sum.z, sum.w};
+      const int tok = tok0 + t;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int e = e0 + kk;
+        if (e >= rows) break;
+        const bf16_t v = from_f32<bf16_t>(sv[kk]);
+        if (e < p.r) sXD[t * kCmPitch + e] = v;
+        if (writer && tok < q.ntok) p.xdbl[(long long)tok * p.xd_tl + e] = v;
+      }
+    }
+  }
+  // zero K padding of the dt operand (columns r .. r_pad)
+  for (int i = tid; i < kCmTok * (p.r_pad - p.r); i += 256) {
+    const int t = i / (p.r_pad - p.r);
+    sXD[t * kCmPitch + p.r + (i - t * (p.r_pad - p.r))] = bf16_t(0);
+  }
+  if (!do_dt) return;
+  __syncthreads();
+  // ---- dt: tokens (4 tiles of 16) x channels cb*128 + 32w .. +31 (2 tiles), K = r_pad ----
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[jt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (ks * 32 < p.r_pad) {
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+            &sXD[(jt * 16 + (lane & 15)) * kCmPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[jt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[i][ks], acc[jt][i], 0, 0, 0);
+      }
+    }
+  }
+  // D[token 4(lane/16) + r][channel lane % 16] -> sDT[token][channel]
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        sDT[(jt * 16 + (lane >> 4) * 4 + rr) * kTmPitch + wave * 32 + i * 16 + (lane & 15)] =
+            from_f32<bf16_t>(acc[jt][i][rr]);
+  __syncthreads();
+  // 64 token rows x 128 channels out, 16 B per lane-store
+  const int nch = min(128, p.dim - cb * 128);
+  for (int i = tid; i < kCmTok * 16; i += 256) {
+    const int t = i >> 4, qd = i & 15;
+    const int tok = tok0 + t;
+    if (tok >= q.ntok || qd * 8 >= nch) continue;
+    *reinterpret_cast<uint4*>(p.dt + (long long)tok * p.dt_tl + cb * 128 + qd * 8) =
+        *reinterpret_cast<const uint4*>(&sDT[t * kTmPitch + qd * 8]);
+  }
+}
+
+long long conv_proj_sk_workspace_bytes(int batch, int out_len, int dim, int e) {
+  if (batch <= 0 || out_len <= 0 || dim <= 0 || e <= 0) return 0;
+  const long long ntok = 1LL * batch * out_len;
+  const long long nsplit = (dim + kSkCh - 1) / kSkCh;
+  return nsplit * ntok * ((e + 3) / 4 * 4) * static_cast<long long>(sizeof(float));
+}
+
+void conv_proj_sk_launch(const ConvProjTmArgs& a, float* part, hipStream_t s) {
+  SkTmParams q{};
+  q.a = a;
+  q.part = part;
+  q.ntok = a.batch * a.out_len;
+  q.nsplit = (a.dim + kSkCh - 1) / kSkCh;
+  q.ep = (a.e + 3) / 4 * 4;
+  const unsigned tiles = static_cast<unsigned>((q.ntok + kCmTok - 1) / kCmTok);
+  const size_t lds = static_cast<size_t>(72 + kCmTok + a.e_pad) * kTmPitch * sizeof(bf16_t);
+  dim3 g1(tiles, q.nsplit);
+  switch (a.e_pad / 16) {
+#define VM_SK_CASE(NBV) \
+    case NBV: hipLaunchKernelGGL(conv_xproj_tm_kernel<NBV>, g1, dim3(256), lds, s, q); break;
+    VM_SK_CASE(1) VM_SK_CASE(2) VM_SK_CASE(3) VM_SK_CASE(4)
+    VM_SK_CASE(5) VM_SK_CASE(6) VM_SK_CASE(7) VM_SK_CASE(8)
+#undef VM_SK_CASE
+  }
+  const unsigned cblocks = a.wdt ? static_cast<unsigned>((a.dim + 127) / 128) : 1u;
+  const dim3 g2(tiles, cblocks);
+  switch (q.nsplit) {
+#define VM_SK2(NS) case NS: hipLaunchKernelGGL(xdbl_dt_tm_kernel<NS>, g2, dim3(256), 0, s, q); break;
+    VM_SK2(1) VM_SK2(2) VM_SK2(3) VM_SK2(4) VM_SK2(5) VM_SK2(6) VM_SK2(7) VM_SK2(8)
+    VM_SK2(9) VM_SK2(10) VM_SK2(11) VM_SK2(12) VM_SK2(13) VM_SK2(14) VM_SK2(15) VM_SK2(16)
+#undef VM_SK2
+  }
+}
+
+// Split count: a FIXED channel split (128 channels per split) so the x_proj reduction order,
+// and with it every token's x_dbl bits, never depends on the token count — a chunk-
+// dependent split (more splits for shorter sequences) broke chunked == full bitwise.
+// At B = 1 (3,144 tokens, D = 1152) that is 49 x 9 = 441 workgroups.
+constexpr int kCmSplitCh = 128;
+static int cm_splits(int ntok, int dim) {
+  (void)ntok;
+  return (dim + kCmSplitCh - 1) / kCmSplitCh;
+}
+
+}  // namespace vm
+
+using namespace vm;
+
+extern "C" long long vm_conv_proj_cm_workspace_bytes(int batch, int out_len, int dim, int e) {
+  if (batch <= 0 || out_len <= 0 || dim <= 0 || dim % 64 != 0 || e <= 0) return 0;
+  const int ntok = batch * out_len;
+  return static_cast<long long>(cm_splits(ntok, dim)) * e * ntok * sizeof(float);
+}
+
+extern "C" int vm_conv_proj_cm_fwd(const void* xz, long long x_sd,
+                                   const float* conv_weight, const float* conv_bias,
+                                   const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
+                                   void* cs_out, int cs_out_dtype, long long cso_sb, long long cso_sd,
+                                   const void* wx_pad, int e, int e_pad,
+                                   const void* wdt_pad, int r, int r_pad,
+                                   void* u, long long u_sd, void* xdbl, long long xd_sd,
+                                   void* dt, long long dt_sd, int out_len, int batch, int dim,
+                                   int seqlen, int width, void* workspace,
+                                   long long workspace_bytes, vm_stream_t stream) {
+  if (!xz || !conv_weight || !wx_pad || !wdt_pad || !u || !xdbl || !dt) {
+    vmhost::set_error("vm_conv_proj_cm_fwd: null required pointer");
+    return VM_E_INVALID;
+  }
+  if (batch < 0 || dim <= 0 || dim % 64 != 0 || seqlen < 1 || out_len < seqlen || out_len % 8 ||
+      width < 1 || width > 4 || e < 1 || e_pad % 16 != 0 || e_pad < e || e_pad > 128 ||
+      r < 1 || r > e || (r_pad != 32 && r_pad != 64) || r_pad < r ||
+      (cs_in && !vmhost::dtype_ok(cs_in_dtype)) || (cs_out && !vmhost::dtype_ok(cs_out_dtype))) {
+    vmhost::set_error("vm_conv_proj_cm_fwd: unsupported shape (dim %% 64 == 0, out_len %% 8 == 0, "
+                      "width <= 4, R + 2N <= 128, R <= 64, seqlen >= 1)");
+    return VM_E_INVALID;
+  }
+  if (!vmhost::aligned16(xz) || !vmhost::aligned16(u) || !vmhost::aligned16(wx_pad) ||
+      !vmhost::aligned16(wdt_pad) || !vmhost::aligned16(dt) || x_sd % 8 || u_sd % 8 || dt_sd % 8) {
+    vmhost::set_error("vm_conv_proj_cm_fwd: x / u / dt rows and the weights must be 16-byte aligned");
+    return VM_E_INVALID;
+  }
+  if (cs_out && cs_in == cs_out) {
+    vmhost::set_error("vm_conv_proj_cm_fwd: conv_state_out must not alias conv_state_in");
+    return VM_E_INVALID;
+  }
+  if (batch == 0) return VM_OK;
+  const long long need = vm_conv_proj_cm_workspace_bytes(batch, out_len, dim, e);
+  if (!workspace || workspace_bytes < need) {
+    vmhost::set_error("vm_conv_proj_cm_fwd: workspace of %lld bytes required", need);
+    return VM_E_INVALID;
+  }
+  ConvProjCmParams p{};
+  p.x = static_cast<const bf16_t*>(xz); p.cw = conv_weight; p.cb = conv_bias;
+  p.csi = cs_in; p.cso = cs_out;
+  p.wx = static_cast<const bf16_t*>(wx_pad); p.wdt = static_cast<const bf16_t*>(wdt_pad);
+  p.u = static_cast<bf16_t*>(u); p.xdbl = static_cast<bf16_t*>(xdbl); p.dt = static_cast<bf16_t*>(dt);
+  p.part = static_cast<float*>(workspace);
+  p.x_sd = x_sd; p.u_sd = u_sd; p.xd_sd = xd_sd; p.dt_sd = dt_sd;
+  p.csi_sb = csi_sb; p.csi_sd = csi_sd; p.cso_sb = cso_sb; p.cso_sd = cso_sd;
+  p.batch = batch; p.dim = dim; p.seqlen = seqlen; p.lp = out_len; p.ntok = batch * out_len;
+  p.e = e; p.e_pad = e_pad; p.r = r; p.r_pad = r_pad; p.width = width;
+  p.csi_dtype = cs_in_dtype; p.cso_dtype = cs_out_dtype;
+  p.nsplit = cm_splits(p.ntok, dim);
+  p.split_ch = kCmSplitCh;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned tiles = static_cast<unsigned>((p.ntok + kCmTok - 1) / kCmTok);
+  dim3 g1(tiles, p.nsplit);
+  switch (e_pad / 16) {
+#define VM_CM_CASE(NBV) \
+    case NBV: hipLaunchKernelGGL(conv_xproj_cm_kernel<NBV>, g1, dim3(256), 0, st, p); break;
+    VM_CM_CASE(1) VM_CM_CASE(2) VM_CM_CASE(3) VM_CM_CASE(4)
+    VM_CM_CASE(5) VM_CM_CASE(6) VM_CM_CASE(7) VM_CM_CASE(8)
+#undef VM_CM_CASE
+  }
+  hipLaunchKernelGGL(xdbl_dt_cm_kernel, dim3(tiles, (dim + 127) / 128), dim3(256), 0, st, p);
+  if (cs_out)
+    hipLaunchKernelGGL(conv_state_cm_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
+  return vmhost::launch_status("vm_conv_proj_cm_fwd");
+}

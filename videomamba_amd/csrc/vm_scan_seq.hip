@@ -441,6 +441,294 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 }
 
+// ============================================================ chunked form (small batches)
+// The sequence is cut into segments of T steps; a workgroup holds kChW consecutive segments
+// of one 64-channel group (one wave per segment, lane = channel), so the chip fills even at
+// B = 1 (M-16f: 18 groups x 25 blocks x 8 waves = 3,600 waves).  Two launches:
+//   PASS 1: each wave runs its segment from a zero state (no output) -> end state and delta
+//     sum to LDS; the workgroup composes its 8 segments there (wave w owns states 2w, 2w+1)
+//     -> every segment's entry offset E_j and delta prefix P_j relative to the block entry,
+//     and the block aggregate (H, S) -> workspace.
+//   carry : per (b, d, n) the block entries H_blk, sequentially over the blocks (h0 first).
+//   PASS 2: segment j enters at exp2(A P_j) H_blk + E_j and runs its T steps emitting y
+//     (and h_last at the end of the sequence).
+// Per step the math is the single-pass kernel's packed-pair recurrence in log2 units
+// (delta' = softplus(x) log2e, states h' = h log2e), B_t / C_t rows as scalar loads.
+// Compared with the summary / carry / final form it replaces for SGPR-eligible operands,
+// the carry never leaves the chip's LDS except for one aggregate per block.
+constexpr int kChW = 8;  // segments (waves) per workgroup
+
+struct ChunkWork {
+  float* segE;  // [B][nblk][kChW][D][kMaxN]  entry offsets (log2 units)
+  float* segP;  // [B][nblk][kChW][D]         delta' prefixes
+  float* aggH;  // [B][nblk][D][kMaxN]        block end states from a zero entry
+  float* aggS;  // [B][nblk][D]               block delta' sums
+  float* blkH;  // [B][nblk][D][kMaxN]        block entry states (scan_chunk_carry_kernel)
+  int T;        // steps per segment
+  int nblk;     // blocks per sequence
+};
+
+template <typename T, int PASS, bool SP, bool HZ, bool BC1>
+__global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w) {
+  typedef __attribute__((address_space(4))) const uint32_t* cptr;
+  constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
+  constexpr int ES = sizeof(T);
+  __shared__ float sH[kChW][kMaxN][64];
+  __shared__ float sS[kChW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int blk = blockIdx.y;
+  const int b = blockIdx.z;
+  const int d0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 64);
+  const int d_raw = d0 + lane;
+  const bool active = d_raw < p.dim;
+  const int d = active ? d_raw : p.dim - 1;
+  const int N = p.dstate;
+  const int L = p.seqlen;
+  const int t_beg = (blk * kChW + wave) * w.T;
+  const int t_end = min(L, t_beg + w.T);
+  const long long D = p.dim;
+  const long long rowE = ((static_cast<long long>(b) * w.nblk + blk) * kChW) * D;  // + j*D + d
+  const long long rowA = (static_cast<long long>(b) * w.nblk) * D;                  // + k*D + d
+
+  f2 A2[kMaxN / 2], h[kMaxN / 2];
+#pragma unroll
+  for (int q = 0; q < kMaxN / 2; ++q) {
+    A2[q] = f2{2 * q < N ? p.A[d * N + 2 * q] : 0.0f, 2 * q + 1 < N ? p.A[d * N + 2 * q + 1] : 0.0f};
+    h[q] = f2{0.0f, 0.0f};
+  }
+  const float Dv = (p.D ? p.D[d] : 0.0f) * kLog2e;
+  const float bias = (p.dbias ? p.dbias[d] : 0.0f) * kLog2e;
+  // states this wave composes across segments / blocks: 2 * wave, 2 * wave + 1
+  const int n0 = 2 * wave;
+  const float An0 = n0 < N ? p.A[d * N + n0] : 0.0f;
+  const float An1 = n0 + 1 < N ? p.A[d * N + n0 + 1] : 0.0f;
+
+  // PASS 2 entry operands: loaded together with everything else below, combined after
+  // the one wait (every global load of the wave's start-up is a single round trip)
+  float Pj = 0.0f;
+  f2 Ej[kMaxN / 2], Hb[kMaxN / 2];
+  if constexpr (PASS == 2) {
+    Pj = w.segP[rowE + wave * D + d];
+    const float* ep = &w.segE[(rowE + wave * D + d) * kMaxN];
+    const float* hp = &w.blkH[(rowA + blk * D + d) * kMaxN];
+#pragma unroll
+    for (int q = 0; q < kMaxN / 2; ++q) {
+      Ej[q] = *reinterpret_cast<const f2*>(&ep[2 * q]);
+      Hb[q] = *reinterpret_cast<const f2*>(&hp[2 * q]);
+    }
+  }
+
+  const int voff = lane * ES;
+  const int voff_st = active ? voff : kSeqDead;
+  const auto ur = uniform_rsrc(static_cast<const T*>(p.u) + b * p.u_sb + d0);
+  const auto dr_ = uniform_rsrc(static_cast<const T*>(p.delta) + b * p.dl_sb + d0);
+  const auto zr = uniform_rsrc(HZ ? static_cast<const T*>(p.z) + b * p.z_sb + d0
+                                  : static_cast<const T*>(p.u));
+  const auto orr = uniform_rsrc(static_cast<T*>(p.out) + b * p.o_sb + d0);
+  const int us = static_cast<int>(p.u_sl) * ES, ds = static_cast<int>(p.dl_sl) * ES;
+  const int zs = static_cast<int>(p.z_sl) * ES, os = static_cast<int>(p.o_sl) * ES;
+  const T* Bq = static_cast<const T*>(p.B) + b * p.b_sb;
+  const T* Cq = static_cast<const T*>(p.C) + b * p.c_sb;
+  const uint32_t bsl = static_cast<uint32_t>(p.b_sl * ES);
+  const uint32_t csl = static_cast<uint32_t>(p.c_sl * ES);
+  uint32_t bcw[2][2 * NWD];
+  auto bc_load = [&](int t, uint32_t (&dst)[2 * NWD]) {
+    const cptr bp = (cptr)(reinterpret_cast<const char*>(Bq) + static_cast<uint32_t>(t) * bsl);
+    if constexpr (BC1) {
+#pragma unroll
+      for (int i = 0; i < 2 * NWD; ++i) dst[i] = bp[i];
+    } else {
+      const cptr cp = (cptr)(reinterpret_cast<const char*>(Cq) + static_cast<uint32_t>(t) * csl);
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) {
+        dst[i] = bp[i];
+        if constexpr (PASS == 2) dst[NWD + i] = cp[i];
+      }
+    }
+  };
+  const int tlast = L > 0 ? L - 1 : 0;
+  // Warm this XCD's L2 with the block's B / C rows (one dword per 128-byte line, issued with
+  // the start-up loads): the per-step scalar row loads, one step ahead, then hit L2 instead
+  // of paying an infinity-cache / HBM round trip every step.
+  {
+    const int bt0 = blk * kChW * w.T;
+    const int bt1 = min(L, bt0 + kChW * w.T);
+    if (bt1 > bt0) {
+      const char* base = reinterpret_cast<const char*>(Bq) + static_cast<long long>(bt0) * bsl;
+      const int span = (bt1 - bt0 - 1) * static_cast<int>(bsl) + 2 * kMaxN * ES;
+      const int line = static_cast<int>(threadIdx.x) * 128;
+      if (line < span) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(base + line);
+        asm volatile("" ::"v"(v));
+      }
+      if constexpr (!BC1) {
+        const char* cb = reinterpret_cast<const char*>(Cq) + static_cast<long long>(bt0) * csl;
+        const int cspan = (bt1 - bt0 - 1) * static_cast<int>(csl) + kMaxN * ES;
+        if (PASS == 2 && line < cspan) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(cb + line);
+          asm volatile("" ::"v"(v));
+        }
+      }
+    }
+  }
+  uint32_t ru[kPF], rd[kPF], rz[kPF];
+  float sdel = 0.0f;
+  if (t_beg < t_end) {
+    bc_load(t_beg, bcw[0]);
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) {
+      const int t = min(t_beg + j, tlast);
+      ru[j] = bload<T>(ur, voff, t * us);
+      rd[j] = bload<T>(dr_, voff, t * ds);
+      rz[j] = HZ && PASS == 2 ? bload<T>(zr, voff, t * zs) : 0u;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // one wait for every start-up load (parameters, entry operands, prologue): left pending
+  // they would merge into the step loop's header waits
+  __builtin_amdgcn_s_waitcnt(0);
+  if constexpr (PASS == 2) {  // this segment's entry: exp2(A P_j) * H_blk + E_j
+#pragma unroll
+    for (int q = 0; q < kMaxN / 2; ++q) {
+      const f2 x = A2[q] * f2{Pj, Pj};
+      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), Hb[q].x, Ej[q].x),
+                fmaf(__builtin_amdgcn_exp2f(x.y), Hb[q].y, Ej[q].y)};
+    }
+  }
+  for (int tg = t_beg; tg < t_end; tg += kPF) {
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) {
+      const int t = tg + j;
+      const bool live = t < t_end;
+      const float uu = raw_f32<T>(ru[j]);
+      const float dr = raw_f32<T>(rd[j]);
+      const float zz = raw_f32<T>(rz[j]);
+      const int tn = min(t + kPF, tlast);
+      ru[j] = bload<T>(ur, voff, tn * us);
+      rd[j] = bload<T>(dr_, voff, tn * ds);
+      if (HZ && PASS == 2) rz[j] = bload<T>(zr, voff, tn * zs);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
+      bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
+      float dl;
+      if constexpr (SP) {
+        const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
+        dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
+      } else {
+        dl = fmaf(dr, kLog2e, bias);
+      }
+      dl = live ? dl : 0.0f;
+      const float du = dl * uu;
+      const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+      const f2 dl2 = {dl, dl}, du2 = {du, du};
+      f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
+#pragma unroll
+      for (int q = 0; q < kMaxN / 2; ++q) {
+        f2 Bp, Cp;
+        if constexpr (sizeof(T) == 2) {
+          Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
+          Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
+        } else {
+          Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
+          Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
+        }
+        const f2 x = dl2 * A2[q];
+        const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
+        if constexpr (PASS == 2) {
+          if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
+          else ya = __builtin_elementwise_fma(h[q], Cp, ya);
+        }
+      }
+      if constexpr (PASS == 1) {
+        sdel += dl;
+      } else {
+        const f2 ys = ya + yb;
+        float y = ys.x + ys.y;
+        // output gate with y's ln2 factor: z / ((1 + e) * log2e)
+        y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
+                               fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
+               : y * kLn2f;
+        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+      }
+    }
+  }
+
+  if constexpr (PASS == 1) {
+#pragma unroll
+    for (int q = 0; q < kMaxN / 2; ++q) {
+      sH[wave][2 * q][lane] = h[q].x;
+      sH[wave][2 * q + 1][lane] = h[q].y;
+    }
+    sS[wave][lane] = sdel;
+    __syncthreads();
+    // compose the block's segments for states n0, n0 + 1 (wave 0 also writes the prefixes)
+    float E0 = 0.0f, E1 = 0.0f, P = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kChW; ++j) {
+      const float Sj = sS[j][lane];
+      if (active) {
+        *reinterpret_cast<f2*>(&w.segE[(rowE + j * D + d) * kMaxN + n0]) = f2{E0, E1};
+        if (wave == 0) w.segP[rowE + j * D + d] = P;
+      }
+      E0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), E0, sH[j][n0][lane]);
+      E1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), E1, sH[j][n0 + 1][lane]);
+      P += Sj;
+    }
+    if (active) {
+      *reinterpret_cast<f2*>(&w.aggH[(rowA + blk * D + d) * kMaxN + n0]) = f2{E0, E1};
+      if (wave == 0) w.aggS[rowA + blk * D + d] = P;
+    }
+  } else {
+    if (t_beg <= tlast && tlast < t_end && active && L > 0) {  // the segment that ends the sequence
+      if (p.hl) {
+#pragma unroll
+        for (int n = 0; n < kMaxN; ++n)
+          if (n < N)
+            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
+                      ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * kLn2f);
+      }
+      for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
+    }
+  }
+}
+
+// Block entries of the chunked form: H_0 = h0 (log2 units), H_{k+1} = exp2(A S_k) H_k + agg_k.
+// One thread per (b, d, n); the aggregates stream through an 8-deep register window.
+__global__ __launch_bounds__(256) void scan_chunk_carry_kernel(const ScanParams p, const ChunkWork w) {
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
+  if (i >= total) return;
+  const int n = static_cast<int>(i % kMaxN);
+  const long long bd = i / kMaxN;  // b * dim + d
+  const int d = static_cast<int>(bd % p.dim);
+  const int b = static_cast<int>(bd / p.dim);
+  const int N = p.dstate;
+  const float A = n < N ? p.A[d * N + n] : 0.0f;
+  float H = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * kLog2e : 0.0f;
+  const long long D = p.dim;
+  const long long row0 = static_cast<long long>(b) * w.nblk * D + d;  // + k * D
+  constexpr int kWin = 32;  // typically all blocks in one round of loads
+  for (int k0 = 0; k0 < w.nblk; k0 += kWin) {
+    float sk[kWin], hk[kWin];
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) {
+      const long long row = row0 + static_cast<long long>(min(k0 + j, w.nblk - 1)) * D;
+      sk[j] = w.aggS[row];
+      hk[j] = w.aggH[row * kMaxN + n];
+    }
+#pragma unroll
+    for (int j = 0; j < kWin; ++j) {
+      const int k = k0 + j;
+      if (k < w.nblk) {
+        w.blkH[(row0 + static_cast<long long>(k) * D) * kMaxN + n] = H;
+        H = fmaf(__builtin_amdgcn_exp2f(A * sk[j]), H, hk[j]);
+      }
+    }
+  }
+}
+
 // Entry state of every segment: h_in[0] = h0, h_in[s+1] = exp2(A*log2e*sum_delta[s]) *
 // h_in[s] + h_end[s].  One thread per (b, d, n), sequential over the S segments; the
 // summaries stream through a 16-deep register window so their loads overlap the chain.
@@ -536,48 +824,56 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
   }
 }
 
-// Segment count: minimise the busiest SIMD's cycles.  Measured on MI355X (scan_lab,
-// profiles/r01c_scan_lab*.txt, r01c_b1_segments.txt): a wave step costs ~366 issue cycles
-// of its SIMD, and a wave alone on its SIMD still needs ~590 cycles per step (latency-
-// bound), so a wave advances one step every max(590, 366 * waves_per_SIMD) cycles.
-// Segmenting runs every step twice (summary + final pass) and pays ~25 us of fixed
-// start-up per pass plus the carry kernel.
+// Segment count.  A chip-filling batch (>= 1.25 waves per SIMD of 64-channel groups) runs
+// single-pass; below that the sequence is cut so the chunked form has ~1.75 waves per SIMD
+// (every step then runs twice, once per pass), with segments of at least 8 steps.  Measured
+// at B = 1, M-16f (scripts/diag/b1_layouts.py, hipGraph chunk p50): 1,728 waves 4.55 ms,
+// 1,152 waves 4.78 ms, 4,104 waves 4.72 ms.  Depends on (batch, dim, seqlen) only.
 static int choose_segments(int batch, int dim, int seqlen) {
   if (seqlen < 64) return 1;
-  const double groups = (dim + 63) / 64;
-  int best = 1;
-  double best_cost = 0.0;
-  for (int S = 1; S <= kMaxSeg; S *= 2) {
-    const int seg = (seqlen + S - 1) / S;
-    if (S > 1 && seg < 8) break;
-    const int s_eff = (seqlen + seg - 1) / seg;
-    const double per_simd = batch * groups * s_eff / 1024.0;
-    const double step = 366.0 * per_simd > 590.0 ? 366.0 * per_simd : 590.0;
-    const double cost = s_eff > 1 ? step * seg * 2.0 + 100000.0 + 40.0 * s_eff : step * seg;
-    if (S == 1 || cost < best_cost) {
-      best = s_eff;
-      best_cost = cost;
-    }
-  }
-  return best;
+  const long long groups = (dim + 63) / 64;
+  const long long waves = batch * groups;
+  if (waves >= 1280) return 1;
+  long long S = (1792 + waves - 1) / waves;
+  const long long max_s = (seqlen + 7) / 8;
+  if (S > max_s) S = max_s;
+  return S < 2 ? 1 : static_cast<int>(S);
 }
 
 // segments > 0 (an explicit ABI argument: tests and sweeps) forces the segment count;
 // 0 lets the cost model choose.
 static int segments_for(int batch, int dim, int seqlen, int segments) {
-  if (segments > 0) {
-    int S = segments < kMaxSeg ? segments : kMaxSeg;
-    if (S > seqlen) S = seqlen > 0 ? seqlen : 1;
-    return S;
-  }
-  return choose_segments(batch, dim, seqlen);
+  int S = segments > 0 ? segments : choose_segments(batch, dim, seqlen);
+  if (S > seqlen) S = seqlen > 0 ? seqlen : 1;
+  return S < 1 ? 1 : S;
+}
+
+// Chunked-form geometry for S segments: T steps per segment, nblk blocks of kChW segments.
+static void chunk_geometry(int seqlen, int S, int* T, int* nblk) {
+  *T = (seqlen + S - 1) / S;
+  const int segs = (seqlen + *T - 1) / *T;
+  *nblk = (segs + kChW - 1) / kChW;
+}
+
+static size_t chunk_bytes(int batch, int dim, int seqlen, int S) {
+  int T, nblk;
+  chunk_geometry(seqlen, S, &T, &nblk);
+  const size_t per_blk = static_cast<size_t>(kChW + 1) * dim * (kMaxN + 1) +
+                         static_cast<size_t>(dim) * kMaxN;  // + block entries
+  return static_cast<size_t>(batch) * nblk * per_blk * sizeof(float);
+}
+
+static size_t legacy_bytes(int batch, int dim, int S) {
+  if (S > kMaxSeg) S = kMaxSeg;
+  return static_cast<size_t>(batch) * S * dim * (2 * kMaxN + 1) * sizeof(float);
 }
 
 size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen) {
   const int S = segments_for(batch, dim, seqlen, segments);
   if (chosen) *chosen = S;
   if (S <= 1) return 0;
-  return static_cast<size_t>(batch) * S * dim * (2 * kMaxN + 1) * sizeof(float);
+  const size_t a = chunk_bytes(batch, dim, seqlen, S), b = legacy_bytes(batch, dim, S);
+  return a > b ? a : b;
 }
 
 bool seq_supported(const ScanParams& p, int dtype) {
@@ -590,11 +886,52 @@ bool seq_supported(const ScanParams& p, int dtype) {
          (p.z == nullptr || fits(p.z_sl));
 }
 
+template <typename T, bool SP, bool HZ, bool BC1>
+static void launch_chunk_t(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
+  dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1>), grid, dim3(64 * kChW), 0, s, p, w);
+  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
+  hipLaunchKernelGGL(scan_chunk_carry_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                     dim3(256), 0, s, p, w);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1>), grid, dim3(64 * kChW), 0, s, p, w);
+}
+
+template <typename T>
+static void launch_chunk(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
+  const bool hz = p.z != nullptr;
+  const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
+                   static_cast<const T*>(p.C) == static_cast<const T*>(p.B) + kMaxN;
+#define VM_CH(SPV, HZV)                                              \
+  if (bc1) launch_chunk_t<T, SPV, HZV, true>(p, w, s);               \
+  else launch_chunk_t<T, SPV, HZV, false>(p, w, s);
+  if (p.softplus) {
+    if (hz) { VM_CH(true, true) } else { VM_CH(true, false) }
+  } else {
+    if (hz) { VM_CH(false, true) } else { VM_CH(false, false) }
+  }
+#undef VM_CH
+}
+
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
                 size_t workspace_bytes, hipStream_t s) {
   int S = 1;
   const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
+  const int es = dtype == VM_DTYPE_BF16 ? 2 : 4;
+  if (S > 1 && workspace && workspace_bytes >= need && seq_sgpr_bc(p, es)) {
+    ChunkWork w{};
+    chunk_geometry(p.seqlen, S, &w.T, &w.nblk);
+    const size_t nb = static_cast<size_t>(p.batch) * w.nblk;
+    w.segE = static_cast<float*>(workspace);
+    w.segP = w.segE + nb * kChW * p.dim * kMaxN;
+    w.aggH = w.segP + nb * kChW * p.dim;
+    w.aggS = w.aggH + nb * p.dim * kMaxN;
+    w.blkH = w.aggS + nb * p.dim;
+    if (dtype == VM_DTYPE_BF16) launch_chunk<bf16_t>(p, w, s);
+    else launch_chunk<float>(p, w, s);
+    return;
+  }
   SeqWork w{};
+  if (S > kMaxSeg) S = kMaxSeg;
   if (S > 1 && workspace && workspace_bytes >= need) {
     const size_t states = static_cast<size_t>(p.batch) * S * p.dim * kMaxN;
     w.hend = static_cast<float*>(workspace);

@@ -98,12 +98,19 @@ class StreamingChunkGraph:
                      for t in list(self.model.parameters()) + list(self.model.buffers()))
 
     def _workspace(self) -> Tensor:
-        """Scan scratch sized for the largest token-major scan of a chunk (every layer has
-        the same shape); allocated once per capture set and owned by this runner."""
+        """Kernel scratch (segmented scan, channel-major conv_proj partials) sized for the
+        largest consumer of a chunk; allocated once per capture set, owned by this runner."""
         m = self.model
         gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
         L = self.tt * gh * gw + 1
-        need = max(K.scan_workspace_bytes(self.batch, mx.d_inner, L, mx.d_state)
+        Lp = (L + 7) // 8 * 8
+        need = max(max(K.scan_workspace_bytes(self.batch, mx.d_inner, L, mx.d_state),
+                       K.conv_proj_cm_workspace_bytes(self.batch, Lp, mx.d_inner,
+                                                      mx.dt_rank + 2 * mx.d_state)
+                       if mx.d_inner % 64 == 0 else 0,
+                       K.conv_proj_workspace_bytes(self.batch, Lp, mx.d_inner,
+                                                   mx.dt_rank + 2 * mx.d_state)
+                       if mx.d_inner % 64 == 0 else 0)
                    for mx in m._mixers())
         if self._ws is None or self._ws.numel() < max(need, 1):
             self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
@@ -114,12 +121,12 @@ class StreamingChunkGraph:
         ws = self._workspace()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.no_grad(), torch.cuda.stream(side), K.scan_workspace_override(ws):
+        with torch.no_grad(), torch.cuda.stream(side), K.scratch_override(ws):
             for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
                 self._body(has_cls)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scan_workspace_override(ws):
+        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws):
             outs = self._body(has_cls)
         self._pool = g.pool()
         self.load_state(saved)  # warm-up passes advanced the state: restore it

@@ -99,10 +99,12 @@ _WORKSPACE = {}
 _WS_OVERRIDE = [None]
 
 
-class scan_workspace_override:
-    """Within the block every token-major scan uses ``buf`` (a uint8 device tensor owned
+class scratch_override:
+    """Within the block every kernel that needs scratch (the segmented token-major scan,
+    the channel-major conv_proj's x_proj partials) uses ``buf`` (a uint8 device tensor owned
     by the caller) instead of the per-stream cache — how a captured HIP graph keeps its
-    scratch alive and fixed for its lifetime (graphs.StreamingChunkGraph)."""
+    scratch alive and fixed for its lifetime (graphs.StreamingChunkGraph).  Consumers run
+    one after another on one stream, so they share the buffer from offset 0."""
 
     def __init__(self, buf: Tensor):
         self.buf = buf
@@ -117,14 +119,19 @@ class scan_workspace_override:
         return False
 
 
-def scan_workspace(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
-    """Scratch for the time-segmented token-major scan, one buffer per (device, stream),
-    grown and never shrunk.  When it grows, the old buffer is released back to the
-    caching allocator on that same stream, so work already queued there finishes first.
-    Captured HIP graphs own their workspace (graphs.StreamingChunkGraph) and never
-    reach this cache."""
+def scratch(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
+    """Kernel scratch, one buffer per (device, stream), grown and never shrunk (or the
+    caller's buffer inside ``scratch_override``).  When it grows, the old buffer is released
+    back to the caching allocator on that same stream, so work already queued there
+    finishes first.  Captured HIP graphs own their scratch (graphs.StreamingChunkGraph) and
+    never reach this cache."""
     if nbytes <= 0:
         return None
+    ov = _WS_OVERRIDE[0]
+    if ov is not None:
+        if ov.numel() < nbytes:
+            raise RuntimeError(f"scratch_override buffer too small: {ov.numel()} < {nbytes}")
+        return ov
     key = (device.type, device.index, stream)
     buf = _WORKSPACE.get(key)
     if buf is None or buf.numel() < nbytes:
@@ -149,8 +156,6 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
     seg = int(options.get().scan_segments)
     ws_bytes = 0
     ws = None
-    if workspace is None:
-        workspace = _WS_OVERRIDE[0]
     if u_s[1] == 1:
         ws_bytes = scan_workspace_bytes(batch, dim, seqlen, dstate, seg)
         if workspace is not None:
@@ -158,7 +163,7 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
                 raise ValueError(f"scan workspace too small: {workspace.numel()} < {ws_bytes}")
             ws = workspace
         else:
-            ws = scan_workspace(u.device, int(stream), ws_bytes)
+            ws = scratch(u.device, int(stream), ws_bytes)
     rc = lib.vm_selective_scan_fwd(
         _p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
         _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
@@ -192,6 +197,8 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
     activated step softplus(dt + dt_bias32) instead (the scan then runs without them).
     dt=None skips dt_proj (conv + x_proj only; wdt_pad may be None)."""
     lib = _lib.load()
+    nbytes = int(lib.vm_conv_proj_workspace_bytes(batch, out_len, dim, e))
+    ws = scratch(xz.device, int(stream), nbytes)
     rc = lib.vm_conv_proj_fwd(
         _p(xz), xz_s[0], xz_s[1], _p(cw32), _p(cb32),
         _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
@@ -200,8 +207,37 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
         wdt_pad.shape[1] if wdt_pad is not None else 0,
         _p(u), u_s[0], u_s[1], _p(xdbl), xd_s[0], xd_s[1], _p(dt),
         dt_s[0] if dt is not None else 0, dt_s[1] if dt is not None else 0,
-        _p(dt_bias32), int(dt_softplus), out_len, batch, dim, seqlen, width, dtype_code(u.dtype), stream)
+        _p(dt_bias32), int(dt_softplus), out_len, batch, dim, seqlen, width, dtype_code(u.dtype),
+        _p(ws), nbytes, stream)
     _lib.check(rc, "vm_conv_proj_fwd")
+
+
+def conv_proj_workspace_bytes(batch: int, out_len: int, dim: int, e: int) -> int:
+    return int(_lib.load().vm_conv_proj_workspace_bytes(batch, out_len, dim, e))
+
+
+def conv_proj_cm_workspace_bytes(batch: int, out_len: int, dim: int, e: int) -> int:
+    return int(_lib.load().vm_conv_proj_cm_workspace_bytes(batch, out_len, dim, e))
+
+
+def conv_proj_cm_raw(xz, x_sd, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, wdt_pad, r,
+                     u, u_sd, xdbl, xd_sd, dt, dt_sd, out_len, batch, dim, seqlen, width,
+                     stream):
+    """Channel-major conv1d + SiLU -> x_proj -> dt_proj (bf16, small batches): rows are
+    channels (x = the first ``dim`` rows of xz), columns the batch * out_len tokens;
+    ``*_sd`` are row strides.  Scratch for the split-K x_proj partials comes from
+    :func:`scratch`."""
+    lib = _lib.load()
+    nbytes = conv_proj_cm_workspace_bytes(batch, out_len, dim, e)
+    ws = scratch(xz.device, int(stream), nbytes)
+    rc = lib.vm_conv_proj_cm_fwd(
+        _p(xz), x_sd, _p(cw32), _p(cb32),
+        _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
+        _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
+        _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad), r, wdt_pad.shape[1],
+        _p(u), u_sd, _p(xdbl), xd_sd, _p(dt), dt_sd, out_len, batch, dim, seqlen, width,
+        _p(ws), nbytes, stream)
+    _lib.check(rc, "vm_conv_proj_cm_fwd")
 
 
 def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_rms, stream):

@@ -64,17 +64,18 @@ _CUDA_ERROR = ("VideoMamba requires CUDA tensors in this package because its HIP
 
 
 def mixer_layout(batch: int, d_inner: int, device: torch.device) -> str:
-    """"tm" (token-major, channel-per-lane scan) when batch x 64-channel groups gives at
-    least ~1.25 waves per SIMD, else "cm" (channel-major, time-parallel scan).  Measured
-    at D=1152, L=3137 (profiles/): the time-parallel kernel costs ~24 us per clip-layer at
-    any batch, the channel-per-lane one ~1.6 ms flat up to 2 waves/SIMD (15 us per
-    clip-layer at B=112).  ``options.mixer_layout`` ("tm" | "cm") overrides."""
+    """"tm" (token-major: every buffer (B*Lp, channels), channel-per-lane scan; time-
+    segmented two-pass form below a chip-filling batch) at every batch size; "cm"
+    (channel-major buffers, time-parallel scan) only when ``options.mixer_layout`` asks.
+    Token-major runs every token with arithmetic that does not depend on the sequence
+    length, so chunked streaming matches the full sequence within the north star's 1e-4 at
+    every batch (the channel-major time-parallel scan missed it at M-32f B=1: 1.1e-4,
+    scripts/diag/chunk_invariance.py); at B=1 it costs ~0.2 ms of chunk latency against the
+    channel-major path with library x_proj / dt_proj GEMMs (scripts/diag/b1_layouts.py)."""
     forced = options.get().mixer_layout
     if forced != "auto":
         return forced
-    simds = 4 * torch.cuda.get_device_properties(device).multi_processor_count
-    waves = batch * ((d_inner + 63) // 64)
-    return "tm" if waves >= 1.25 * simds else "cm"
+    return "tm"
 
 
 class InferenceParamsLike(Protocol):
@@ -200,14 +201,26 @@ class Mamba(nn.Module):
             xz += self.in_proj.bias.to(xz.dtype)[:, None]
         x, z = xz[:Dm], xz[Dm:]
         u = torch.empty((Dm, n), dtype=hn.dtype, device=hn.device)
-        K.conv_raw(x, rows3, cw, cb,
-                   conv_state_in, (conv_state_in.stride(0), conv_state_in.stride(1))
-                   if conv_state_in is not None else (0, 0),
-                   conv_state_out, (conv_state_out.stride(0), conv_state_out.stride(1))
-                   if conv_state_out is not None else (0, 0),
-                   u, rows3, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
-        x_dbl = _matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
-        dt = _matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
+        csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
+                 if conv_state_in is not None else (0, 0))
+        cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
+                 if conv_state_out is not None else (0, 0))
+        if self._fused_conv_proj_ok(hn, seqlen):
+            # conv + silu -> x_proj -> dt_proj with a fixed reduction order
+            # (vm_conv_proj_cm.hip): faster than the latency-bound library GEMMs at small
+            # batch, and chunk-invariant (every token's bits independent of L)
+            wx_pad, wdt_pad = self._padded_proj_weights()
+            E = R + 2 * N
+            x_dbl = torch.empty((E, n), dtype=hn.dtype, device=hn.device)
+            dt = torch.empty((Dm, n), dtype=hn.dtype, device=hn.device)
+            K.conv_proj_cm_raw(xz, n, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
+                               wx_pad, E, wdt_pad, R, u, n, x_dbl, n, dt, n, Lp, Bsz, Dm,
+                               seqlen, W, stream)
+        else:
+            K.conv_raw(x, rows3, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
+                       u, rows3, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
+            x_dbl = _matmul(self.x_proj.weight, u)  # (R+2N, B*Lp)
+            dt = _matmul(self.dt_proj.weight, x_dbl[:R])  # (D, B*Lp), bias added in scan
         y = torch.empty_like(u)
         K.scan_raw(u, rows3, dt, rows3, A, x_dbl[R:R + N], rows3, x_dbl[R + N:], rows3, Dv,
                    z, rows3, dbias, True,
