@@ -19,6 +19,10 @@
  *                                 layout (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
+ *   vm_norm_pool_fwd           <- final add + norm (videomamba.py:896-918) with the
+ *                                 per-frame / whole-clip column sums of the pooling
+ *   vm_pool_finish_fwd         <- the pooling tail: means, CLS add / concat and pool_norm
+ *                                 LayerNorm (videomamba.py:983-1062, :702-751 masked)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
  *                                 (videomamba.py:359-368, :806-815)
  *
@@ -40,7 +44,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 4
+#define VM_ABI_VERSION 5
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -207,6 +211,40 @@ int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dt
                     const float* weight, const float* bias, void* out, int out_dtype,
                     void* residual_out, int res_out_dtype, long long rows, int cols,
                     float eps, int is_rms, vm_stream_t stream);
+
+/*
+ * Final add + norm fused with the pooling front half.  Per batch row b, rows
+ * [0, rows) of x (+ residual) at x + b*in_batch_stride are normalised into the
+ * contiguous out (batch, rows, cols).  Rows [0, head) (the CLS row) are only normalised;
+ * rows [head, rows) form `groups` pooling groups: equal groups of `group_rows` rows when
+ * bounds == NULL (head + groups*group_rows == rows, max_group_rows == group_rows), else
+ * bounds (batch, groups+1) int32 row bounds with bounds[b][0] == head and
+ * bounds[b][groups] == rows and every group at most max_group_rows rows.  With a
+ * workspace (>= vm_norm_pool_workspace_bytes) the fp32 column sums of the rounded outputs
+ * of each group are written there for vm_pool_finish_fwd; NULL skips them.
+ * cols % 4 == 0, cols <= 2048, 16-byte aligned x / residual / out / weight.
+ */
+long long vm_norm_pool_workspace_bytes(int batch, int groups, int max_group_rows, int cols);
+int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
+                     long long in_batch_stride, const float* weight, const float* bias,
+                     float eps, int is_rms, void* out, int out_dtype, int batch, int rows,
+                     int cols, int head, int groups, int group_rows, const int* bounds,
+                     int max_group_rows, void* workspace, long long workspace_bytes,
+                     vm_stream_t stream);
+
+/*
+ * Pool tail over vm_norm_pool_fwd's workspace (same batch / groups / group_rows /
+ * bounds / max_group_rows).  mode: 0 avg, 1 cls+avg, 2 cls_cat_avg, 3 cls.  The average
+ * is per group (keep_temporal) or over all groups, rounded to xp_dtype; cls+avg adds the
+ * CLS row (cls + b*cls_batch_stride, rounded again); cls_cat_avg puts the CLS row first.
+ * Each pooled row then gets LayerNorm(ln_weight, ln_bias, ln_eps) -> x_pool
+ * (batch, P, cols) with P = 1 (cls), groups or 1 (avg, cls+avg), 1 + that (cls_cat_avg).
+ */
+int vm_pool_finish_fwd(const void* workspace, int batch, int groups, int group_rows,
+                       const int* bounds, int max_group_rows, const void* cls, int cls_dtype,
+                       long long cls_batch_stride, int mode, int keep_temporal,
+                       const float* ln_weight, const float* ln_bias, float ln_eps,
+                       void* x_pool, int xp_dtype, int cols, vm_stream_t stream);
 
 /*
  * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,P,P)):

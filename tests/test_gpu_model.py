@@ -11,6 +11,7 @@ from types import SimpleNamespace
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 import video_mamba
 from conftest import load_golden
@@ -213,6 +214,80 @@ def test_mask_validation_messages():
         m[:, torch.tensor([0, 1, 5, 6, 9, 13, 14, 15])] = False
         _, xp = model(x, mask=m, keep_temporal=True)
         assert xp.shape == (2, 4, 16)
+
+
+def _torch_pool(feats, pool, keep_temporal, vis, tt, hw, pool_norm):
+    """Plain-torch restatement of the reference pooling (videomamba.py:983-1062, masked
+    per-frame means :702-751 with fp32 sums) over the fused kernel's features."""
+    cls_tok, patch = feats[:, :1], feats[:, 1:]
+    ln = lambda v: F.layer_norm(v.float(), (v.shape[-1],), pool_norm.weight.float(),  # noqa: E731
+                                pool_norm.bias.float(), pool_norm.eps).to(v.dtype)
+    if pool == "cls":
+        return ln(cls_tok)
+    if keep_temporal:
+        Bsz, n, C = patch.shape
+        if vis is None:
+            avg = patch.float().reshape(Bsz, tt, hw, C).mean(2).to(patch.dtype)
+        else:
+            fr = torch.div(vis[:, 1:] - 1, hw, rounding_mode="floor")
+            sums = torch.zeros(Bsz, tt, C, device=patch.device)
+            sums.scatter_add_(1, fr.unsqueeze(-1).expand(-1, -1, C), patch.float())
+            cnt = torch.zeros(Bsz, tt, 1, device=patch.device)
+            cnt.scatter_add_(1, fr.unsqueeze(-1), torch.ones(Bsz, n, 1, device=patch.device))
+            avg = (sums / cnt).to(patch.dtype)
+    else:
+        avg = patch.float().mean(1, keepdim=True).to(patch.dtype)
+    if pool == "cls+avg":
+        return ln(cls_tok + avg)
+    if pool == "cls_cat_avg":
+        return ln(torch.cat([cls_tok, avg], 1))
+    return ln(avg)
+
+
+@pytest.mark.parametrize("geom", ["small", "m16"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("keep_temporal", [False, True])
+@pytest.mark.parametrize("pool", ["avg", "cls+avg", "cls_cat_avg", "cls"])
+def test_fused_final_norm_pool_matches_torch_pooling(pool, keep_temporal, masked, dt, geom):
+    """vm_norm_pool_fwd + vm_pool_finish_fwd: features bit-equal to forward_features and
+    x_pool equal to a torch restatement of the reference pooling over those features
+    (fp32 1e-5; bf16 within 2 ulp of the pooled values: the sums run in another order)."""
+    torch.manual_seed(1)
+    if geom == "small":
+        model = _small_model(pool_type=pool)
+        T, S, n_keep = 4, 8, 2
+    else:
+        model = PretrainVideoMamba(depth=1, embed_dim=576, num_frames=16, pool_type=pool)
+        T, S, n_keep = 16, 224, 60
+    model = model.to(DEV, dt).eval()
+    with torch.no_grad():
+        model.pool_norm.weight.normal_()
+        model.pool_norm.bias.normal_()
+    Bsz = 2
+    x = torch.randn(Bsz, 3, T, S, S, device=DEV, dtype=dt)
+    tt = model._validate_temporal_length(T)
+    hw = (S // model.patch_embed.patch_size[0]) ** 2
+    mask = vis = None
+    if masked:  # keep n_keep tokens of every frame (+ CLS), different per sample
+        mask = torch.ones(Bsz, 1 + tt * hw, dtype=torch.bool, device=DEV)
+        mask[:, 0] = False
+        for b in range(Bsz):
+            for f in range(tt):
+                keep = torch.randperm(hw, device=DEV)[:n_keep] + 1 + f * hw
+                mask[b, keep] = False
+        vis = torch.sort(torch.where(~mask, torch.arange(mask.shape[1], device=DEV),
+                                     mask.shape[1]), 1).values[:, :1 + tt * n_keep]
+    with torch.no_grad():
+        feats = model.forward_features(x, mask)
+        xv, xp = model(x, mask, keep_temporal=keep_temporal)
+    assert torch.equal(xv, feats[:, 1:])
+    ref = _torch_pool(feats, pool, keep_temporal, vis, tt, hw, model.pool_norm)
+    assert xp.shape == ref.shape and xp.dtype == ref.dtype
+    if dt == torch.float32:
+        torch.testing.assert_close(xp, ref, rtol=1e-5, atol=1e-5)
+    else:
+        torch.testing.assert_close(xp.float(), ref.float(), rtol=2e-2, atol=4e-2)
 
 
 def test_temporal_runtime_length_and_offsets():

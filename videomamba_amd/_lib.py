@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _P = c_void_p
 _LL = c_longlong
@@ -71,6 +71,17 @@ _SIGNATURES = {
         [_P, _LL, _P, _I, _LL, _LL, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_add_norm_fwd": (
         [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _LL, _I, c_float, _I, _P], _I),
+    "vm_norm_pool_workspace_bytes": ([_I, _I, _I, _I], _LL),
+    "vm_norm_pool_fwd": (
+        [_P, _I, _P, _I, _LL,                     # x, residual, batch stride
+         _P, _P, c_float, _I,                     # weight, bias, eps, is_rms
+         _P, _I, _I, _I, _I,                      # out, out dtype, batch, rows, cols
+         _I, _I, _I, _P, _I,                      # head, groups, group_rows, bounds, max rows
+         _P, _LL, _P], _I),
+    "vm_pool_finish_fwd": (
+        [_P, _I, _I, _I, _P, _I,                  # workspace, batch, groups, rows, bounds, max
+         _P, _I, _LL, _I, _I,                     # cls, dtype, stride, mode, keep_temporal
+         _P, _P, c_float, _P, _I, _I, _P], _I),   # LN w / b / eps, x_pool, dtype, cols
     "vm_patch_embed_fwd": (
         [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
 }

@@ -158,9 +158,296 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const NormParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Final add + norm fused with the pooling front half (videomamba.py:896-918 then :983-1062).
+//
+// Rows of one batch row are cut into a head (the CLS row, normalised but not pooled) and
+// `groups` contiguous pooling groups (frames; for masked input the host passes the
+// frame bounds of the gathered visible tokens).  A workgroup normalises up to kPoolRB
+// rows of one group — writing them straight into the contiguous (batch, rows, cols)
+// features, so the padded buffer needs no slice copy — and writes the fp32 column sum
+// of the rounded outputs to part[b][g][slice].  pool_finish_kernel then sums the slices
+// (and groups) in a fixed order, so the result is deterministic and independent of the
+// launch geometry; the reference's means are of the rounded patch tokens as well.
+constexpr int kPoolRB = 16;
+
+struct NormPoolParams {
+  const void* x; const void* res; const float* w; const float* bias; void* out;
+  long long in_bstride;             // elements between batch rows of x / res (padded L * cols)
+  int rows, cols; float eps; int is_rms, x_dtype, res_dtype, out_dtype;
+  int head, groups, group_rows;     // implicit equal groups when bounds == nullptr
+  const int* bounds;                // (batch, groups + 1) row bounds or nullptr
+  int slices;                       // kPoolRB-row slices per group
+  float* part;                      // (batch, groups, slices, cols) or nullptr
+};
+
+template <int CPL>
+__global__ __launch_bounds__(256) void norm_pool_rows_kernel(const NormPoolParams p) {
+  extern __shared__ float red[];    // [4][cols]
+  const int b = blockIdx.z, gy = blockIdx.y, s = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int lo, hi;
+  if (gy == 0) {
+    if (s) return;
+    lo = 0; hi = p.head;
+  } else if (p.bounds) {
+    lo = p.bounds[(long long)b * (p.groups + 1) + gy - 1];
+    hi = p.bounds[(long long)b * (p.groups + 1) + gy];
+  } else {
+    lo = p.head + (gy - 1) * p.group_rows;
+    hi = lo + p.group_rows;
+  }
+  const int r0 = lo + s * kPoolRB;
+  const int r1 = min(hi, r0 + kPoolRB);
+  float acc[CPL][4];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = 0.0f;
+  for (int r = r0 + wave; r < r1; r += 4) {
+    const long long in = (long long)b * p.in_bstride + (long long)r * p.cols;
+    const long long on = ((long long)b * p.rows + r) * p.cols;
+    float v[CPL][4];
+    float sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane * 4 + 256 * j;
+      if (c < p.cols) {
+        load4_dyn(p.x, in + c, p.x_dtype, v[j]);
+        if (p.res) {
+          float q[4];
+          load4_dyn(p.res, in + c, p.res_dtype, q);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[j][i] += q[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[j][i] = 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += v[j][i];
+    }
+    float mean = 0.0f, sq = 0.0f;
+    if (!p.is_rms) mean = wave_sum(sum) / p.cols;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const bool in_c = lane * 4 + 256 * j < p.cols;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dv = in_c ? v[j][i] - mean : 0.0f;
+        sq = fmaf(dv, dv, sq);
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(sq) / p.cols + p.eps);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane * 4 + 256 * j;
+      if (c < p.cols) {
+        const float4 w = *reinterpret_cast<const float4*>(p.w + c);
+        const float wv[4] = {w.x, w.y, w.z, w.w};
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          y[i] = (v[j][i] - mean) * rstd * wv[i];
+          if (p.bias) y[i] += p.bias[c + i];
+          if (p.out_dtype == VM_DTYPE_BF16) y[i] = to_f32(from_f32<bf16_t>(y[i]));
+          acc[j][i] += y[i];
+        }
+        store4_dyn(p.out, on + c, p.out_dtype, y);
+      }
+    }
+  }
+  if (gy == 0 || !p.part) return;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane * 4 + 256 * j;
+    if (c < p.cols)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave * p.cols + c + i] = acc[j][i];
+  }
+  __syncthreads();
+  float* dst = p.part + (((long long)b * p.groups + gy - 1) * p.slices + s) * p.cols;
+  for (int c = threadIdx.x; c < p.cols; c += 256)
+    dst[c] = ((red[c] + red[p.cols + c]) + red[2 * p.cols + c]) + red[3 * p.cols + c];
+}
+
+// Pool finish: per (pooled row, batch row) sum the slices of its group(s) in order, take
+// the mean (rounded to the output dtype like the reference's bf16 mean), add the CLS row
+// for cls+avg, and apply the pool LayerNorm (fp32 statistics, eps of the module).
+enum PoolMode { kPoolAvg = 0, kPoolClsAvg = 1, kPoolClsCatAvg = 2, kPoolCls = 3 };
+
+struct PoolFinishParams {
+  const float* part; int groups, slices, group_rows; const int* bounds;
+  const void* cls; long long cls_bstride; int cls_dtype;
+  int mode, keep_temporal;
+  const float* lnw; const float* lnb; float ln_eps;
+  void* xpool; int xp_dtype; int cols, prow;  // prow = pooled rows per batch row
+};
+
+__device__ __forceinline__ float block_sum256(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+__global__ __launch_bounds__(256) void pool_finish_kernel(const PoolFinishParams p) {
+  constexpr int kMaxPer = 8;  // cols <= 2048
+  __shared__ float sh[4];
+  const int q = blockIdx.x, b = blockIdx.y;
+  const bool rnd = p.xp_dtype == VM_DTYPE_BF16;
+  auto group_count = [&](int g) -> int {
+    return p.bounds ? p.bounds[(long long)b * (p.groups + 1) + g + 1] -
+                          p.bounds[(long long)b * (p.groups + 1) + g]
+                    : p.group_rows;
+  };
+  const bool use_cls = p.mode == kPoolCls || (p.mode == kPoolClsCatAvg && q == 0);
+  const int aq = p.mode == kPoolClsCatAvg ? q - 1 : q;  // index of the averaged row
+  const int g0 = p.keep_temporal ? aq : 0;
+  const int g1 = p.keep_temporal ? aq + 1 : p.groups;
+  int count = 0;
+  if (!use_cls)
+    for (int g = g0; g < g1; ++g) count += group_count(g);
+  float v[kMaxPer];
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    float x = 0.0f;
+    if (c < p.cols) {
+      const float cl = p.cls ? load_dyn(p.cls, (long long)b * p.cls_bstride + c, p.cls_dtype)
+                             : 0.0f;
+      if (use_cls) {
+        x = cl;
+      } else {
+        float sum = 0.0f;
+        for (int g = g0; g < g1; ++g)
+          for (int s = 0; s < p.slices; ++s)
+            sum += p.part[(((long long)b * p.groups + g) * p.slices + s) * p.cols + c];
+        x = sum / static_cast<float>(count);
+        if (rnd) x = to_f32(from_f32<bf16_t>(x));
+        if (p.mode == kPoolClsAvg) {
+          x += cl;
+          if (rnd) x = to_f32(from_f32<bf16_t>(x));
+        }
+      }
+    }
+    v[k] = x;
+  }
+  float s1 = 0.0f;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) s1 += v[k];
+  const float mean = block_sum256(s1, sh) / p.cols;
+  float s2 = 0.0f;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const float d = threadIdx.x + 256 * k < p.cols ? v[k] - mean : 0.0f;
+    s2 = fmaf(d, d, s2);
+  }
+  const float rstd = rsqrtf(block_sum256(s2, sh) / p.cols + p.ln_eps);
+  const long long o = ((long long)b * p.prow + q) * p.cols;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    if (c < p.cols) {
+      float y = (v[k] - mean) * rstd;
+      if (p.lnw) y *= p.lnw[c];
+      if (p.lnb) y += p.lnb[c];
+      store_dyn(p.xpool, o + c, p.xp_dtype, y);
+    }
+  }
+}
+
 }  // namespace vm
 
 using namespace vm;
+
+extern "C" long long vm_norm_pool_workspace_bytes(int batch, int groups, int max_group_rows,
+                                                  int cols) {
+  if (batch < 0 || groups < 0 || max_group_rows < 0 || cols < 0) return -1;
+  const long long slices = (max_group_rows + kPoolRB - 1) / kPoolRB;
+  return (long long)batch * groups * slices * cols * static_cast<long long>(sizeof(float));
+}
+
+extern "C" int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
+                                long long in_batch_stride, const float* weight, const float* bias,
+                                float eps, int is_rms, void* out, int out_dtype, int batch,
+                                int rows, int cols, int head, int groups, int group_rows,
+                                const int* bounds, int max_group_rows, void* workspace,
+                                long long workspace_bytes, vm_stream_t stream) {
+  if (!x || !weight || !out) {
+    vmhost::set_error("vm_norm_pool_fwd: null required pointer");
+    return VM_E_INVALID;
+  }
+  if (batch < 0 || rows < 0 || cols < 4 || cols > 2048 || cols % 4 || head < 0 || head > rows ||
+      groups < 1 || max_group_rows < 0 || in_batch_stride < (long long)rows * cols ||
+      in_batch_stride % 4 || !vmhost::dtype_ok(x_dtype) || !vmhost::dtype_ok(out_dtype) ||
+      (residual && !vmhost::dtype_ok(res_dtype)) ||
+      (!bounds && head + (long long)groups * group_rows != rows) ||
+      (!bounds && group_rows != max_group_rows)) {
+    vmhost::set_error("vm_norm_pool_fwd: bad shape/dtype (cols % 4 == 0, cols <= 2048; "
+                      "implicit groups must tile rows after the head)");
+    return VM_E_INVALID;
+  }
+  if (!vmhost::aligned16(x) || !vmhost::aligned16(out) || !vmhost::aligned16(weight) ||
+      (residual && !vmhost::aligned16(residual))) {
+    vmhost::set_error("vm_norm_pool_fwd: x, residual, out and weight must be 16-byte aligned");
+    return VM_E_INVALID;
+  }
+  const long long need = vm_norm_pool_workspace_bytes(batch, groups, max_group_rows, cols);
+  if (workspace && workspace_bytes < need) {
+    vmhost::set_error("vm_norm_pool_fwd: workspace smaller than vm_norm_pool_workspace_bytes");
+    return VM_E_INVALID;
+  }
+  if (batch == 0 || rows == 0) return VM_OK;
+  NormPoolParams p{};
+  p.x = x; p.res = residual; p.w = weight; p.bias = bias; p.out = out;
+  p.in_bstride = in_batch_stride; p.rows = rows; p.cols = cols; p.eps = eps; p.is_rms = is_rms;
+  p.x_dtype = x_dtype; p.res_dtype = res_dtype; p.out_dtype = out_dtype;
+  p.head = head; p.groups = groups; p.group_rows = group_rows; p.bounds = bounds;
+  p.slices = max_group_rows > 0 ? (max_group_rows + kPoolRB - 1) / kPoolRB : 1;
+  p.part = static_cast<float*>(workspace);
+  dim3 grid(p.slices, groups + 1, batch);
+  const size_t lds = 4 * cols * sizeof(float);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int cpl = (cols + 255) / 256;
+  if (cpl <= 1) hipLaunchKernelGGL(norm_pool_rows_kernel<1>, grid, dim3(256), lds, s, p);
+  else if (cpl <= 2) hipLaunchKernelGGL(norm_pool_rows_kernel<2>, grid, dim3(256), lds, s, p);
+  else if (cpl <= 4) hipLaunchKernelGGL(norm_pool_rows_kernel<4>, grid, dim3(256), lds, s, p);
+  else hipLaunchKernelGGL(norm_pool_rows_kernel<8>, grid, dim3(256), lds, s, p);
+  return vmhost::launch_status("vm_norm_pool_fwd");
+}
+
+extern "C" int vm_pool_finish_fwd(const void* workspace, int batch, int groups, int group_rows,
+                                  const int* bounds, int max_group_rows, const void* cls,
+                                  int cls_dtype, long long cls_batch_stride, int mode,
+                                  int keep_temporal, const float* ln_weight, const float* ln_bias,
+                                  float ln_eps, void* x_pool, int xp_dtype, int cols,
+                                  vm_stream_t stream) {
+  const bool needs_cls = mode == kPoolClsAvg || mode == kPoolClsCatAvg || mode == kPoolCls;
+  const bool needs_avg = mode != kPoolCls;
+  if (!x_pool || (needs_cls && !cls) || (needs_avg && !workspace)) {
+    vmhost::set_error("vm_pool_finish_fwd: null required pointer");
+    return VM_E_INVALID;
+  }
+  if (batch < 0 || groups < 1 || mode < 0 || mode > 3 || cols < 1 || cols > 2048 ||
+      max_group_rows < 1 || !vmhost::dtype_ok(xp_dtype) || (cls && !vmhost::dtype_ok(cls_dtype))) {
+    vmhost::set_error("vm_pool_finish_fwd: bad mode/shape/dtype");
+    return VM_E_INVALID;
+  }
+  if (batch == 0) return VM_OK;
+  PoolFinishParams p{};
+  p.part = static_cast<const float*>(workspace); p.groups = groups;
+  p.slices = (max_group_rows + kPoolRB - 1) / kPoolRB; p.group_rows = group_rows;
+  p.bounds = bounds; p.cls = cls; p.cls_bstride = cls_batch_stride; p.cls_dtype = cls_dtype;
+  p.mode = mode; p.keep_temporal = keep_temporal; p.lnw = ln_weight; p.lnb = ln_bias;
+  p.ln_eps = ln_eps; p.xpool = x_pool; p.xp_dtype = xp_dtype; p.cols = cols;
+  const int navg = keep_temporal ? groups : 1;
+  p.prow = mode == kPoolCls ? 1 : (mode == kPoolClsCatAvg ? 1 + navg : navg);
+  hipLaunchKernelGGL(pool_finish_kernel, dim3(p.prow, batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), p);
+  return vmhost::launch_status("vm_pool_finish_fwd");
+}
 
 extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
                                const float* weight, const float* bias, void* out, int out_dtype,

@@ -83,15 +83,18 @@ class StreamingChunkGraph:
     def _body(self, has_cls: bool):
         m = self.model
         offset = 0 if has_cls else 1  # only has_cls matters inside; tpos comes from the buffer
-        x_vis, new_state = m._forward_features(self.static_x, None, self._state, offset,
-                                               tpos=self.static_tpos)
+        pool = None
+        if m.add_pool_norm:
+            gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
+            pool = (False, self.tt, gh * gw)
+        feats, x_pool, new_state = m._encode(self.static_x, None, self._state, offset,
+                                             tpos=self.static_tpos, pool=pool)
         for (c, _), (c_new, _) in zip(self._state, new_state):
             if c_new.data_ptr() != c.data_ptr():
                 c.copy_(c_new)
-        if not m.add_pool_norm:
-            return (x_vis,)
-        gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
-        return m._pool(self.static_x, x_vis, None, False, has_cls, self.tt, gh * gw)
+        if pool is None:
+            return (feats,)
+        return (feats[:, 1:] if has_cls else feats), x_pool
 
     def _params_key(self):
         return tuple((t.data_ptr(), t._version, t.dtype, t.device)
@@ -105,6 +108,8 @@ class StreamingChunkGraph:
         L = self.tt * gh * gw + 1
         Lp = (L + 7) // 8 * 8
         need = max(max(K.scan_workspace_bytes(self.batch, mx.d_inner, L, mx.d_state),
+                       K.norm_pool_workspace_bytes(self.batch, 1, L, m.embed_dim),
+                       K.norm_pool_workspace_bytes(self.batch, self.tt, gh * gw, m.embed_dim),
                        K.conv_proj_cm_workspace_bytes(self.batch, Lp, mx.d_inner,
                                                       mx.dt_rank + 2 * mx.d_state)
                        if mx.d_inner % 64 == 0 else 0,
@@ -140,10 +145,8 @@ class StreamingChunkGraph:
                              f"{tuple(self.static_x.shape)}")
         m = self.model
         has_cls = temporal_pos_offset <= 0
-        if not has_cls and m.pool_type in {"cls", "cls+avg", "cls_cat_avg"} and m.add_pool_norm:
-            raise ValueError(
-                f"pool_type='{m.pool_type}' requires a CLS token, but continuation streaming "
-                "chunks do not include CLS. Use pool_type='avg' for chunked streaming.")
+        if m.add_pool_norm:
+            m._check_pool(has_cls)
         tpos = m._get_temporal_pos_embedding(self.tt, offset=temporal_pos_offset,
                                              dtype=self.dtype, device=self.device)
         self.static_tpos.copy_(tpos)

@@ -251,6 +251,64 @@ def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_r
     _lib.check(rc, "vm_add_norm_fwd")
 
 
+POOL_MODES = {"avg": 0, "cls+avg": 1, "cls_cat_avg": 2, "cls": 3}
+
+
+def norm_pool_workspace_bytes(batch: int, groups: int, max_group_rows: int, cols: int) -> int:
+    return int(_lib.load().vm_norm_pool_workspace_bytes(batch, groups, max_group_rows, cols))
+
+
+def norm_pool(h: Tensor, residual: Optional[Tensor], rows: int, w32: Tensor,
+              b32: Optional[Tensor], eps: float, is_rms: bool, *, head: int, groups: int,
+              group_rows: int = 0, bounds: Optional[Tensor] = None, max_group_rows: int = 0,
+              sums: bool = False, out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """Final add + norm of rows [0, rows) of the padded (B, Lp, C) ``h`` (+ ``residual``)
+    into a contiguous (B, rows, C) tensor; with ``sums`` also the per-group fp32 column
+    sums for :func:`pool_finish` (returned workspace, valid until the next scratch user
+    on this stream).  Groups: ``groups`` x ``group_rows`` rows after ``head`` rows, or
+    int32 ``bounds`` (B, groups+1)."""
+    Bsz, Lp, C = h.shape
+    if out is None:
+        out = torch.empty((Bsz, rows, C), dtype=h.dtype, device=h.device)
+    if bounds is None:
+        max_group_rows = group_rows
+    ws, nbytes = None, 0
+    if sums:
+        nbytes = norm_pool_workspace_bytes(Bsz, groups, max_group_rows, C)
+        ws = scratch(h.device, _stream(h), nbytes)
+    if residual is not None and residual.stride() != h.stride():
+        raise ValueError("residual must share h's padded layout")
+    rc = _lib.load().vm_norm_pool_fwd(
+        _p(h), dtype_code(h.dtype), _p(residual),
+        dtype_code(residual.dtype) if residual is not None else 0, h.stride(0),
+        _p(w32), _p(b32), float(eps), int(is_rms), _p(out), dtype_code(out.dtype),
+        Bsz, rows, C, head, groups, group_rows, _p(bounds), max_group_rows,
+        _p(ws), nbytes, _stream(h))
+    _lib.check(rc, "vm_norm_pool_fwd")
+    return out, ws
+
+
+def pool_finish(ws: Optional[Tensor], feats: Tensor, *, mode: str, keep_temporal: bool,
+                groups: int, group_rows: int = 0, bounds: Optional[Tensor] = None,
+                max_group_rows: int = 0, has_cls: bool, lnw32: Optional[Tensor],
+                lnb32: Optional[Tensor], ln_eps: float) -> Tensor:
+    """Pool tail over :func:`norm_pool`'s sums: means (per group with ``keep_temporal``),
+    the CLS add / concat of ``mode`` (CLS = row 0 of ``feats``) and the pool LayerNorm."""
+    Bsz, _, C = feats.shape
+    if bounds is None:
+        max_group_rows = group_rows
+    navg = groups if keep_temporal else 1
+    prow = {"cls": 1, "cls_cat_avg": 1 + navg}.get(mode, navg)
+    x_pool = torch.empty((Bsz, prow, C), dtype=feats.dtype, device=feats.device)
+    rc = _lib.load().vm_pool_finish_fwd(
+        _p(ws), Bsz, groups, group_rows, _p(bounds), max(1, max_group_rows),
+        _p(feats) if has_cls else None, dtype_code(feats.dtype), feats.stride(0),
+        POOL_MODES[mode], int(keep_temporal), _p(lnw32), _p(lnb32), float(ln_eps),
+        _p(x_pool), dtype_code(x_pool.dtype), C, _stream(feats))
+    _lib.check(rc, "vm_pool_finish_fwd")
+    return x_pool
+
+
 # --------------------------------------------------------------------------- selective scan
 def selective_scan_fn(u: Tensor, delta: Tensor, A: Tensor, B: Tensor, C: Tensor,
                       D: Optional[Tensor] = None, z: Optional[Tensor] = None,

@@ -9,7 +9,8 @@ initialisation, error types and messages: ``Block``, ``create_block``, ``PatchEm
 
     tubelet patch embed + pos adds (HIP, MFMA) -> [CLS row] -> optional mask gather
     per layer: fused residual-add + RMSNorm (HIP) -> Mamba mixer (HIP conv/scan + GEMMs)
-    final fused add + norm (HIP) -> pooling (small torch ops) -> (x_vis, x_pool[, state])
+    final add + norm fused with the pooling sums (HIP) -> pool tail + LayerNorm (HIP)
+    -> (x_vis, x_pool[, state])
 
 which is the same computation as calling ``Block.forward`` per layer on the unpadded
 tokens (``Block.forward`` itself is kept for callers that use blocks directly).
@@ -409,32 +410,22 @@ class PretrainVideoMamba(nn.Module):
         pos = pos.masked_fill(mask, token_count)
         return mask, torch.sort(pos, dim=1).values[:, :n_vis]
 
-    def _masked_temporal_average(self, patch_tokens, visible_positions, temporal_tokens,
-                                 tokens_per_frame, has_cls_token):
-        """Per-frame mean of the visible patch tokens (``videomamba.py:702-751``)."""
-        if patch_tokens.ndim != 3:
-            raise ValueError("patch_tokens must have shape [B, N, C].")
-        if visible_positions.ndim != 2:
-            raise ValueError("visible_positions must have shape [B, N_total_visible].")
-        if patch_tokens.shape[0] != visible_positions.shape[0]:
-            raise ValueError("Batch size mismatch between patch_tokens and visible_positions.")
-        if visible_positions.shape[1] != patch_tokens.shape[1] + (1 if has_cls_token else 0):
-            raise ValueError("visible_positions and patch_tokens lengths are inconsistent.")
-        if has_cls_token and visible_positions.numel() > 0 and \
-                not bool((visible_positions[:, 0] == 0).all()):
-            raise ValueError("mask must keep CLS token visible for temporal pooling.")
-        ppos = visible_positions[:, 1:] - 1 if has_cls_token else visible_positions
-        frame = torch.div(ppos, tokens_per_frame, rounding_mode="floor").long()
-        Bsz, n, C = patch_tokens.shape
-        sums = patch_tokens.new_zeros(Bsz, temporal_tokens, C)
-        sums.scatter_add_(1, frame.unsqueeze(-1).expand(-1, -1, C), patch_tokens)
-        counts = patch_tokens.new_zeros(Bsz, temporal_tokens, 1)
-        counts.scatter_add_(1, frame.unsqueeze(-1), patch_tokens.new_ones(Bsz, n, 1))
-        if bool((counts == 0).any()):
+    def _frame_bounds(self, visible_positions, temporal_tokens, tokens_per_frame,
+                      has_cls_token):
+        """Row bounds (B, T'+1) int32 of each frame's visible patch tokens in the gathered
+        order, plus the largest frame; the masked keep_temporal groups of
+        ``videomamba.py:702-751`` (positions are ascending, so a frame's tokens are
+        contiguous).  Raises the reference's ValueError when a frame has none."""
+        head = 1 if has_cls_token else 0
+        starts = head + torch.arange(temporal_tokens + 1, device=visible_positions.device,
+                                     dtype=visible_positions.dtype) * tokens_per_frame
+        bounds = torch.searchsorted(visible_positions.contiguous(),
+                                    starts.expand(visible_positions.shape[0], -1).contiguous())
+        counts = bounds[:, 1:] - bounds[:, :-1]
+        if counts.numel() and bool((counts == 0).any()):
             raise ValueError("keep_temporal with masking requires at least one visible patch "
                              "token for each temporal slice.")
-        return sums / counts
-
+        return bounds.to(torch.int32).contiguous(), int(counts.max().item())
 
     # ------------------------------------------------------------------ layer loop
     def _run_layers(self, h, residual, L, ssm_state):
@@ -459,15 +450,53 @@ class PretrainVideoMamba(nn.Module):
                 new_states[idx] = layer_state
         return h, residual, new_states, tuple_out
 
-    def _final_norm(self, h, residual, out=None):
+    def _final_norm_pool(self, h, residual, L, has_cls, visible, pool):
+        """Final add + norm of the padded buffer straight into contiguous (B, L, C)
+        features, fused with the pooling sums (``vm_norm_pool_fwd``), then the pool tail
+        (``vm_pool_finish_fwd``): (features, x_pool | None).  ``pool`` is None (no pooling)
+        or (keep_temporal, temporal_tokens, tokens_per_frame)."""
         nw, nb, eps = self.norm.weight, self.norm.bias, self.norm.eps
         is_rms = _norm_kind(self.norm)
-        if self.fused_add_norm:
-            return K._norm(self.drop_path(h), nw, nb, residual, False, self.residual_in_fp32,
-                           eps, is_rms, out=out, owner=self.norm)
-        residual = h if residual is None else residual + self.drop_path(h)
-        return K._norm(residual.to(nw.dtype), nw, nb, None, False, False, eps, is_rms, out=out,
-                       owner=self.norm)
+        C = self.embed_dim
+        if C % 4 or C > 2048:
+            raise NotImplementedError(f"embed_dim {C}: the HIP final norm takes C % 4 == 0, "
+                                      "C <= 2048")
+        if not self.fused_add_norm:  # ``:896-901``: add in the residual dtype, cast, norm
+            residual = h if residual is None else residual + self.drop_path(h)
+            h, residual = residual.to(nw.dtype).contiguous(), None
+        elif residual is not None and residual.dtype != h.dtype and not self.residual_in_fp32:
+            residual = residual.to(h.dtype)
+        w32, b32 = K.f32_cached(self.norm, nw, "w"), K.f32_cached(self.norm, nb, "b")
+        head = 1 if has_cls else 0
+        npatch = L - head
+        mode = self.pool_type
+        sums = pool is not None and mode != "cls"
+        groups, group_rows, bounds, max_rows = 1, npatch, None, npatch
+        if sums:
+            if npatch == 0:
+                raise ValueError("mask must keep at least one patch token visible when using "
+                                 f"pool_type='{mode}'.")
+            keep_temporal, tt, per_frame = pool
+            if keep_temporal:
+                if visible is None:
+                    groups, group_rows, max_rows = tt, per_frame, per_frame
+                else:
+                    bounds, max_rows = self._frame_bounds(visible, tt, per_frame, has_cls)
+                    groups, group_rows = tt, 0
+        feats, ws = K.norm_pool(h, residual, L, w32, b32, eps, is_rms, head=head,
+                                groups=groups, group_rows=group_rows, bounds=bounds,
+                                max_group_rows=max_rows, sums=sums)
+        if pool is None:
+            return feats, None
+        pn = self.pool_norm
+        if not isinstance(pn, nn.LayerNorm) or len(pn.normalized_shape) != 1:
+            raise NotImplementedError("pool_norm must be an nn.LayerNorm over the channels")
+        x_pool = K.pool_finish(ws, feats, mode=mode, keep_temporal=bool(pool[0]),
+                               groups=groups, group_rows=group_rows, bounds=bounds,
+                               max_group_rows=max_rows, has_cls=has_cls,
+                               lnw32=K.f32_cached(pn, pn.weight, "w"),
+                               lnb32=K.f32_cached(pn, pn.bias, "b"), ln_eps=pn.eps)
+        return feats, x_pool
 
     # ------------------------------------------------------------------ forward
     def _embed(self, x: Tensor, has_cls: bool, temporal_pos_offset: int, tpos=None):
@@ -506,6 +535,11 @@ class PretrainVideoMamba(nn.Module):
             return self._forward_features(x, mask, ssm_state, temporal_pos_offset)
 
     def _forward_features(self, x, mask, ssm_state, temporal_pos_offset, tpos=None):
+        feats, _, st = self._encode(x, mask, ssm_state, temporal_pos_offset, tpos=tpos)
+        return feats if ssm_state is None else (feats, st)
+
+    def _encode(self, x, mask, ssm_state, temporal_pos_offset, tpos=None, pool=None):
+        """(features (B, N_vis, C), x_pool | None, state result | None)."""
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
         h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset, tpos=tpos)
         Bsz = x.shape[0]
@@ -518,18 +552,19 @@ class PretrainVideoMamba(nn.Module):
             h[:, :L] = gathered
 
         h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state)
-        out = self._final_norm(h, residual)
-        x_vis = out[:, :L].contiguous()
+        feats, x_pool = self._final_norm_pool(h, residual, L, has_cls, visible, pool)
 
         if new_states is not None and isinstance(new_states, list):
             if any(s is None for s in new_states):
                 raise ValueError("Expected full state for all layers.")
-            return x_vis, (tuple(new_states) if tuple_out else new_states)
-        if ssm_state is None:
-            return x_vis
-        if new_states is not None:
-            return x_vis, new_states
-        return x_vis, ssm_state
+            st = tuple(new_states) if tuple_out else new_states
+        elif ssm_state is None:
+            st = None
+        elif new_states is not None:
+            st = new_states
+        else:
+            st = ssm_state
+        return feats, x_pool, st
 
     def forward(self, x: Tensor, mask: Optional[Tensor] = None, use_image: bool = False,
                 keep_temporal: bool = False, ssm_state: Optional[StateCollection] = None,
@@ -542,54 +577,28 @@ class PretrainVideoMamba(nn.Module):
         per_frame = gh * gw
         temporal_tokens = self._validate_temporal_length(x.shape[2])
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
-        feats = self.forward_features(x, mask, use_image, ssm_state=ssm_state,
-                                      temporal_pos_offset=temporal_pos_offset)
-        if ssm_state is None:
-            x_vis = feats
-        else:
-            x_vis, ssm_state = feats
         if not self.add_pool_norm:
-            return x_vis if ssm_state is None else (x_vis, ssm_state)
+            return self.forward_features(x, mask, use_image, ssm_state=ssm_state,
+                                         temporal_pos_offset=temporal_pos_offset)
+        self._check_pool(has_cls)
+        K.require_gpu(x, what="VideoMamba")
+        warn_if_grad(x, self.patch_embed.proj.weight)
         with torch.no_grad():
-            x_vis, x_pool = self._pool(x, x_vis, mask, keep_temporal, has_cls, temporal_tokens,
-                                       per_frame)
-        return (x_vis, x_pool) if ssm_state is None else (x_vis, x_pool, ssm_state)
+            feats, x_pool, st = self._encode(x, mask, ssm_state, temporal_pos_offset,
+                                             pool=(bool(keep_temporal), temporal_tokens,
+                                                   per_frame))
+        patch = feats[:, 1:] if has_cls else feats
+        return (patch, x_pool) if ssm_state is None else (patch, x_pool, st)
 
-    def _pool(self, x, x_vis, mask, keep_temporal, has_cls, temporal_tokens, per_frame):
-        cls_tok = x_vis[:, :1] if has_cls else None
-        patch = x_vis[:, 1:] if has_cls else x_vis
+    def _check_pool(self, has_cls: bool) -> None:
         pool = self.pool_type
-        if pool in {"cls", "cls+avg", "cls_cat_avg"} and cls_tok is None:
+        if pool not in K.POOL_MODES:
+            raise ValueError(f"Unsupported pool_type: {pool}")
+        if pool in {"cls", "cls+avg", "cls_cat_avg"} and not has_cls:
             raise ValueError(
                 f"pool_type='{pool}' requires a CLS token, but continuation "
                 "streaming chunks (temporal_pos_offset > 0 with full state) do not include CLS. "
                 "Use pool_type='avg' for chunked streaming.")
-        if pool != "cls" and patch.shape[1] == 0:
-            raise ValueError("mask must keep at least one patch token visible when using "
-                             f"pool_type='{pool}'.")
-        if pool == "cls":
-            return patch, self.pool_norm(cls_tok)
-        if keep_temporal:
-            Bsz, _, C = patch.shape
-            if mask is None:
-                avg = patch.reshape(Bsz, temporal_tokens, per_frame, C).mean(2)
-            else:
-                full = (1 if has_cls else 0) + temporal_tokens * per_frame
-                _, vis = self._visible_token_positions(mask, Bsz, full, x.device,
-                                                       require_cls_visible=has_cls)
-                avg = self._masked_temporal_average(patch, vis, temporal_tokens, per_frame,
-                                                    has_cls)
-        else:
-            avg = patch.mean(1, keepdim=True)
-        if pool == "cls+avg":
-            pooled = self.pool_norm(cls_tok + avg)
-        elif pool == "cls_cat_avg":
-            pooled = self.pool_norm(torch.cat([cls_tok, avg], dim=1))
-        elif pool == "avg":
-            pooled = self.pool_norm(avg)
-        else:
-            raise ValueError(f"Unsupported pool_type: {pool}")
-        return patch, pooled
 
 
 # ----------------------------------------------------------------------------- loading
