@@ -9,6 +9,8 @@
  *                                 (models/videomamba/mamba_simple.py:122-152, stateless and
  *                                  initial_state forms; also replaces the per-token
  *                                  selective_state_update loop at :153-172)
+ *   vm_selective_scan_bidir_fwd <- the forward + flipped backward scans of
+ *                                 BiMambaRefinerBlock (models/refiner_backbone.py:98-135)
  *   vm_selective_state_update  <- mamba_ssm selective_state_update  (mamba_simple.py:483-494)
  *   vm_causal_conv1d_fwd       <- causal_conv1d_fn (+ conv_state prepend)
  *                                 (mamba_simple.py:381-404)
@@ -94,6 +96,35 @@ int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd, long lo
                           int out_len, int batch, int dim, int seqlen, int dstate, int dtype,
                           int segments, void* workspace, long long workspace_bytes,
                           vm_stream_t stream);
+
+/*
+ * Both directions of a bidirectional block in one scan (BiMambaRefinerBlock,
+ * models/refiner_backbone.py:98-135, whose backward block scans torch.flip of the
+ * sequence).  Arguments as vm_selective_scan_fwd over batch = 2*split rows on token-major
+ * operands: rows [0, split) scan forward with (A, D, delta_bias, h0, h_last); rows
+ * [split, 2*split) hold the backward direction's operands already in flipped step order
+ * and use (A_bwd, D_bwd, delta_bias_bwd, h0_bwd, h_last_bwd) (state row b - split, same
+ * dtypes / strides), and their step t output is stored at the un-flipped row
+ * t + (L - F) - 2F*floor(t/F), F = frame_len (1 = plain time reversal; the frame size
+ * reverses frame order and keeps token order within a frame).  Needs dstate == 16 with
+ * unit state stride and, when the cost model segments the sequence, the
+ * vm_selective_scan_workspace_bytes(batch, ...) workspace.
+ */
+int vm_selective_scan_bidir_fwd(
+    const void* u, long long u_sb, long long u_sd, long long u_sl,
+    const void* delta, long long dl_sb, long long dl_sd, long long dl_sl,
+    const float* A,
+    const void* B, long long b_sb, long long b_sn, long long b_sl,
+    const void* C, long long c_sb, long long c_sn, long long c_sl,
+    const float* D, const void* z, long long z_sb, long long z_sd, long long z_sl,
+    const float* delta_bias, int delta_softplus,
+    const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
+    void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
+    void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
+    int batch, int dim, int seqlen, int dstate, int dtype,
+    int split, const float* A_bwd, const float* D_bwd, const float* delta_bias_bwd,
+    const void* h0_bwd, void* h_last_bwd, int frame_len,
+    int segments, void* workspace, long long workspace_bytes, vm_stream_t stream);
 
 /* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape and
  * segment request (0 = the cost model's choice). */
@@ -214,8 +245,10 @@ int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dt
 
 /*
  * Final add + norm fused with the pooling front half.  Per batch row b, rows
- * [0, rows) of x (+ residual) at x + b*in_batch_stride are normalised into the
- * contiguous out (batch, rows, cols).  Rows [0, head) (the CLS row) are only normalised;
+ * [0, rows) of x (+ residual) at x + b*in_batch_stride are normalised into out + b *
+ * out_batch_stride (rows contiguous).  rev_frame > 0 reads rows [head, rows) in reversed
+ * frame order (frames of rev_frame rows, row order kept within a frame): the flipped
+ * input of BiMambaRefinerBlock's backward block (models/refiner_backbone.py:98-135).  Rows [0, head) (the CLS row) are only normalised;
  * rows [head, rows) form `groups` pooling groups: equal groups of `group_rows` rows when
  * bounds == NULL (head + groups*group_rows == rows, max_group_rows == group_rows), else
  * bounds (batch, groups+1) int32 row bounds with bounds[b][0] == head and
@@ -227,9 +260,10 @@ int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dt
 long long vm_norm_pool_workspace_bytes(int batch, int groups, int max_group_rows, int cols);
 int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
                      long long in_batch_stride, const float* weight, const float* bias,
-                     float eps, int is_rms, void* out, int out_dtype, int batch, int rows,
-                     int cols, int head, int groups, int group_rows, const int* bounds,
-                     int max_group_rows, void* workspace, long long workspace_bytes,
+                     float eps, int is_rms, void* out, int out_dtype,
+                     long long out_batch_stride, int batch, int rows, int cols, int head,
+                     int groups, int group_rows, const int* bounds, int max_group_rows,
+                     int rev_frame, void* workspace, long long workspace_bytes,
                      vm_stream_t stream);
 
 /*

@@ -43,6 +43,12 @@ _SIGNATURES = {
          _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
          _I, _P, _LL,             # segments, workspace, workspace_bytes
          _P], _I),
+    "vm_selective_scan_bidir_fwd": (
+        [_P, _LL, _LL, _LL, _P, _LL, _LL, _LL, _P, _P, _LL, _LL, _LL, _P, _LL, _LL, _LL,
+         _P, _P, _LL, _LL, _LL, _P, _I, _P, _I, _LL, _LL, _P, _I, _LL, _LL,
+         _P, _LL, _LL, _LL, _I, _I, _I, _I, _I, _I,
+         _I, _P, _P, _P, _P, _P, _I,              # split, A/D/bias/h0/h_last bwd, frame_len
+         _I, _P, _LL, _P], _I),
     "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_state_update": (
         [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
@@ -75,8 +81,8 @@ _SIGNATURES = {
     "vm_norm_pool_fwd": (
         [_P, _I, _P, _I, _LL,                     # x, residual, batch stride
          _P, _P, c_float, _I,                     # weight, bias, eps, is_rms
-         _P, _I, _I, _I, _I,                      # out, out dtype, batch, rows, cols
-         _I, _I, _I, _P, _I,                      # head, groups, group_rows, bounds, max rows
+         _P, _I, _LL, _I, _I, _I,                 # out, dtype, batch stride, batch, rows, cols
+         _I, _I, _I, _P, _I, _I,                  # head, groups, rows, bounds, max, rev_frame
          _P, _LL, _P], _I),
     "vm_pool_finish_fwd": (
         [_P, _I, _I, _I, _P, _I,                  # workspace, batch, groups, rows, bounds, max

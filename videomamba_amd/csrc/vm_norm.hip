@@ -174,7 +174,9 @@ constexpr int kPoolRB = 16;
 struct NormPoolParams {
   const void* x; const void* res; const float* w; const float* bias; void* out;
   long long in_bstride;             // elements between batch rows of x / res (padded L * cols)
+  long long out_bstride;            // elements between batch rows of out
   int rows, cols; float eps; int is_rms, x_dtype, res_dtype, out_dtype;
+  int rev_frame;                    // > 0: grouped rows read in reversed frame order
   int head, groups, group_rows;     // implicit equal groups when bounds == nullptr
   const int* bounds;                // (batch, groups + 1) row bounds or nullptr
   int slices;                       // kPoolRB-row slices per group
@@ -205,8 +207,13 @@ __global__ __launch_bounds__(256) void norm_pool_rows_kernel(const NormPoolParam
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = 0.0f;
   for (int r = r0 + wave; r < r1; r += 4) {
-    const long long in = (long long)b * p.in_bstride + (long long)r * p.cols;
-    const long long on = ((long long)b * p.rows + r) * p.cols;
+    int ri = r;  // input row: frame-order reversal of the grouped rows (BiMamba backward)
+    if (p.rev_frame > 0 && r >= p.head) {
+      const int x = r - p.head, F = p.rev_frame;
+      ri = p.head + x + (p.rows - p.head - F) - 2 * F * (x / F);
+    }
+    const long long in = (long long)b * p.in_bstride + (long long)ri * p.cols;
+    const long long on = (long long)b * p.out_bstride + (long long)r * p.cols;
     float v[CPL][4];
     float sum = 0.0f;
 #pragma unroll
@@ -371,9 +378,10 @@ extern "C" long long vm_norm_pool_workspace_bytes(int batch, int groups, int max
 
 extern "C" int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual, int res_dtype,
                                 long long in_batch_stride, const float* weight, const float* bias,
-                                float eps, int is_rms, void* out, int out_dtype, int batch,
-                                int rows, int cols, int head, int groups, int group_rows,
-                                const int* bounds, int max_group_rows, void* workspace,
+                                float eps, int is_rms, void* out, int out_dtype,
+                                long long out_batch_stride, int batch, int rows, int cols,
+                                int head, int groups, int group_rows, const int* bounds,
+                                int max_group_rows, int rev_frame, void* workspace,
                                 long long workspace_bytes, vm_stream_t stream) {
   if (!x || !weight || !out) {
     vmhost::set_error("vm_norm_pool_fwd: null required pointer");
@@ -381,7 +389,9 @@ extern "C" int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual
   }
   if (batch < 0 || rows < 0 || cols < 4 || cols > 2048 || cols % 4 || head < 0 || head > rows ||
       groups < 1 || max_group_rows < 0 || in_batch_stride < (long long)rows * cols ||
-      in_batch_stride % 4 || !vmhost::dtype_ok(x_dtype) || !vmhost::dtype_ok(out_dtype) ||
+      in_batch_stride % 4 || out_batch_stride < (long long)rows * cols || out_batch_stride % 4 ||
+      rev_frame < 0 || (rev_frame > 0 && (rows - head) % rev_frame) ||
+      !vmhost::dtype_ok(x_dtype) || !vmhost::dtype_ok(out_dtype) ||
       (residual && !vmhost::dtype_ok(res_dtype)) ||
       (!bounds && head + (long long)groups * group_rows != rows) ||
       (!bounds && group_rows != max_group_rows)) {
@@ -402,7 +412,8 @@ extern "C" int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual
   if (batch == 0 || rows == 0) return VM_OK;
   NormPoolParams p{};
   p.x = x; p.res = residual; p.w = weight; p.bias = bias; p.out = out;
-  p.in_bstride = in_batch_stride; p.rows = rows; p.cols = cols; p.eps = eps; p.is_rms = is_rms;
+  p.in_bstride = in_batch_stride; p.out_bstride = out_batch_stride; p.rev_frame = rev_frame;
+  p.rows = rows; p.cols = cols; p.eps = eps; p.is_rms = is_rms;
   p.x_dtype = x_dtype; p.res_dtype = res_dtype; p.out_dtype = out_dtype;
   p.head = head; p.groups = groups; p.group_rows = group_rows; p.bounds = bounds;
   p.slices = max_group_rows > 0 ? (max_group_rows + kPoolRB - 1) / kPoolRB : 1;

@@ -21,7 +21,33 @@ struct ScanParams {
   int batch, dim, seqlen, out_len, dstate, softplus, h0_dtype, hl_dtype;
   int vec_x;   // u/delta/z/out rows allow 8-element vector access
   int vec_bc;  // B/C rows allow 8-element vector access
+  // Paired scan (vm_selective_scan_bidir_fwd): batch rows b >= split take A_hi / D_hi /
+  // dbias_hi and store step t's output at row ro_c0 + ro_s*t - ro_c1*umulhi(t, ro_m), the
+  // frame-order reversal.  split == batch for a plain scan.
+  // Their entry / last states are h0_hi / hl_hi at row b - split (same dtypes and strides).
+  int split;
+  const float* A_hi; const float* D_hi; const float* dbias_hi;
+  const void* h0_hi; void* hl_hi;
+  int ro_c0, ro_s, ro_c1; unsigned ro_m;
 };
+
+// Parameter set of batch row b (uniform per workgroup).  PAIR = false folds to the plain
+// scan's (p.A, p.D, p.dbias, identity row map) at compile time.
+struct PairSel {
+  const float* A; const float* D; const float* dbias;
+  const void* h0; void* hl; int hb;  // state pointers and the state row of this batch row
+  int c0, s, c1; unsigned m;
+  __device__ __forceinline__ int orow(int t) const {
+    return c0 + s * t - c1 * static_cast<int>(__umulhi(static_cast<unsigned>(t), m));
+  }
+};
+template <bool PAIR>
+__device__ __forceinline__ PairSel pair_sel(const ScanParams& p, int b) {
+  if (PAIR && b >= p.split)
+    return {p.A_hi, p.D_hi, p.dbias_hi, p.h0_hi, p.hl_hi, b - p.split,
+            p.ro_c0, p.ro_s, p.ro_c1, p.ro_m};
+  return {p.A, p.D, p.dbias, p.h0, p.hl, b, 0, 1, 0, 0u};
+}
 
 
 // Token-major path (vm_scan_seq.hip).  Workspace for the time-segmented form, in bytes;
@@ -33,5 +59,7 @@ size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* ch
 bool seq_supported(const ScanParams& p, int dtype);
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
                 size_t workspace_bytes, hipStream_t s);
+// Paired scans need the scalar-B/C kernels and, when segmented, the chunked form.
+bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes);
 
 }  // namespace vm

@@ -459,7 +459,16 @@ static void dispatch_scan(const ScanParams& p, hipStream_t s) {
 
 using namespace vm;
 
-extern "C" int vm_selective_scan_fwd(
+namespace {
+// Second parameter set of a paired (bidirectional) scan; nullptr for a plain scan.
+struct PairArgs {
+  int split; const float* A; const float* D; const float* dbias; const void* h0; void* hl;
+  int frame_len;
+};
+}  // namespace
+
+static int scan_entry(
+    const char* name,
     const void* u, long long u_sb, long long u_sd, long long u_sl,
     const void* delta, long long dl_sb, long long dl_sd, long long dl_sl,
     const float* A,
@@ -470,20 +479,20 @@ extern "C" int vm_selective_scan_fwd(
     const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
     void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
-    int batch, int dim, int seqlen, int dstate, int dtype,
+    int batch, int dim, int seqlen, int dstate, int dtype, const PairArgs* pair,
     int segments, void* workspace, long long workspace_bytes, vm_stream_t stream) {
   if (!u || !delta || !A || !B || !C || !out) {
-    vmhost::set_error("vm_selective_scan_fwd: null required pointer");
+    vmhost::set_error("%s: null required pointer", name);
     return VM_E_INVALID;
   }
   if (batch < 0 || dim < 0 || seqlen < 0 || out_len < seqlen || dstate < 1 || dstate > kMaxN) {
-    vmhost::set_error("vm_selective_scan_fwd: bad shape batch=%d dim=%d seqlen=%d dstate=%d "
-                      "(dstate must be in [1, %d])", batch, dim, seqlen, dstate, kMaxN);
+    vmhost::set_error("%s: bad shape batch=%d dim=%d seqlen=%d dstate=%d "
+                      "(dstate must be in [1, %d])", name, batch, dim, seqlen, dstate, kMaxN);
     return VM_E_INVALID;
   }
   if (!vmhost::dtype_ok(dtype) || (h0 && !vmhost::dtype_ok(h0_dtype)) ||
       (h_last && !vmhost::dtype_ok(hl_dtype))) {
-    vmhost::set_error("vm_selective_scan_fwd: unsupported dtype");
+    vmhost::set_error("%s: unsupported dtype", name);
     return VM_E_INVALID;
   }
   if (batch == 0 || dim == 0) return VM_OK;
@@ -497,17 +506,42 @@ extern "C" int vm_selective_scan_fwd(
   p.h0_sb = h0_sb; p.h0_sd = h0_sd; p.hl_sb = hl_sb; p.hl_sd = hl_sd;
   p.batch = batch; p.dim = dim; p.seqlen = seqlen; p.out_len = out_len; p.dstate = dstate;
   p.softplus = delta_softplus; p.h0_dtype = h0_dtype; p.hl_dtype = hl_dtype;
+  p.split = batch;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t ws_bytes = workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0;
+  if (pair) {
+    const int F = pair->frame_len;
+    if (!pair->A || pair->split * 2 != batch || F < 1 || seqlen % F ||
+        static_cast<long long>(seqlen) * F >= (1ll << 31)) {
+      vmhost::set_error("%s: need batch == 2*split, A_bwd, and frame_len dividing seqlen", name);
+      return VM_E_INVALID;
+    }
+    if (!seq_supported(p, dtype) || !seq_pair_supported(p, dtype, segments, workspace ? ws_bytes : 0)) {
+      vmhost::set_error("%s: paired scans take token-major operands with 16 unit-stride states "
+                        "and, when segmented, the vm_selective_scan_workspace_bytes workspace",
+                        name);
+      return VM_E_INVALID;
+    }
+    p.split = pair->split; p.A_hi = pair->A; p.D_hi = pair->D; p.dbias_hi = pair->dbias;
+    p.h0_hi = pair->h0; p.hl_hi = pair->hl;
+    // output row of step t: t + (L - F) - 2F floor(t / F) (reversed frame order, tokens
+    // within a frame in order); floor by a reciprocal multiply, exact for L*F < 2^32
+    if (F == 1) {
+      p.ro_c0 = seqlen - 1; p.ro_s = -1; p.ro_c1 = 0; p.ro_m = 0u;
+    } else {
+      p.ro_c0 = seqlen - F; p.ro_s = 1; p.ro_c1 = 2 * F;
+      p.ro_m = static_cast<unsigned>(0xffffffffu / static_cast<unsigned>(F)) + 1u;
+    }
+  }
   // Token-major operands (channel stride 1): channel-per-lane sequential kernels.
   if (seq_supported(p, dtype)) {
-    seq_launch(p, dtype, segments, workspace,
-               workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0, s);
-    return vmhost::launch_status("vm_selective_scan_fwd");
+    seq_launch(p, dtype, segments, workspace, ws_bytes, s);
+    return vmhost::launch_status(name);
   }
   // Channel-major operands (step stride 1): time-parallel kernels.
   if (u_sl != 1 || dl_sl != 1 || b_sl != 1 || c_sl != 1 || o_sl != 1 || (z && z_sl != 1)) {
-    vmhost::set_error("vm_selective_scan_fwd: operands must have a unit channel stride "
-                      "(u/delta/z/out) or a unit step stride (all operands)");
+    vmhost::set_error("%s: operands must have a unit channel stride "
+                      "(u/delta/z/out) or a unit step stride (all operands)", name);
     return VM_E_INVALID;
   }
   const long long m = dtype == VM_DTYPE_BF16 ? 8 : 4;  // elements per 16 bytes
@@ -520,8 +554,42 @@ extern "C" int vm_selective_scan_fwd(
   // seqlen == 0 still launches: the block loop is empty and h_last receives h0 (or 0).
   if (dtype == VM_DTYPE_BF16) dispatch_scan<bf16_t>(p, s);
   else dispatch_scan<float>(p, s);
-  return vmhost::launch_status("vm_selective_scan_fwd");
+  return vmhost::launch_status(name);
 }
+
+#define VM_SCAN_ARGS                                                                  \
+  const void *u, long long u_sb, long long u_sd, long long u_sl, const void *delta,   \
+      long long dl_sb, long long dl_sd, long long dl_sl, const float *A, const void *B, \
+      long long b_sb, long long b_sn, long long b_sl, const void *C, long long c_sb,     \
+      long long c_sn, long long c_sl, const float *D, const void *z, long long z_sb,     \
+      long long z_sd, long long z_sl, const float *delta_bias, int delta_softplus,       \
+      const void *h0, int h0_dtype, long long h0_sb, long long h0_sd, void *h_last,      \
+      int hl_dtype, long long hl_sb, long long hl_sd, void *out, long long o_sb,         \
+      long long o_sd, long long o_sl, int out_len, int batch, int dim, int seqlen,       \
+      int dstate, int dtype
+#define VM_SCAN_PASS                                                                  \
+  u, u_sb, u_sd, u_sl, delta, dl_sb, dl_sd, dl_sl, A, B, b_sb, b_sn, b_sl, C, c_sb, c_sn, \
+      c_sl, D, z, z_sb, z_sd, z_sl, delta_bias, delta_softplus, h0, h0_dtype, h0_sb,      \
+      h0_sd, h_last, hl_dtype, hl_sb, hl_sd, out, o_sb, o_sd, o_sl, out_len, batch, dim,  \
+      seqlen, dstate, dtype
+
+extern "C" int vm_selective_scan_fwd(VM_SCAN_ARGS, int segments, void* workspace,
+                                     long long workspace_bytes, vm_stream_t stream) {
+  return scan_entry("vm_selective_scan_fwd", VM_SCAN_PASS, nullptr, segments, workspace,
+                    workspace_bytes, stream);
+}
+
+extern "C" int vm_selective_scan_bidir_fwd(VM_SCAN_ARGS, int split, const float* A_bwd,
+                                           const float* D_bwd, const float* delta_bias_bwd,
+                                           const void* h0_bwd, void* h_last_bwd, int frame_len,
+                                           int segments, void* workspace,
+                                           long long workspace_bytes, vm_stream_t stream) {
+  const PairArgs pair{split, A_bwd, D_bwd, delta_bias_bwd, h0_bwd, h_last_bwd, frame_len};
+  return scan_entry("vm_selective_scan_bidir_fwd", VM_SCAN_PASS, &pair, segments, workspace,
+                    workspace_bytes, stream);
+}
+#undef VM_SCAN_ARGS
+#undef VM_SCAN_PASS
 
 extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen,
                                                        int dstate, int segments) {

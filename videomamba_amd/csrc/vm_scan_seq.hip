@@ -78,7 +78,8 @@ __device__ __forceinline__ float raw_f32(uint32_t r) {
 // pairs — leaving the 16 v_exp_f32 unpaired.  Measured in the step mix
 // (tools/probes/pk_rate.hip) a pair costs ~4.7 cycles per packed op against ~3.6 per
 // scalar op in dependent chains, so the step drops from ~343 to ~265 cycles per wave.
-template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB, bool PK, bool BC1 = false>
+template <typename T, int NW, int MODE, bool SP, bool HZ, bool SB, bool PK, bool BC1 = false,
+          bool PAIR = false>
 __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, const SeqWork w) {
   static_assert(!PK || SB, "packed pairs take B/C from SGPR pairs");
   static_assert(NW * 64 >= 4 * kTS, "B/C staging needs 4 threads per block step");
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const int L = p.seqlen;
   const int t_beg = seg * w.seg_len;
   const int t_end = min(L, t_beg + w.seg_len);
+  const PairSel ps = pair_sel<PAIR>(p, b);
   const long long ws_row = (static_cast<long long>(b) * w.S + seg) * p.dim + d;
 
   // LG (single pass with softplus): delta is carried in log2 units, dl' = softplus(x)*log2e
@@ -113,11 +115,11 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   f2 A2[kMaxN / 2], h[kMaxN / 2];
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) {
-    const float a = n < N ? p.A[d * N + n] * (LG ? 1.0f : kLog2e) : 0.0f;
+    const float a = n < N ? ps.A[d * N + n] * (LG ? 1.0f : kLog2e) : 0.0f;
     float h_init = 0.0f;
     if constexpr (MODE == 0) {
-      if (n < N && p.h0)
-        h_init = load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * lg_in;
+      if (n < N && ps.h0)
+        h_init = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * lg_in;
     }
     if constexpr (MODE == 2) h_init = w.hin[ws_row * kMaxN + n];
     if (n & 1) {
@@ -128,8 +130,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       h[n >> 1].x = h_init;
     }
   }
-  const float Dv = (p.D ? p.D[d] : 0.0f) * lg_in;
-  const float bias = (p.dbias ? p.dbias[d] : 0.0f) * lg_in;
+  const float Dv = (ps.D ? ps.D[d] : 0.0f) * lg_in;
+  const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * lg_in;
   // Wave-uniform row bases (buffer descriptors) + the lane's channel byte offset.
   const int d0 = __builtin_amdgcn_readfirstlane((blockIdx.x * NW + wave) * 64 < p.dim
                                                     ? (blockIdx.x * NW + wave) * 64
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         } else {
           const f2 ys = ya + yb;
           const float y = gate(ys.x + ys.y);
-          bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+          bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
         }
         return;
       }
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         const float y = gate(y0 + y1);
         // unconditional store (a branch here makes the loop-carried vmcnt accounting
         // conservative): dead lanes / steps get an out-of-range voffset instead
-        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
       }
   };
 
@@ -429,11 +431,11 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
     }
   } else {
     if (t_end >= L && active) {  // the segment that ends the sequence
-      if (p.hl) {
+      if (ps.hl) {
 #pragma unroll
         for (int n = 0; n < kMaxN; ++n)
           if (n < N)
-            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
+            store_dyn(ps.hl, ps.hb * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
                       ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * (LG ? kLn2f : 1.0f));
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
@@ -468,7 +470,7 @@ struct ChunkWork {
   int nblk;     // blocks per sequence
 };
 
-template <typename T, int PASS, bool SP, bool HZ, bool BC1>
+template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>
 __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w) {
   typedef __attribute__((address_space(4))) const uint32_t* cptr;
   constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
@@ -490,19 +492,20 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const long long D = p.dim;
   const long long rowE = ((static_cast<long long>(b) * w.nblk + blk) * kChW) * D;  // + j*D + d
   const long long rowA = (static_cast<long long>(b) * w.nblk) * D;                  // + k*D + d
+  const PairSel ps = pair_sel<PAIR>(p, b);
 
   f2 A2[kMaxN / 2], h[kMaxN / 2];
 #pragma unroll
   for (int q = 0; q < kMaxN / 2; ++q) {
-    A2[q] = f2{2 * q < N ? p.A[d * N + 2 * q] : 0.0f, 2 * q + 1 < N ? p.A[d * N + 2 * q + 1] : 0.0f};
+    A2[q] = f2{2 * q < N ? ps.A[d * N + 2 * q] : 0.0f, 2 * q + 1 < N ? ps.A[d * N + 2 * q + 1] : 0.0f};
     h[q] = f2{0.0f, 0.0f};
   }
-  const float Dv = (p.D ? p.D[d] : 0.0f) * kLog2e;
-  const float bias = (p.dbias ? p.dbias[d] : 0.0f) * kLog2e;
+  const float Dv = (ps.D ? ps.D[d] : 0.0f) * kLog2e;
+  const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * kLog2e;
   // states this wave composes across segments / blocks: 2 * wave, 2 * wave + 1
   const int n0 = 2 * wave;
-  const float An0 = n0 < N ? p.A[d * N + n0] : 0.0f;
-  const float An1 = n0 + 1 < N ? p.A[d * N + n0 + 1] : 0.0f;
+  const float An0 = n0 < N ? ps.A[d * N + n0] : 0.0f;
+  const float An1 = n0 + 1 < N ? ps.A[d * N + n0 + 1] : 0.0f;
 
   // PASS 2 entry operands: loaded together with everything else below, combined after
   // the one wait (every global load of the wave's start-up is a single round trip)
@@ -650,7 +653,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
                                fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
                : y * kLn2f;
-        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, t * os);
+        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
       }
     }
   }
@@ -682,11 +685,11 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     }
   } else {
     if (t_beg <= tlast && tlast < t_end && active && L > 0) {  // the segment that ends the sequence
-      if (p.hl) {
+      if (ps.hl) {
 #pragma unroll
         for (int n = 0; n < kMaxN; ++n)
           if (n < N)
-            store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
+            store_dyn(ps.hl, ps.hb * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
                       ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * kLn2f);
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
@@ -705,8 +708,12 @@ __global__ __launch_bounds__(256) void scan_chunk_carry_kernel(const ScanParams 
   const int d = static_cast<int>(bd % p.dim);
   const int b = static_cast<int>(bd / p.dim);
   const int N = p.dstate;
-  const float A = n < N ? p.A[d * N + n] : 0.0f;
-  float H = (n < N && p.h0) ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * kLog2e : 0.0f;
+  const bool hi = b >= p.split;  // second parameter set of a paired scan
+  const float* Ap = hi ? p.A_hi : p.A;
+  const void* h0 = hi ? p.h0_hi : p.h0;
+  const int hb = hi ? b - p.split : b;
+  const float A = n < N ? Ap[d * N + n] : 0.0f;
+  float H = (n < N && h0) ? load_dyn(h0, hb * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * kLog2e : 0.0f;
   const long long D = p.dim;
   const long long row0 = static_cast<long long>(b) * w.nblk * D + d;  // + k * D
   constexpr int kWin = 32;  // typically all blocks in one round of loads
@@ -783,10 +790,21 @@ template <typename T, int MODE, bool SP, bool HZ>
 static void launch_seq_mode(const ScanParams& p, const SeqWork& w, int segs, hipStream_t s) {
   const int groups = (p.dim + 63) / 64;
   dim3 grid((groups + kSeqNW - 1) / kSeqNW, segs, p.batch);
+  const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
+                   static_cast<const T*>(p.C) == static_cast<const T*>(p.B) + kMaxN;
+  if constexpr (MODE == 0) {
+    if (p.split < p.batch) {  // paired: scalar B/C single pass only (seq_pair_supported)
+      if (bc1)
+        hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, 0, SP, HZ, true, true, true, true>), grid,
+                           dim3(64 * kSeqNW), 0, s, p, w);
+      else
+        hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, 0, SP, HZ, true, true, false, true>),
+                           grid, dim3(64 * kSeqNW), 0, s, p, w);
+      return;
+    }
+  }
   if (seq_sgpr_bc(p, sizeof(T))) {
     // BC1: C directly follows B in one row (the mixer's x_dbl): one scalar load for both
-    const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
-                     static_cast<const T*>(p.C) == static_cast<const T*>(p.B) + kMaxN;
     if (bc1)
       hipLaunchKernelGGL((scan_seq_kernel<T, kSeqNW, MODE, SP, HZ, true, true, true>), grid,
                          dim3(64 * kSeqNW), 0, s, p, w);
@@ -886,14 +904,22 @@ bool seq_supported(const ScanParams& p, int dtype) {
          (p.z == nullptr || fits(p.z_sl));
 }
 
-template <typename T, bool SP, bool HZ, bool BC1>
-static void launch_chunk_t(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
+template <typename T, bool SP, bool HZ, bool BC1, bool PAIR>
+static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
-  hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1>), grid, dim3(64 * kChW), 0, s, p, w);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
+                     p, w);
   const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
   hipLaunchKernelGGL(scan_chunk_carry_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
                      dim3(256), 0, s, p, w);
-  hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1>), grid, dim3(64 * kChW), 0, s, p, w);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
+                     p, w);
+}
+
+template <typename T, bool SP, bool HZ, bool BC1>
+static void launch_chunk_t(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
+  if (p.split < p.batch) launch_chunk_p<T, SP, HZ, BC1, true>(p, w, s);
+  else launch_chunk_p<T, SP, HZ, BC1, false>(p, w, s);
 }
 
 template <typename T>
@@ -910,6 +936,12 @@ static void launch_chunk(const ScanParams& p, const ChunkWork& w, hipStream_t s)
     if (hz) { VM_CH(false, true) } else { VM_CH(false, false) }
   }
 #undef VM_CH
+}
+
+bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes) {
+  int S = 1;
+  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
+  return seq_sgpr_bc(p, dtype == VM_DTYPE_BF16 ? 2 : 4) && (S <= 1 || workspace_bytes >= need);
 }
 
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,

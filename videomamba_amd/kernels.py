@@ -148,10 +148,12 @@ def scan_workspace_bytes(batch: int, dim: int, seqlen: int, dstate: int,
 
 def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, softplus,
              h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen, dstate, dtype,
-             stream, workspace: Optional[Tensor] = None):
+             stream, workspace: Optional[Tensor] = None, pair=None):
     """Strides are (batch, channel|state, step) element strides; either every
     u/delta/z/out channel stride is 1 (token-major) or every step stride is 1.
-    ``workspace`` (a uint8 device buffer) replaces the per-stream scratch cache."""
+    ``workspace`` (a uint8 device buffer) replaces the per-stream scratch cache.
+    ``pair`` = (split, A32_bwd, D32_bwd, bias32_bwd, h0_bwd, h_last_bwd, frame_len) runs
+    ``vm_selective_scan_bidir_fwd``: rows >= split are the flipped backward direction."""
     lib = _lib.load()
     seg = int(options.get().scan_segments)
     ws_bytes = 0
@@ -164,15 +166,20 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
             ws = workspace
         else:
             ws = scratch(u.device, int(stream), ws_bytes)
-    rc = lib.vm_selective_scan_fwd(
-        _p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
-        _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
-        _p(D32), _p(z), z_s[0], z_s[1], z_s[2], _p(bias32), int(softplus),
-        _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
-        _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
-        _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate, dtype,
-        seg, _p(ws), ws_bytes, stream)
-    _lib.check(rc, "vm_selective_scan_fwd")
+    args = (_p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
+            _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
+            _p(D32), _p(z), z_s[0], z_s[1], z_s[2], _p(bias32), int(softplus),
+            _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
+            _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0],
+            hl_s[1], _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate, dtype)
+    if pair is None:
+        rc = lib.vm_selective_scan_fwd(*args, seg, _p(ws), ws_bytes, stream)
+        _lib.check(rc, "vm_selective_scan_fwd")
+        return
+    split, a_b, d_b, bias_b, h0_b, hl_b, frame = pair
+    rc = lib.vm_selective_scan_bidir_fwd(*args, split, _p(a_b), _p(d_b), _p(bias_b), _p(h0_b),
+                                         _p(hl_b), frame, seg, _p(ws), ws_bytes, stream)
+    _lib.check(rc, "vm_selective_scan_bidir_fwd")
 
 
 def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, batch, dim,
@@ -261,12 +268,14 @@ def norm_pool_workspace_bytes(batch: int, groups: int, max_group_rows: int, cols
 def norm_pool(h: Tensor, residual: Optional[Tensor], rows: int, w32: Tensor,
               b32: Optional[Tensor], eps: float, is_rms: bool, *, head: int, groups: int,
               group_rows: int = 0, bounds: Optional[Tensor] = None, max_group_rows: int = 0,
-              sums: bool = False, out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+              sums: bool = False, out: Optional[Tensor] = None,
+              rev_frame: int = 0) -> Tuple[Tensor, Optional[Tensor]]:
     """Final add + norm of rows [0, rows) of the padded (B, Lp, C) ``h`` (+ ``residual``)
     into a contiguous (B, rows, C) tensor; with ``sums`` also the per-group fp32 column
     sums for :func:`pool_finish` (returned workspace, valid until the next scratch user
     on this stream).  Groups: ``groups`` x ``group_rows`` rows after ``head`` rows, or
-    int32 ``bounds`` (B, groups+1)."""
+    int32 ``bounds`` (B, groups+1).  ``out`` may be a (B, >= rows, C) buffer with contiguous
+    rows; ``rev_frame`` > 0 reads the grouped rows in reversed frame order."""
     Bsz, Lp, C = h.shape
     if out is None:
         out = torch.empty((Bsz, rows, C), dtype=h.dtype, device=h.device)
@@ -282,8 +291,8 @@ def norm_pool(h: Tensor, residual: Optional[Tensor], rows: int, w32: Tensor,
         _p(h), dtype_code(h.dtype), _p(residual),
         dtype_code(residual.dtype) if residual is not None else 0, h.stride(0),
         _p(w32), _p(b32), float(eps), int(is_rms), _p(out), dtype_code(out.dtype),
-        Bsz, rows, C, head, groups, group_rows, _p(bounds), max_group_rows,
-        _p(ws), nbytes, _stream(h))
+        out.stride(0), Bsz, rows, C, head, groups, group_rows, _p(bounds), max_group_rows,
+        int(rev_frame), _p(ws), nbytes, _stream(h))
     _lib.check(rc, "vm_norm_pool_fwd")
     return out, ws
 

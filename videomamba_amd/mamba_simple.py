@@ -54,6 +54,15 @@ def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
         return F.linear(x, w, b)
 
 
+def _linear_into(x: Tensor, w: Tensor, b: Optional[Tensor], out: Tensor) -> Tensor:
+    """:func:`_linear` into a preallocated buffer with unit column stride (a half of the
+    bidirectional refiner's paired buffers)."""
+    with tuned():
+        if b is None:
+            return torch.mm(x, w.t(), out=out)
+        return torch.addmm(b.to(out.dtype), x, w.t(), out=out)
+
+
 def _matmul(a: Tensor, b: Tensor) -> Tensor:
     with tuned():
         return torch.matmul(a, b)
@@ -232,19 +241,25 @@ class Mamba(nn.Module):
             out += self.out_proj.bias.to(out.dtype)
         return out.view(Bsz, Lp, C)
 
-    def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last):
-        """Token-major form of :meth:`_forward_padded` (same math, same rounding points)."""
+    def _tm_front(self, hn, seqlen, conv_state_in, conv_state_out, bufs=None):
+        """in_proj -> conv + silu -> x_proj -> dt_proj of the token-major form: (xz, u,
+        x_dbl, dt), each (B*Lp, channels).  ``bufs`` = preallocated (xz, u, x_dbl, dt) (the
+        refiner's paired buffers); otherwise they are allocated here."""
         Bsz, Lp, C = hn.shape
         Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
         n = Bsz * Lp
         E = R + 2 * N
         dt_code = K.dtype_code(hn.dtype)
         stream = torch.cuda.current_stream(hn.device).cuda_stream
-        A, Dv, dbias, cw, cb = self._fp32_params()
-        s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
-
-        xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
-        u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+        _, _, _, cw, cb = self._fp32_params()
+        s_u, s_xz = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm)
+        if bufs is None:
+            xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
+            u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            x_dbl = dt = None
+        else:
+            xz, u, x_dbl, dt = bufs
+            _linear_into(hn.view(n, C), self.in_proj.weight, self.in_proj.bias, xz)
         csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
@@ -255,16 +270,33 @@ class Mamba(nn.Module):
             # epilogue it measured a wash at B = 336 (scan -222 us, conv_proj +385 us per
             # layer, profiles/r01f_delta_placement.txt)
             wx_pad, wdt_pad = self._padded_proj_weights()
-            x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
-            dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            if x_dbl is None:
+                x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
+                dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
             K.conv_proj_raw(xz, s_xz[::2], cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                             wx_pad, E, wdt_pad, R, u, s_u[::2], x_dbl, (Lp * E, E), dt,
                             s_u[::2], Lp, Bsz, Dm, seqlen, W, stream)
         else:
             K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                        u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
-            x_dbl = _linear(u, self.x_proj.weight)  # (n, R+2N)
-            dt = _linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias added in the scan
+            if x_dbl is None:
+                x_dbl = _linear(u, self.x_proj.weight)  # (n, R+2N)
+                dt = _linear(x_dbl[:, :R], self.dt_proj.weight)  # (n, D); bias in the scan
+            else:
+                _linear_into(u, self.x_proj.weight, None, x_dbl)
+                _linear_into(x_dbl[:, :R], self.dt_proj.weight, None, dt)
+        return xz, u, x_dbl, dt
+
+    def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last):
+        """Token-major form of :meth:`_forward_padded` (same math, same rounding points)."""
+        Bsz, Lp, C = hn.shape
+        Dm, N, R = self.d_inner, self.d_state, self.dt_rank
+        E = R + 2 * N
+        dt_code = K.dtype_code(hn.dtype)
+        stream = torch.cuda.current_stream(hn.device).cuda_stream
+        A, Dv, dbias, _, _ = self._fp32_params()
+        s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
+        xz, u, x_dbl, dt = self._tm_front(hn, seqlen, conv_state_in, conv_state_out)
         y = torch.empty_like(u)
         K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                    xz[:, Dm:], s_xz, dbias, True,
