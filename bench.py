@@ -199,6 +199,14 @@ def _oracle_clip_seconds(cfg, runs=3):
     return statistics.median(times)
 
 
+# The timed oracle against the reference's own CPU path, both on 8 threads of the build
+# container (profiles/r02_cpu_calibration.json, scripts/cpu_calibration.py): the port runs
+# within the survey's +-15 % band of the reference, so its rate stands in for the reference's.
+CPU_CALIBRATION = {"threads": 8, "oracle_over_reference_s_per_clip": {"ti8": 1.161, "m16": 0.895},
+                   "reference_s_per_clip": {"ti8": 3.32, "m16": 24.9},
+                   "source": "profiles/r02_cpu_calibration.json"}
+
+
 def cpu_baseline(cfg, threads):
     """the oracle (the CPU restatement pinned to the reference) on the host
     cores, median of 3 after 1 warm-up, fp32 B=1: the bench clip, and C1 (Ti 8x224^2)."""
@@ -207,7 +215,7 @@ def cpu_baseline(cfg, threads):
     ti = CONFIGS["ti8"]
     dt_c1 = _oracle_clip_seconds(ti)
     return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
-            "cores": threads, "kind": "port",
+            "cores": threads, "kind": "port", "calibration": CPU_CALIBRATION,
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
                       f"median of 3 after 1 warm-up ({dt:.2f} s), oracle/videomamba_oracle.py",
             "c1": {"value": round(ti["frames"] * 196 / dt_c1, 2), "unit": "video-tokens/s",
