@@ -21,7 +21,8 @@ max-over-ranks / JSON-line control flow on the gloo backend (tests/test_sharding
 launches it under torchrun with 2 ranks).
 
 Extra fields: chunk_p50_ms (B=1 chunk latency, HIP-graph replay; chunk_p50_eager_ms the
-eager launch path), roofline of the selective-scan kernel
+eager launch path), b1_kernels (per-stage roofline fractions of one M layer at the B=1
+chunk shape), roofline of the selective-scan kernel
 (HIP-event timed at the bench shape; algorithmic bytes per launch), cpu_baseline (the
 CPU oracle on one M-16f clip, rank 0 at N=1 only).
 """
@@ -173,6 +174,88 @@ def scan_roofline(batch, reps, device, layout="tm"):
                                LAB_NO_MEMORY_US_PER_CLIP_LAYER * batch * 1e-6 / avg_s, 4),
                            "note": "1 exp + 4 fma-class per (element, state) at measured gfx950 "
                                    "issue costs, 2.4 GHz; the HBM floor is below it"}}
+
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def _event_us(fn, reps):
+    """Average HIP-event time of fn() on the current stream, after warm-up."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def b1_kernel_rooflines(device, reps=50):
+    """Per-kernel roofline fractions of one VideoMamba-M layer at the B=1 streaming-chunk
+    shape (L=3137, padded 3144 rows): each stage launched alone, HIP-event timed on the
+    launch stream, against its algorithmic bytes (HBM-bound kernels) or flops (GEMMs).
+    Stages: add+RMSNorm (x bf16 + residual fp32 in, residual fp32 + normed bf16 out),
+    in_proj GEMM, fused conv+x_proj+dt_proj (+ conv state out), the scan (scan_roofline at
+    B=1: the segmented chunk form), out_proj GEMM."""
+    from videomamba_amd import kernels as K
+    from videomamba_amd.layers import round_up
+    from videomamba_amd.mamba_simple import Mamba, _linear
+
+    torch.manual_seed(0)
+    C, L = 576, 3137
+    Lp = round_up(L)
+    bf = torch.bfloat16
+    mx = Mamba(d_model=C, layer_idx=0).to(device, bf).eval()
+    Dm, N, R, W = mx.d_inner, mx.d_state, mx.dt_rank, mx.d_conv
+    E = R + 2 * N
+    stream = torch.cuda.current_stream(device).cuda_stream
+    x = torch.randn(Lp, C, device=device, dtype=bf)
+    res = torch.randn(Lp, C, device=device)
+    w32 = torch.ones(C, device=device)
+    hn = torch.empty(Lp, C, device=device, dtype=bf)
+    xz = torch.randn(Lp, 2 * Dm, device=device, dtype=bf)
+    y = torch.randn(Lp, Dm, device=device, dtype=bf)
+    u = torch.empty(Lp, Dm, device=device, dtype=bf)
+    dt = torch.empty(Lp, Dm, device=device, dtype=bf)
+    xdbl = torch.empty(Lp, E, device=device, dtype=bf)
+    cs_in = torch.randn(1, Dm, W, device=device, dtype=bf)
+    cs_out = torch.empty(1, Dm, W, device=device, dtype=bf)
+    _, _, _, cw, cb = mx._fp32_params()
+    wx_pad, wdt_pad = mx._padded_proj_weights()
+    out = {}
+
+    def hbm(name, us, nbytes):
+        gbs = nbytes / us / 1e3
+        out[name] = {"us": round(us, 2), "bound": "hbm", "achieved": round(gbs, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+    def mfma(name, us, flops):
+        tf = flops / us / 1e6
+        out[name] = {"us": round(us, 2), "bound": "mfma", "achieved": round(tf, 1),
+                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4)}
+
+    with torch.no_grad():
+        hbm("add_norm", _event_us(lambda: K.add_norm_raw(x, res, w32, None, hn, res, Lp, C, 1e-5,
+                                                         True, stream), reps), 12 * Lp * C)
+        mfma("in_proj", _event_us(lambda: _linear(hn, mx.in_proj.weight), reps),
+             2 * Lp * C * 2 * Dm)
+        hbm("conv_proj", _event_us(lambda: K.conv_proj_raw(
+            xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs_in, (cs_in.stride(0), cs_in.stride(1)),
+            cs_out, (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, wdt_pad, R, u,
+            (Lp * Dm, Dm), xdbl, (Lp * E, E), dt, (Lp * Dm, Dm), Lp, 1, Dm, L, W, stream), reps),
+            2 * Lp * (3 * Dm + E) + 2 * (wx_pad.numel() + wdt_pad.numel()))
+        sc = scan_roofline(1, reps, device, "tm")
+        out["scan"] = {k: sc[k] for k in ("avg_us", "bound", "achieved", "peak", "unit", "frac")}
+        out["scan"]["us"] = out["scan"].pop("avg_us")
+        mfma("out_proj", _event_us(lambda: _linear(y, mx.out_proj.weight), reps),
+             2 * Lp * Dm * C)
+    out["layer_us_sum"] = round(sum(v["us"] for v in out.values()), 2)
+    out["shape"] = f"VideoMamba-M layer, B=1, L={L} (padded {Lp}), bf16, stages launched alone"
+    return out
 
 
 def _oracle_clip_seconds(cfg, runs=3):
@@ -365,6 +448,7 @@ def main():
         from videomamba_amd.mamba_simple import mixer_layout
         roof = scan_roofline(max(B, 1), args.scan_reps, device,
                              mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device))
+        b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 else None
 
     if rank == 0:
         line.update({
@@ -373,6 +457,8 @@ def main():
             "chunk_p50_batch": 1, "chunk_p50_mode": "hipGraph replay (StreamingChunkGraph)",
             "roofline": roof,
         })
+        if b1 is not None:
+            line["b1_kernels"] = b1
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         print(json.dumps(line), flush=True)
