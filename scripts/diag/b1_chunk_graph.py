@@ -1,0 +1,43 @@
+"""B=1 M-16f stateful chunks replayed from the captured HIP graph (the bench's chunk_p50
+path), for rocprofv3 kernel stats: python scripts/diag/b1_chunk_graph.py [replays]"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from videomamba_amd.graphs import StreamingChunkGraph  # noqa: E402
+from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+torch.manual_seed(0)
+model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16).cuda().to(torch.bfloat16).eval()
+x = torch.randn(1, 3, 16, 224, 224, device="cuda").to(torch.bfloat16)
+runner = StreamingChunkGraph(model, batch=1, frames=16)
+with torch.no_grad():
+    runner.run(x, temporal_pos_offset=0)
+    torch.cuda.synchronize()
+    lat = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        runner.run(x, temporal_pos_offset=0)
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    g, _ = runner._graphs[True]
+    rep = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        rep.append((time.perf_counter() - t0) * 1e3)
+    key = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        runner._params_key()
+        key.append((time.perf_counter() - t0) * 1e3)
+lat.sort()
+rep.sort()
+key.sort()
+print(f"graph replays {n}: run() p50 {lat[n // 2]:.3f} ms  min {lat[0]:.3f} ms; "
+      f"replay-only p50 {rep[n // 2]:.3f} ms; params-key p50 {key[n // 2]:.3f} ms")

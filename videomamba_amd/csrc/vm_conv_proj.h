@@ -13,6 +13,7 @@ struct ConvProjTmArgs {
   const bf16_t* x; long long x_tl;
   const float* cw; const float* cb;
   const void* csi; int csi_dtype; long long csi_sb, csi_sd;
+  void* cso; int cso_dtype; long long cso_sb, cso_sd;  // new conv state (nullable)
   const bf16_t* wx; int e, e_pad;
   const bf16_t* wdt; int r, r_pad;   // wdt == nullptr: no dt_proj
   bf16_t* u; long long u_tl;

@@ -408,7 +408,8 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   // skips it (conv + x_proj only: a consumer that projects dt itself)
   const bool fused_dt = dt != nullptr;
   const bool spd = dt_softplus != 0;
-  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= 80 && r_pad <= 80) {
+  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= 80 && r_pad <= 80 &&
+      out_len >= 8) {
     // small batch: the split-K form (vm_conv_proj_sk.hip) fills the chip and keeps the
     // x_proj reduction order fixed per token
     const long long need = conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
@@ -420,13 +421,12 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     ConvProjTmArgs a{};
     a.x = p.xz; a.x_tl = xz_sl; a.cw = conv_weight; a.cb = conv_bias;
     a.csi = cs_in; a.csi_dtype = cs_in_dtype; a.csi_sb = csi_sb; a.csi_sd = csi_sd;
+    a.cso = cs_out; a.cso_dtype = cs_out_dtype; a.cso_sb = cso_sb; a.cso_sd = cso_sd;
     a.wx = p.wx; a.e = e; a.e_pad = e_pad; a.wdt = fused_dt ? p.wdt : nullptr; a.r = r;
     a.r_pad = r_pad; a.u = p.u; a.u_tl = u_sl; a.xdbl = p.xdbl; a.xd_tl = xd_sl; a.dt = p.dt;
     a.dt_tl = dt_sl; a.out_len = out_len; a.batch = batch; a.dim = dim; a.seqlen = seqlen;
     a.width = width;
-    conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
-    if (cs_out)
-      hipLaunchKernelGGL(conv_state_out_kernel, dim3((dim + 255) / 256, batch), dim3(256), 0, st, p);
+    conv_proj_sk_launch(a, static_cast<float*>(workspace), st);  // writes the conv state too
     return vmhost::launch_status("vm_conv_proj_fwd");
   }
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };

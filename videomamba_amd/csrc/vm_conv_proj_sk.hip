@@ -273,6 +273,10 @@ __global__ __launch_bounds__(256) void conv_state_cm_kernel(const ConvProjCmPara
 // ================================================================ token-major split-K
 constexpr int kTmPitch = 136;  // LDS row pitch in bf16 (272 B): 128 channels + 16-B pad
 constexpr int kSkCh = 128;     // channels per split (fixed: see the file header)
+// conv-state rows staged per tile: sequences whose first 3 steps touch a 64-token tile
+// (out_len >= 8: at most 64 / 8 + 1)
+constexpr int kSkCsRows = kCmTok / 8 + 1;
+constexpr int kSkCsLoads = (kSkCsRows * 3 * kSkCh + 255) / 256;
 
 struct SkTmParams {
   ConvProjTmArgs a;
@@ -291,6 +295,7 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
   bf16_t* sX = sm;                         // [72][kTmPitch]
   bf16_t* sU = sX + 72 * kTmPitch;         // [64][kTmPitch]
   bf16_t* sW = sU + kCmTok * kTmPitch;     // [e_pad][kTmPitch]
+  float* sC = reinterpret_cast<float*>(sW + p.e_pad * kTmPitch);  // [kSkCsRows][3][128]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -330,6 +335,27 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
     wh[k] = k < W ? p.cw[(c + 1) * W + k] : 0.0f;
   }
   const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
+  // old conv-state taps (steps -3 .. -1) of every sequence whose first steps fall in this
+  // tile, staged with the same load round: read inside the conv loop they were dependent
+  // round trips that held the tile containing a sequence start for several microseconds
+  const int b_lo = tok0 / p.out_len;
+  const int nbs = p.csi ? min(p.batch - 1, (tok0 + kCmTok - 1) / p.out_len) - b_lo + 1 : 0;
+  float cv[kSkCsLoads];
+#pragma unroll
+  for (int k = 0; k < kSkCsLoads; ++k) {
+    const int i = tid + k * 256;
+    const int bb = i / (3 * kSkCh), m = (i / kSkCh) % 3, ch = i % kSkCh;
+    const int tap = W - 1 - m;  // state column of step -(m + 1)
+    cv[k] = 0.0f;
+    if (bb < nbs && ch < nch && tap >= 0)
+      cv[k] = load_dyn(p.csi, (b_lo + bb) * p.csi_sb + (long long)(c0 + ch) * p.csi_sd + tap,
+                       p.csi_dtype);
+  }
+#pragma unroll
+  for (int k = 0; k < kSkCsLoads; ++k) {
+    const int i = tid + k * 256;
+    if (i / (3 * kSkCh) < nbs) sC[i] = cv[k];
+  }
 #pragma unroll
   for (int k = 0; k < kXI; ++k) {
     const int i = tid + k * 256;
@@ -341,6 +367,25 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
     if (i < NB * 16 * 16) *reinterpret_cast<uint4*>(&sW[(i >> 4) * kTmPitch + (i & 15) * 8]) = wv[k];
   }
   __syncthreads();
+  // ---- new conv state: the last `width` raw inputs of every sequence ending in this tile
+  // (mamba_simple.py:383-399), from the staged rows (width - 1 <= halo) or the old state ----
+  if (p.cso && tid < nch) {
+    const int b1 = min(p.batch - 1, (tok0 + kCmTok - 1) / p.out_len);
+    for (int b = tok0 / p.out_len; b <= b1; ++b) {
+      const int tl = b * p.out_len + p.seqlen - 1;
+      if (tl < tok0 || tl >= tok0 + kCmTok) continue;
+      const int ch = c0 + tid;
+      for (int s = 0; s < W; ++s) {
+        const int te = p.seqlen - W + s;
+        float v = 0.0f;
+        if (te >= 0)
+          v = to_f32(sX[(kCmHalo + b * p.out_len + te - tok0) * kTmPitch + tid]);
+        else if (p.csi)
+          v = load_dyn(p.csi, b * p.csi_sb + (long long)ch * p.csi_sd + W + te, p.csi_dtype);
+        store_dyn(p.cso, b * p.cso_sb + (long long)ch * p.cso_sd + s, p.cso_dtype, v);
+      }
+    }
+  }
   // ---- conv + SiLU: channels c, c + 1 (one packed word), tokens 16w .. 16w+15 ----
   const int t0 = wave * 16;
   uint32_t upk[16];
@@ -365,9 +410,11 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
                 &sX[(kCmHalo + t0 + i - (W - 1) + k) * kTmPitch + 2 * lane]);
             vl = __uint_as_float(wd << 16);
             vh = __uint_as_float(wd & 0xffff0000u);
-          } else if (p.csi && tok < q.ntok && cact) {  // taps before the sequence start
-            vl = load_dyn(p.csi, b * p.csi_sb + (long long)c * p.csi_sd + W + j, p.csi_dtype);
-            vh = load_dyn(p.csi, b * p.csi_sb + (long long)(c + 1) * p.csi_sd + W + j, p.csi_dtype);
+          } else if (p.csi && tok < q.ntok) {  // taps before the sequence start (staged)
+            const float2 cs = *reinterpret_cast<const float2*>(
+                &sC[((b - b_lo) * 3 - j - 1) * kSkCh + 2 * lane]);
+            vl = cs.x;
+            vh = cs.y;
           }
           al = fmaf(wl[k], vl, al);
           ah = fmaf(wh[k], vh, ah);
@@ -550,7 +597,8 @@ void conv_proj_sk_launch(const ConvProjTmArgs& a, float* part, hipStream_t s) {
   q.nsplit = (a.dim + kSkCh - 1) / kSkCh;
   q.ep = (a.e + 3) / 4 * 4;
   const unsigned tiles = static_cast<unsigned>((q.ntok + kCmTok - 1) / kCmTok);
-  const size_t lds = static_cast<size_t>(72 + kCmTok + a.e_pad) * kTmPitch * sizeof(bf16_t);
+  const size_t lds = static_cast<size_t>(72 + kCmTok + a.e_pad) * kTmPitch * sizeof(bf16_t) +
+                    static_cast<size_t>(kSkCsRows) * 3 * kSkCh * sizeof(float);
   dim3 g1(tiles, q.nsplit);
   switch (a.e_pad / 16) {
 #define VM_SK_CASE(NBV) \

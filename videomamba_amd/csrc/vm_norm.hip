@@ -291,18 +291,27 @@ struct PoolFinishParams {
   void* xpool; int xp_dtype; int cols, prow;  // prow = pooled rows per batch row
 };
 
-__device__ __forceinline__ float block_sum256(float v, float* sh) {
+__device__ __forceinline__ float block_sum1024(float v, float* sh) {
   v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+  float t = 0.0f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += sh[w];
+  return t;
 }
 
-__global__ __launch_bounds__(256) void pool_finish_kernel(const PoolFinishParams p) {
-  constexpr int kMaxPer = 8;  // cols <= 2048
-  __shared__ float sh[4];
+// Slice sums: the (group, slice) rows of one pooled row are consecutive in the workspace.
+// Thread t owns column quad t % nq and every P-th row from t / nq (P = 1024 / nq threads
+// per quad, 4 loads in flight each); the P partial sums combine in LDS in a fixed order.
+// (One dependent load per slice and column made this a 140 us tail at B = 1.)
+__global__ __launch_bounds__(1024) void pool_finish_kernel(const PoolFinishParams p) {
+  constexpr int kMaxPer = 2;  // cols <= 2048
+  __shared__ float sh[16];
+  __shared__ __attribute__((aligned(16))) float4 red[1024];
   const int q = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
   const bool rnd = p.xp_dtype == VM_DTYPE_BF16;
   auto group_count = [&](int g) -> int {
     return p.bounds ? p.bounds[(long long)b * (p.groups + 1) + g + 1] -
@@ -316,10 +325,36 @@ __global__ __launch_bounds__(256) void pool_finish_kernel(const PoolFinishParams
   int count = 0;
   if (!use_cls)
     for (int g = g0; g < g1; ++g) count += group_count(g);
+  const int nq = p.cols >> 2;  // <= 512
+  const int P = 1024 / nq;
+  const int nrow = (g1 - g0) * p.slices;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int part = tid / nq, qd = tid % nq;
+  if (!use_cls && part < P) {
+    const float4* base = reinterpret_cast<const float4*>(
+        p.part + ((long long)b * p.groups + g0) * p.slices * p.cols) + qd;
+    int r = part;
+    for (; r + 3 * P < nrow; r += 4 * P) {
+      const float4 a0 = base[(long long)r * nq];
+      const float4 a1 = base[(long long)(r + P) * nq];
+      const float4 a2 = base[(long long)(r + 2 * P) * nq];
+      const float4 a3 = base[(long long)(r + 3 * P) * nq];
+      acc.x += a0.x; acc.y += a0.y; acc.z += a0.z; acc.w += a0.w;
+      acc.x += a1.x; acc.y += a1.y; acc.z += a1.z; acc.w += a1.w;
+      acc.x += a2.x; acc.y += a2.y; acc.z += a2.z; acc.w += a2.w;
+      acc.x += a3.x; acc.y += a3.y; acc.z += a3.z; acc.w += a3.w;
+    }
+    for (; r < nrow; r += P) {
+      const float4 a0 = base[(long long)r * nq];
+      acc.x += a0.x; acc.y += a0.y; acc.z += a0.z; acc.w += a0.w;
+    }
+  }
+  red[tid] = acc;
+  __syncthreads();
   float v[kMaxPer];
 #pragma unroll
   for (int k = 0; k < kMaxPer; ++k) {
-    const int c = threadIdx.x + 256 * k;
+    const int c = tid + 1024 * k;
     float x = 0.0f;
     if (c < p.cols) {
       const float cl = p.cls ? load_dyn(p.cls, (long long)b * p.cls_bstride + c, p.cls_dtype)
@@ -328,9 +363,8 @@ __global__ __launch_bounds__(256) void pool_finish_kernel(const PoolFinishParams
         x = cl;
       } else {
         float sum = 0.0f;
-        for (int g = g0; g < g1; ++g)
-          for (int s = 0; s < p.slices; ++s)
-            sum += p.part[(((long long)b * p.groups + g) * p.slices + s) * p.cols + c];
+        for (int pp = 0; pp < P; ++pp)
+          sum += reinterpret_cast<const float*>(&red[pp * nq + (c >> 2)])[c & 3];
         x = sum / static_cast<float>(count);
         if (rnd) x = to_f32(from_f32<bf16_t>(x));
         if (p.mode == kPoolClsAvg) {
@@ -344,18 +378,18 @@ __global__ __launch_bounds__(256) void pool_finish_kernel(const PoolFinishParams
   float s1 = 0.0f;
 #pragma unroll
   for (int k = 0; k < kMaxPer; ++k) s1 += v[k];
-  const float mean = block_sum256(s1, sh) / p.cols;
+  const float mean = block_sum1024(s1, sh) / p.cols;
   float s2 = 0.0f;
 #pragma unroll
   for (int k = 0; k < kMaxPer; ++k) {
-    const float d = threadIdx.x + 256 * k < p.cols ? v[k] - mean : 0.0f;
+    const float d = tid + 1024 * k < p.cols ? v[k] - mean : 0.0f;
     s2 = fmaf(d, d, s2);
   }
-  const float rstd = rsqrtf(block_sum256(s2, sh) / p.cols + p.ln_eps);
+  const float rstd = rsqrtf(block_sum1024(s2, sh) / p.cols + p.ln_eps);
   const long long o = ((long long)b * p.prow + q) * p.cols;
 #pragma unroll
   for (int k = 0; k < kMaxPer; ++k) {
-    const int c = threadIdx.x + 256 * k;
+    const int c = tid + 1024 * k;
     if (c < p.cols) {
       float y = (v[k] - mean) * rstd;
       if (p.lnw) y *= p.lnw[c];
@@ -441,7 +475,7 @@ extern "C" int vm_pool_finish_fwd(const void* workspace, int batch, int groups, 
     vmhost::set_error("vm_pool_finish_fwd: null required pointer");
     return VM_E_INVALID;
   }
-  if (batch < 0 || groups < 1 || mode < 0 || mode > 3 || cols < 1 || cols > 2048 ||
+  if (batch < 0 || groups < 1 || mode < 0 || mode > 3 || cols < 4 || cols > 2048 || cols % 4 ||
       max_group_rows < 1 || !vmhost::dtype_ok(xp_dtype) || (cls && !vmhost::dtype_ok(cls_dtype))) {
     vmhost::set_error("vm_pool_finish_fwd: bad mode/shape/dtype");
     return VM_E_INVALID;
@@ -455,7 +489,7 @@ extern "C" int vm_pool_finish_fwd(const void* workspace, int batch, int groups, 
   p.ln_eps = ln_eps; p.xpool = x_pool; p.xp_dtype = xp_dtype; p.cols = cols;
   const int navg = keep_temporal ? groups : 1;
   p.prow = mode == kPoolCls ? 1 : (mode == kPoolClsCatAvg ? 1 + navg : navg);
-  hipLaunchKernelGGL(pool_finish_kernel, dim3(p.prow, batch), dim3(256), 0,
+  hipLaunchKernelGGL(pool_finish_kernel, dim3(p.prow, batch), dim3(1024), 0,
                      static_cast<hipStream_t>(stream), p);
   return vmhost::launch_status("vm_pool_finish_fwd");
 }

@@ -14,7 +14,8 @@ chunk kind (first chunk with CLS, continuation chunk without) into a ``torch.cud
   eager ``model(x, ssm_state=..., temporal_pos_offset=...)`` would return minus the state
   container — views of static buffers, valid until the next ``run``;
 * the state advances in place (the ssm state is updated in place by the scan as in the
-  eager path; the graph copies each layer's new conv window back into its static buffer),
+  eager path; the conv kernels write every layer's new conv window into one stacked buffer
+  and the graph copies it back into the stacked state in one copy),
   so consecutive ``run`` calls stream exactly like the eager loop with carried state.
 
 Semantics are the eager path's (same kernels, same rounding points); tests check replay
@@ -24,9 +25,10 @@ against eager chunk by chunk.  Masks and keep_temporal pooling are not graph-cap
 Lifetimes.  A graph replays raw device pointers, so everything it touches is pinned for
 its lifetime: the runner owns the scan's scratch workspace (no shared cache can grow and
 free it under the graph), and it records every parameter's (data_ptr, version) at
-capture.  When the model's parameters change (``load_state_dict``, an in-place edit, a
-``.to()``), the next ``run`` drops the stale graphs and captures again, so a replay never
-reads weight caches that the eager path has since replaced.
+capture (and holds references to them).  When the model's parameters change
+(``load_state_dict``, an in-place edit, a ``.to()``), the next ``run`` drops the stale
+graphs and captures again, so a replay never reads weight caches that the eager path has
+since replaced; replacing Parameter objects outright needs ``invalidate()``.
 """
 
 from __future__ import annotations
@@ -56,11 +58,17 @@ class StreamingChunkGraph:
                                     device=self.device)
         self.static_tpos = torch.zeros(1, self.tt, model.embed_dim, dtype=self.dtype,
                                        device=self.device)
+        # per-layer states as views of two stacked buffers: the new conv states land in
+        # _conv_next (written by the conv kernels) and one copy per chunk carries them over
+        st = model.allocate_state(batch, dtype=self.dtype, device=self.device)
+        self._conv_all = torch.stack([c for c, _ in st])
+        self._conv_next = torch.empty_like(self._conv_all)
         self._state: List[Tuple[Tensor, Tensor]] = [
-            (c, s) for c, s in model.allocate_state(batch, dtype=self.dtype, device=self.device)]
+            (self._conv_all[i], s) for i, (_, s) in enumerate(st)]
         self._graphs: Dict[bool, Tuple[torch.cuda.CUDAGraph, object]] = {}
         self._pool = None
         self._param_key = None
+        self._plist = None
         self._ws = None  # scan scratch owned by the captured graphs
 
     # ------------------------------------------------------------------ state
@@ -87,18 +95,29 @@ class StreamingChunkGraph:
         if m.add_pool_norm:
             gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
             pool = (False, self.tt, gh * gw)
-        feats, x_pool, new_state = m._encode(self.static_x, None, self._state, offset,
-                                             tpos=self.static_tpos, pool=pool)
-        for (c, _), (c_new, _) in zip(self._state, new_state):
-            if c_new.data_ptr() != c.data_ptr():
-                c.copy_(c_new)
+        feats, x_pool, _ = m._encode(self.static_x, None, self._state, offset,
+                                     tpos=self.static_tpos, pool=pool, conv_out=self._conv_next)
+        self._conv_all.copy_(self._conv_next)
         if pool is None:
             return (feats,)
         return (feats[:, 1:] if has_cls else feats), x_pool
 
     def _params_key(self):
-        return tuple((t.data_ptr(), t._version, t.dtype, t.device)
-                     for t in list(self.model.parameters()) + list(self.model.buffers()))
+        # the parameter list is walked once (the module-tree walk was ~0.4 ms of every
+        # run); held references keep the captured tensors' memory alive, and a load /
+        # in-place edit / .to() shows as a version or data_ptr change on them
+        if self._plist is None:
+            self._plist = list(self.model.parameters()) + list(self.model.buffers())
+        return tuple((t._version, t.data_ptr()) for t in self._plist)
+
+    def invalidate(self) -> None:
+        """Drop the captured graphs and re-scan the parameters: call after replacing
+        Parameter objects (``module.weight = nn.Parameter(...)``); loads, in-place edits
+        and ``.to()`` are detected on their own."""
+        self._graphs.clear()
+        self._pool = None
+        self._plist = None
+        self._param_key = None
 
     def _workspace(self) -> Tensor:
         """Kernel scratch (segmented scan, channel-major conv_proj partials) sized for the

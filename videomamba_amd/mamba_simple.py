@@ -316,9 +316,10 @@ class Mamba(nn.Module):
 
     def forward_padded(self, hn: Tensor, seqlen: int, *, ssm_state: Optional[Tensor] = None,
                        state: Optional[Tuple[Tensor, Tensor]] = None,
-                       return_state: bool = False):
+                       return_state: bool = False, conv_out: Optional[Tensor] = None):
         """Model-internal entry on the padded layout (no inference_params).  Same state
-        semantics as :meth:`forward`."""
+        semantics as :meth:`forward`; ``conv_out`` (B, D, d_conv) receives the new conv
+        state instead of a fresh tensor (the graph runner's batched state buffers)."""
         conv_state = None
         if state is not None:
             conv_state, ssm_state = state
@@ -329,7 +330,9 @@ class Mamba(nn.Module):
             self._check_state(ssm_state, self.d_state, "ssm_state", Bsz)
         use_inplace = ssm_state is not None and state is None and not return_state
         cs_out = None
-        if return_state:
+        if return_state and conv_out is not None:
+            cs_out = self._check_state(conv_out, self.d_conv, "conv_out", Bsz)
+        elif return_state:
             cs_dtype = conv_state.dtype if conv_state is not None else hn.dtype
             cs_out = torch.empty((Bsz, self.d_inner, self.d_conv), dtype=cs_dtype,
                                  device=hn.device)

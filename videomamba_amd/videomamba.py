@@ -121,11 +121,11 @@ class Block(nn.Module):
         return hidden, residual
 
     def forward_padded(self, hidden: Tensor, residual: Optional[Tensor], seqlen: int,
-                       state=None, ssm_state=None, return_state: bool = False):
+                       state=None, ssm_state=None, return_state: bool = False, conv_out=None):
         """Model-internal: same as ``forward`` on the padded (B, Lp, C) buffers."""
         hn, residual = self._add_norm(hidden, residual, inplace=True)
         res = self.mixer.forward_padded(hn, seqlen, ssm_state=ssm_state, state=state,
-                                        return_state=return_state)
+                                        return_state=return_state, conv_out=conv_out)
         if return_state:
             return res[0], residual, res[1]
         return res, residual, None
@@ -428,8 +428,9 @@ class PretrainVideoMamba(nn.Module):
         return bounds.to(torch.int32).contiguous(), int(counts.max().item())
 
     # ------------------------------------------------------------------ layer loop
-    def _run_layers(self, h, residual, L, ssm_state):
-        """The depth loop over padded buffers: (h, residual, new_states|None, tuple_out)."""
+    def _run_layers(self, h, residual, L, ssm_state, conv_out=None):
+        """The depth loop over padded buffers: (h, residual, new_states|None, tuple_out).
+        ``conv_out`` (depth, B, D, d_conv) receives the new conv states (graph runner)."""
         new_states = None
         tuple_out = False
         for idx, layer in enumerate(self.layers):
@@ -443,7 +444,8 @@ class PretrainVideoMamba(nn.Module):
                     tuple_out = isinstance(ssm_state, tuple)
             if full:
                 h, residual, layer_state = layer.forward_padded(
-                    h, residual, L, state=tuple(layer_state), return_state=True)
+                    h, residual, L, state=tuple(layer_state), return_state=True,
+                    conv_out=None if conv_out is None else conv_out[idx])
             else:
                 h, residual, _ = layer.forward_padded(h, residual, L, ssm_state=layer_state)
             if new_states is not None:
@@ -538,7 +540,8 @@ class PretrainVideoMamba(nn.Module):
         feats, _, st = self._encode(x, mask, ssm_state, temporal_pos_offset, tpos=tpos)
         return feats if ssm_state is None else (feats, st)
 
-    def _encode(self, x, mask, ssm_state, temporal_pos_offset, tpos=None, pool=None):
+    def _encode(self, x, mask, ssm_state, temporal_pos_offset, tpos=None, pool=None,
+                conv_out=None):
         """(features (B, N_vis, C), x_pool | None, state result | None)."""
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
         h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset, tpos=tpos)
@@ -551,7 +554,7 @@ class PretrainVideoMamba(nn.Module):
             h = torch.zeros((Bsz, round_up(L), self.embed_dim), dtype=h.dtype, device=h.device)
             h[:, :L] = gathered
 
-        h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state)
+        h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state, conv_out)
         feats, x_pool = self._final_norm_pool(h, residual, L, has_cls, visible, pool)
 
         if new_states is not None and isinstance(new_states, list):
