@@ -272,9 +272,9 @@ def test_scan_workspace_query_without_gpu():
     # an explicit segment request (the ABI's only configuration argument) is honoured
     one = lib.vm_selective_scan_workspace_bytes(2, 64, 100, 16, 1)
     four = lib.vm_selective_scan_workspace_bytes(2, 64, 100, 16, 4)
-    # max of the chunked form (one 8-segment block: 9 x 64 x 17 + 64 x 16 floats per batch
-    # row) and the legacy summary / carry / final form (4 x 64 x 33 floats per batch row)
-    chunked = 2 * (9 * 64 * 17 + 64 * 16) * 4
+    # max of the chunked form (one 8-segment block: 9 x 64 x 17 floats per batch row) and
+    # the legacy summary / carry / final form (4 x 64 x 33 floats per batch row)
+    chunked = 2 * (9 * 64 * 17) * 4
     legacy = 2 * 4 * 64 * (2 * 16 + 1) * 4
     assert one == 0 and four == max(chunked, legacy)
 

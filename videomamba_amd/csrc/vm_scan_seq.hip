@@ -451,9 +451,11 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
 //     sum to LDS; the workgroup composes its 8 segments there (wave w owns states 2w, 2w+1)
 //     -> every segment's entry offset E_j and delta prefix P_j relative to the block entry,
 //     and the block aggregate (H, S) -> workspace.
-//   carry : per (b, d, n) the block entries H_blk, sequentially over the blocks (h0 first).
-//   PASS 2: segment j enters at exp2(A P_j) H_blk + E_j and runs its T steps emitting y
-//     (and h_last at the end of the sequence).
+//   PASS 2: the workgroup first walks the block aggregates before it from h0 to its block
+//     entry H_blk (wave w: states 2w, 2w+1; shared through LDS), then segment j enters at
+//     exp2(A P_j) H_blk + E_j and runs its T steps emitting y (and h_last at the end of the
+//     sequence).  (A separate carry launch between the passes cost ~5 us + a kernel
+//     boundary per layer at B = 1.)
 // Per step the math is the single-pass kernel's packed-pair recurrence in log2 units
 // (delta' = softplus(x) log2e, states h' = h log2e), B_t / C_t rows as scalar loads.
 // Compared with the summary / carry / final form it replaces for SGPR-eligible operands,
@@ -465,7 +467,6 @@ struct ChunkWork {
   float* segP;  // [B][nblk][kChW][D]         delta' prefixes
   float* aggH;  // [B][nblk][D][kMaxN]        block end states from a zero entry
   float* aggS;  // [B][nblk][D]               block delta' sums
-  float* blkH;  // [B][nblk][D][kMaxN]        block entry states (scan_chunk_carry_kernel)
   int T;        // steps per segment
   int nblk;     // blocks per sequence
 };
@@ -508,17 +509,27 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const float An1 = n0 + 1 < N ? ps.A[d * N + n0 + 1] : 0.0f;
 
   // PASS 2 entry operands: loaded together with everything else below, combined after
-  // the one wait (every global load of the wave's start-up is a single round trip)
-  float Pj = 0.0f;
-  f2 Ej[kMaxN / 2], Hb[kMaxN / 2];
+  // the one wait (every global load of the wave's start-up is a single round trip),
+  // including the block aggregates the block entry is walked from
+  constexpr int kCW = 16;  // block aggregates loaded with the start-up round
+  float Pj = 0.0f, H0 = 0.0f, H1 = 0.0f;
+  f2 Ej[kMaxN / 2];
+  float cS[kCW], cH0[kCW], cH1[kCW];
   if constexpr (PASS == 2) {
     Pj = w.segP[rowE + wave * D + d];
     const float* ep = &w.segE[(rowE + wave * D + d) * kMaxN];
-    const float* hp = &w.blkH[(rowA + blk * D + d) * kMaxN];
 #pragma unroll
-    for (int q = 0; q < kMaxN / 2; ++q) {
-      Ej[q] = *reinterpret_cast<const f2*>(&ep[2 * q]);
-      Hb[q] = *reinterpret_cast<const f2*>(&hp[2 * q]);
+    for (int q = 0; q < kMaxN / 2; ++q) Ej[q] = *reinterpret_cast<const f2*>(&ep[2 * q]);
+    if (ps.h0) {
+      if (n0 < N) H0 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0, p.h0_dtype);
+      if (n0 + 1 < N) H1 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + 1, p.h0_dtype);
+    }
+#pragma unroll
+    for (int j = 0; j < kCW; ++j) {
+      const long long row = rowA + static_cast<long long>(j < blk ? j : 0) * D + d;
+      cS[j] = w.aggS[row];
+      cH0[j] = w.aggH[row * kMaxN + n0];
+      cH1[j] = w.aggH[row * kMaxN + n0 + 1];
     }
   }
 
@@ -591,12 +602,31 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // one wait for every start-up load (parameters, entry operands, prologue): left pending
   // they would merge into the step loop's header waits
   __builtin_amdgcn_s_waitcnt(0);
-  if constexpr (PASS == 2) {  // this segment's entry: exp2(A P_j) * H_blk + E_j
+  if constexpr (PASS == 2) {
+    H0 *= kLog2e;  // log2 units
+    H1 *= kLog2e;
+#pragma unroll
+    for (int j = 0; j < kCW; ++j) {
+      if (j < blk) {
+        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * cS[j]), H0, cH0[j]);
+        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * cS[j]), H1, cH1[j]);
+      }
+    }
+    for (int k = kCW; k < blk; ++k) {  // long sequences: the remaining blocks, one by one
+      const long long row = rowA + static_cast<long long>(k) * D + d;
+      const float Sk = w.aggS[row];
+      H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sk), H0, w.aggH[row * kMaxN + n0]);
+      H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sk), H1, w.aggH[row * kMaxN + n0 + 1]);
+    }
+    sH[0][n0][lane] = H0;
+    sH[0][n0 + 1][lane] = H1;
+    __syncthreads();
+    // this segment's entry: exp2(A P_j) * H_blk + E_j
 #pragma unroll
     for (int q = 0; q < kMaxN / 2; ++q) {
       const f2 x = A2[q] * f2{Pj, Pj};
-      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), Hb[q].x, Ej[q].x),
-                fmaf(__builtin_amdgcn_exp2f(x.y), Hb[q].y, Ej[q].y)};
+      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), sH[0][2 * q][lane], Ej[q].x),
+                fmaf(__builtin_amdgcn_exp2f(x.y), sH[0][2 * q + 1][lane], Ej[q].y)};
     }
   }
   for (int tg = t_beg; tg < t_end; tg += kPF) {
@@ -693,45 +723,6 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
                       ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * kLn2f);
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
-    }
-  }
-}
-
-// Block entries of the chunked form: H_0 = h0 (log2 units), H_{k+1} = exp2(A S_k) H_k + agg_k.
-// One thread per (b, d, n); the aggregates stream through an 8-deep register window.
-__global__ __launch_bounds__(256) void scan_chunk_carry_kernel(const ScanParams p, const ChunkWork w) {
-  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
-  if (i >= total) return;
-  const int n = static_cast<int>(i % kMaxN);
-  const long long bd = i / kMaxN;  // b * dim + d
-  const int d = static_cast<int>(bd % p.dim);
-  const int b = static_cast<int>(bd / p.dim);
-  const int N = p.dstate;
-  const bool hi = b >= p.split;  // second parameter set of a paired scan
-  const float* Ap = hi ? p.A_hi : p.A;
-  const void* h0 = hi ? p.h0_hi : p.h0;
-  const int hb = hi ? b - p.split : b;
-  const float A = n < N ? Ap[d * N + n] : 0.0f;
-  float H = (n < N && h0) ? load_dyn(h0, hb * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * kLog2e : 0.0f;
-  const long long D = p.dim;
-  const long long row0 = static_cast<long long>(b) * w.nblk * D + d;  // + k * D
-  constexpr int kWin = 32;  // typically all blocks in one round of loads
-  for (int k0 = 0; k0 < w.nblk; k0 += kWin) {
-    float sk[kWin], hk[kWin];
-#pragma unroll
-    for (int j = 0; j < kWin; ++j) {
-      const long long row = row0 + static_cast<long long>(min(k0 + j, w.nblk - 1)) * D;
-      sk[j] = w.aggS[row];
-      hk[j] = w.aggH[row * kMaxN + n];
-    }
-#pragma unroll
-    for (int j = 0; j < kWin; ++j) {
-      const int k = k0 + j;
-      if (k < w.nblk) {
-        w.blkH[(row0 + static_cast<long long>(k) * D) * kMaxN + n] = H;
-        H = fmaf(__builtin_amdgcn_exp2f(A * sk[j]), H, hk[j]);
-      }
     }
   }
 }
@@ -876,8 +867,7 @@ static void chunk_geometry(int seqlen, int S, int* T, int* nblk) {
 static size_t chunk_bytes(int batch, int dim, int seqlen, int S) {
   int T, nblk;
   chunk_geometry(seqlen, S, &T, &nblk);
-  const size_t per_blk = static_cast<size_t>(kChW + 1) * dim * (kMaxN + 1) +
-                         static_cast<size_t>(dim) * kMaxN;  // + block entries
+  const size_t per_blk = static_cast<size_t>(kChW + 1) * dim * (kMaxN + 1);
   return static_cast<size_t>(batch) * nblk * per_blk * sizeof(float);
 }
 
@@ -909,9 +899,6 @@ static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t 
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
   hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
                      p, w);
-  const long long total = static_cast<long long>(p.batch) * p.dim * kMaxN;
-  hipLaunchKernelGGL(scan_chunk_carry_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
-                     dim3(256), 0, s, p, w);
   hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
                      p, w);
 }
@@ -957,7 +944,6 @@ void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
     w.segP = w.segE + nb * kChW * p.dim * kMaxN;
     w.aggH = w.segP + nb * kChW * p.dim;
     w.aggS = w.aggH + nb * p.dim * kMaxN;
-    w.blkH = w.aggS + nb * p.dim;
     if (dtype == VM_DTYPE_BF16) launch_chunk<bf16_t>(p, w, s);
     else launch_chunk<float>(p, w, s);
     return;
