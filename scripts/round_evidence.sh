@@ -3,16 +3,21 @@
 # command, kernel stats of the scan microbench alone at the bench shape (the roofline
 # kernel), FETCH_SIZE / WRITE_SIZE / SQ counter passes on that microbench, the same
 # FETCH/WRITE passes on a calibration kernel with the scan's access pattern and a known byte
-# count (tools/probes/scan_lab calib), and the C5 long-video run.
+# count (tools/probes/scan_lab calib), the C5 long-video run and the B=1 graph-replay chunk
+# profile.  PART=1: bench + its profile; PART=2: the rest (one gpurun call each).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-R=${ROUND:-r01}
+R=${ROUND:-r02}
 B=${BATCH:-336}
 O=gpurun_out/$R
 mkdir -p $O
-timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail $O/bench.err; exit 1; }
+if [ "${PART:-1}" = 1 ]; then
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --no-cpu-baseline > $O/prof_bench.log 2>&1 || { echo prof failed; tail $O/prof_bench.log; exit 1; }
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --no-cpu-baseline > $O/prof_bench.log 2>&1 || { echo prof failed; tail $O/prof_bench.log; exit 1; }
+echo part 1 done
+exit 0
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_scan -o scan -- python scripts/bench_scan.py --batches $B --reps 20 > $O/prof_scan.log 2>&1 || { echo scan prof failed; tail $O/prof_scan.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
   tag=$(echo $c | cut -d' ' -f1)
@@ -23,4 +28,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -k 10 600 python scripts/bench_long_video.py > $O/long_video.json 2> $O/long_video.err || { echo long video failed; tail $O/long_video.err; exit 1; }
 cat $O/long_video.json
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_b1_graph -o run -- python -u scripts/diag/b1_chunk_graph.py 20 > $O/prof_b1_graph.log 2>&1 || { echo b1 prof failed; tail $O/prof_b1_graph.log; exit 1; }
+grep "graph replays" $O/prof_b1_graph.log
 echo evidence done

@@ -791,6 +791,36 @@ def test_graph_replay_survives_workspace_growth_and_weight_reload():
         torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
+def test_graph_replay_after_parameter_object_replaced_needs_invalidate():
+    """Replacing a Parameter object outright is not a version / data_ptr change of the
+    captured tensors: StreamingChunkGraph.invalidate() re-scans and re-captures, and the
+    replay then equals the eager forward with the new weight.  The streaming state keeps
+    advancing across runs (the stacked conv-state carry)."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    torch.manual_seed(3)
+    model = _small_model(img_size=32, patch_size=16, depth=2, embed_dim=64, fused_add_norm=True,
+                         rms_norm=True, residual_in_fp32=True, num_frames=4, pool_type="avg",
+                         add_pool_norm=False).to(DEV).eval()
+    x1, x2 = torch.randn(2, 1, 3, 2, 32, 32, device=DEV)
+    runner = StreamingChunkGraph(model, batch=1, frames=2, height=32, width=32)
+    with torch.no_grad():
+        runner.run(x1, temporal_pos_offset=0)
+        mx = model.layers[1].mixer
+        mx.out_proj.weight = torch.nn.Parameter(mx.out_proj.weight.detach() * 1.5)
+        runner.invalidate()
+        runner.reset_state()
+        g1 = runner.run(x1, temporal_pos_offset=0).clone()
+        g2 = runner.run(x2, temporal_pos_offset=1).clone()
+        state = model.allocate_state(1, device=DEV)
+        e1, state = model(x1, ssm_state=state, temporal_pos_offset=0)
+        e2, state = model(x2, ssm_state=state, temporal_pos_offset=1)
+    torch.testing.assert_close(g1, e1, rtol=0, atol=0)
+    torch.testing.assert_close(g2, e2, rtol=0, atol=0)
+    for (c, s), (ce, se) in zip(runner.state, state):
+        torch.testing.assert_close(c, ce, rtol=0, atol=0)
+        torch.testing.assert_close(s, se, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("Bsz,L,cut", [(1, 3137, 1569), (3, 301, 130), (2, 70, 3)])
 def test_conv_proj_cm_chunk_invariant_bitwise(Bsz, L, cut):
     """vm_conv_proj_cm_fwd's per-token outputs do not depend on the sequence length: u,

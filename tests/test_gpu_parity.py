@@ -496,6 +496,42 @@ def test_conv_proj_delta_softplus_epilogue():
     assert err <= 2.0 ** -8, err
 
 
+def test_conv_proj_split_k_conv_state_out():
+    """The split-K form writes the new conv state from its staged tile rows (and the old
+    state's taps for sequences shorter than the kernel): the last d_conv raw inputs of
+    [conv_state | x] per channel (mamba_simple.py:383-399), bit-equal to the wide kernel's
+    separate launch, for long and shorter-than-width sequences and several batch rows."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(5)
+    m = Mamba(d_model=576, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    _, _, _, cw, cb = m._fp32_params()
+    wx_pad, wdt_pad = m._padded_proj_weights()
+    st = torch.cuda.current_stream().cuda_stream
+    for L in (2, 61, 777):
+        Lp = (L + 7) // 8 * 8
+        xz9 = torch.randn(9, Lp, 2 * Dm, device=DEV).to(torch.bfloat16)
+        xz9[:, L:] = 0
+        cs9 = torch.randn(9, Dm, W, device=DEV).to(torch.bfloat16)
+        got = []
+        for bsz in (9, 3):  # wide kernel, split-K form
+            n = bsz * Lp
+            xz = xz9[:bsz].reshape(n, 2 * Dm).contiguous()
+            cs = cs9[:bsz].contiguous()
+            cso = torch.full((bsz, Dm, W), float("nan"), device=DEV, dtype=torch.bfloat16)
+            u = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+            xd = torch.empty(n, E, device=DEV, dtype=torch.bfloat16)
+            dt = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+            K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, (Dm * W, W), cso,
+                            (Dm * W, W), wx_pad, E, wdt_pad, R, u, (Lp * Dm, Dm), xd,
+                            (Lp * E, E), dt, (Lp * Dm, Dm), Lp, bsz, Dm, L, W, st)
+            got.append(cso[:3])
+        torch.cuda.synchronize()
+        want = torch.cat([cs9[:3], xz9[:3, :L, :Dm].transpose(1, 2)], dim=-1)[..., -W:]
+        assert torch.equal(got[0], want), L
+        assert torch.equal(got[1], want), L
+
+
 @pytest.mark.parametrize("d_model", [576, 96])
 def test_conv_proj_split_k_matches_wide_kernel(d_model):
     """vm_conv_proj_fwd runs the split-K form (fixed 128-channel splits of the x_proj
