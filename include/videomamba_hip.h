@@ -25,6 +25,8 @@
  *                                 per-frame / whole-clip column sums of the pooling
  *   vm_pool_finish_fwd         <- the pooling tail: means, CLS add / concat and pool_norm
  *                                 LayerNorm (videomamba.py:983-1062, :702-751 masked)
+ *   vm_linear_fwd              <- the mixer's in_proj / out_proj nn.Linear at one clip's
+ *                                 token count (mamba_simple.py:333-339, :445-446)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
  *                                 (videomamba.py:359-368, :806-815)
  *
@@ -279,6 +281,16 @@ int vm_pool_finish_fwd(const void* workspace, int batch, int groups, int group_r
                        long long cls_batch_stride, int mode, int keep_temporal,
                        const float* ln_weight, const float* ln_bias, float ln_eps,
                        void* x_pool, int xp_dtype, int cols, vm_stream_t stream);
+
+/*
+ * out (m, n) = x (m, k) @ w (n, k)^T (+ bias (n), fp32, nullable): bf16 operands, fp32
+ * accumulation, rows K-contiguous with leading dimensions ldx / ldw / ldo (elements).
+ * n, k and the leading dimensions multiples of 8, 16-byte aligned operands.  Each output
+ * row is computed in the same order for every m (sequence-length independent).
+ */
+int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
+                  const float* bias, void* out, long long ldo, int m, int n, int k, int dtype,
+                  vm_stream_t stream);
 
 /*
  * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,P,P)):

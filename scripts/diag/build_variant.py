@@ -12,6 +12,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # small-M GEMM with 64-row tiles at every shape
+    "lin64": [("vm_gemm.hip", "  const bool big = (long long)((m + 127) / 128) * nt >= 384;",
+               "  const bool big = false;")],
+    # split-K conv_proj single-tile latency: only token tile 0 (9 workgroups) of each kernel
+    "cx_onetile": [("vm_conv_proj_sk.hip", "  dim3 g1(tiles, q.nsplit);", "  dim3 g1(1, q.nsplit);"),
+                   ("vm_conv_proj_sk.hip", "  const dim3 g2(tiles, cblocks);",
+                    "  const dim3 g2(1, cblocks);")],
+    # no conv + SiLU math (u tile = raw x); no x_proj MFMA
+    "cx_noconv": [("vm_conv_proj_sk.hip", "      const bool live = step < p.seqlen && tok < q.ntok && cact;",
+                   "      const bool live = step < p.seqlen && tok < q.ntok && cact;\n      al = bl; ah = bh;")],
+    "cx_nomfma": [("vm_conv_proj_sk.hip",
+                   "  for (int ks = 0; ks < 4; ++ks) {\n    const bf16x8 av = *reinterpret_cast<const bf16x8*>(\n        &sU[(wave",
+                   "  for (int ks = 0; ks < 0; ++ks) {\n    const bf16x8 av = *reinterpret_cast<const bf16x8*>(\n        &sU[(wave")],
+    # split-K conv_proj pricing (results wrong): no x_proj partial stores / no u stores /
+    # no x tile loads
+    "cx_nopart": [("vm_conv_proj_sk.hip", "      if (e < p.e) dst[e] = acc[j][rr];",
+                   "      if (e < p.e && acc[j][rr] == 1234.5f) dst[e] = acc[j][rr];")],
+    "cx_nou": [("vm_conv_proj_sk.hip", "  if (cact) {\n#pragma unroll\n    for (int i = 0; i < 16; ++i) {\n      const int tok = tok0 + t0 + i;",
+                "  if (cact && tok0 < 0) {\n#pragma unroll\n    for (int i = 0; i < 16; ++i) {\n      const int tok = tok0 + t0 + i;")],
+    "cx_noload": [("vm_conv_proj_sk.hip", "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch)",
+                   "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch && tok0 < 0)")],
     # timing probe: every step reads the segment's first B/C row (L1/K$-resident), so the
     # chunk kernel's time without the per-step scalar-load latency shows (results wrong)
     "bc_fixed": [("vm_scan_seq.hip",

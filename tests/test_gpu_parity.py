@@ -577,3 +577,43 @@ def test_conv_proj_split_k_matches_wide_kernel(d_model):
     ref_u, _ = orc.causal_conv1d(xz9[:1, :L, :Dm].transpose(1, 2).cpu(), cw.cpu(), cb.cpu(), True,
                                  cs9[:1].cpu())
     _close(u1[:L].t().unsqueeze(0), ref_u, 1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(3144, 2304, 576), (3144, 576, 1152), (1, 576, 1152),
+                                   (77, 2304, 576), (600, 64, 192), (5000, 136, 384)])
+def test_small_m_linear_matches_fp32_reference(m, n, k):
+    """vm_linear_fwd (the B = 1 in_proj / out_proj GEMM) against an fp32 torch reference of
+    the same bf16 operands: within one bf16 rounding of the output (fp32 accumulation in
+    another order).  Rows are independent of m (bit-equal on a prefix: the chunk-invariance
+    property), and a column-sliced output view gets the same bits."""
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) * k ** -0.5).to(torch.bfloat16)
+    y = K.linear(x, w)
+    ref = x.float() @ w.float().t()
+    assert ((y.float() - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-3).all()
+    p = min(m, 37)
+    assert torch.equal(K.linear(x[:p].contiguous(), w), y[:p])
+    out = torch.full((m, 2 * n), 7.0, device=DEV, dtype=torch.bfloat16)
+    K.linear(x, w, out=out[:, n:])
+    assert torch.equal(out[:, n:], y) and (out[:, :n] == 7.0).all()
+
+
+def test_b1_mixer_projections_run_on_the_hip_gemm():
+    """At one clip's token count the mixer's out_proj takes vm_linear_fwd (the native path;
+    in_proj's N = 2304 stays on the library GEMM, faster there), and the mixer output matches
+    the library-GEMM path within bf16 rounding."""
+    from videomamba_amd.mamba_simple import Mamba, _small_gemm_ok
+    torch.manual_seed(0)
+    m = Mamba(d_model=576, layer_idx=0).to(DEV, torch.bfloat16).eval()
+    x = torch.randn(1, 3137, 576, device=DEV).to(torch.bfloat16)
+    hp = torch.zeros(1, 3144, 576, device=DEV, dtype=torch.bfloat16)
+    assert not _small_gemm_ok(hp.view(3144, 576), m.in_proj.weight, None)
+    y = torch.zeros(3144, 1152, device=DEV, dtype=torch.bfloat16)
+    assert _small_gemm_ok(y, m.out_proj.weight, None)
+    with torch.no_grad():
+        y_hip = m(x)
+        with options.override(small_gemm_rows=0):
+            y_lib = m(x)
+    rel = ((y_hip.float() - y_lib.float()).norm() / y_lib.float().norm()).item()
+    assert rel < 1e-2, rel

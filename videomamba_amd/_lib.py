@@ -88,6 +88,7 @@ _SIGNATURES = {
         [_P, _I, _I, _I, _P, _I,                  # workspace, batch, groups, rows, bounds, max
          _P, _I, _LL, _I, _I,                     # cls, dtype, stride, mode, keep_temporal
          _P, _P, c_float, _P, _I, _I, _P], _I),   # LN w / b / eps, x_pool, dtype, cols
+    "vm_linear_fwd": ([_P, _LL, _P, _LL, _P, _P, _LL, _I, _I, _I, _I, _P], _I),
     "vm_patch_embed_fwd": (
         [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
 }

@@ -26,6 +26,7 @@ struct ConvProjTmArgs {
 // never on the sequence length, so a sequence run in chunks sees the same arithmetic as
 // the full-sequence run (chunked == full bitwise).
 constexpr int kSkMaxBatch = 8;
+constexpr int kSkMaxEp = 76;  // round_up(R + 2N, 4) the split-K form stages per token row
 long long conv_proj_sk_workspace_bytes(int batch, int out_len, int dim, int e);
 void conv_proj_sk_launch(const ConvProjTmArgs& a, float* part, hipStream_t s);
 

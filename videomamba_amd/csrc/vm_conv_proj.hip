@@ -408,8 +408,8 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   // skips it (conv + x_proj only: a consumer that projects dt itself)
   const bool fused_dt = dt != nullptr;
   const bool spd = dt_softplus != 0;
-  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= 80 && r_pad <= 80 &&
-      out_len >= 8) {
+  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= kSkMaxEp &&
+      r_pad <= 80 && out_len >= 8) {
     // small batch: the split-K form (vm_conv_proj_sk.hip) fills the chip and keeps the
     // x_proj reduction order fixed per token
     const long long need = conv_proj_sk_workspace_bytes(batch, out_len, dim, e);

@@ -328,11 +328,14 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
     if (i < NB * 16 * 16 && qd * 8 < nch)
       wv[k] = *reinterpret_cast<const uint4*>(p.wx + (long long)e * p.dim + c0 + qd * 8);
   }
+  // taps right-aligned to 4 (a width-W filter is a 4-tap filter with 4 - W leading zeros),
+  // so tap k of token i always reads window row i + k
   float wl[4], wh[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    wl[k] = k < W ? p.cw[c * W + k] : 0.0f;
-    wh[k] = k < W ? p.cw[(c + 1) * W + k] : 0.0f;
+    static_assert(4 * 16 * kSkMaxEp * 4 <= 72 * kTmPitch * 2, "partial rows exceed the x tile");
+    wl[k] = k >= 4 - W ? p.cw[c * W + k - (4 - W)] : 0.0f;
+    wh[k] = k >= 4 - W ? p.cw[(c + 1) * W + k - (4 - W)] : 0.0f;
   }
   const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
   // old conv-state taps (steps -3 .. -1) of every sequence whose first steps fall in this
@@ -387,47 +390,70 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
     }
   }
   // ---- conv + SiLU: channels c, c + 1 (one packed word), tokens 16w .. 16w+15 ----
+  // The wave's 16 tokens read a 19-row window, loaded from LDS up front (a uniform branch
+  // per tap made every token a chain of LDS round trips: 7.6 us of the kernel at B = 1).
+  // Tokens in the first 3 steps of their sequence are redone below with the taps before
+  // the sequence (old conv state staged in sC, or zeros).
   const int t0 = wave * 16;
-  uint32_t upk[16];
-  {
-    int b = (tok0 + t0) / p.out_len;
-    int step = tok0 + t0 - b * p.out_len;
+  uint32_t xw[19];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i > 0 && ++step == p.out_len) {  // next batch row (out_len >= 8: at most 2 wraps)
-        step = 0;
-        ++b;
-      }
-      const int tok = tok0 + t0 + i;
+  for (int r = 0; r < 19; ++r)
+    xw[r] = *reinterpret_cast<const uint32_t*>(&sX[(kCmHalo + t0 - 3 + r) * kTmPitch + 2 * lane]);
+  const int bw = (tok0 + t0) / p.out_len;  // batch row and step of the wave's first token
+  const int sw = tok0 + t0 - bw * p.out_len;
+  auto token_pos = [&](int i, int& b, int& st) {  // out_len >= 8: at most 2 wraps in 16
+    b = bw;
+    st = sw + i;
+    if (st >= p.out_len) { st -= p.out_len; ++b; }
+    if (st >= p.out_len) { st -= p.out_len; ++b; }
+  };
+  auto pack = [&](float al, float ah, bool live) -> uint32_t {
+    const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
+    const float uh = live ? ah * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-ah * kLog2e)) : 0.0f;
+    return static_cast<uint32_t>(from_f32<bf16_t>(ul)) |
+           (static_cast<uint32_t>(from_f32<bf16_t>(uh)) << 16);
+  };
+  uint32_t upk[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float al = bl, ah = bh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      al = fmaf(wl[k], __uint_as_float(xw[i + k] << 16), al);
+      ah = fmaf(wh[k], __uint_as_float(xw[i + k] & 0xffff0000u), ah);
+    }
+    int b, st;
+    token_pos(i, b, st);
+    upk[i] = pack(al, ah, st < p.seqlen && tok0 + t0 + i < q.ntok && cact);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    int b, st;
+    token_pos(i, b, st);
+    if (st < 3) {  // uniform: a sequence starts at or just before this token
       float al = bl, ah = bh;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (k < W) {
-          const int j = step - (W - 1) + k;  // input step in the virtual sequence
-          float vl = 0.0f, vh = 0.0f;
-          if (j >= 0) {
-            const uint32_t wd = *reinterpret_cast<const uint32_t*>(
-                &sX[(kCmHalo + t0 + i - (W - 1) + k) * kTmPitch + 2 * lane]);
-            vl = __uint_as_float(wd << 16);
-            vh = __uint_as_float(wd & 0xffff0000u);
-          } else if (p.csi && tok < q.ntok) {  // taps before the sequence start (staged)
+        const int j = st - 3 + k;  // input step in the virtual sequence
+        float vl = __uint_as_float(xw[i + k] << 16), vh = __uint_as_float(xw[i + k] & 0xffff0000u);
+        if (j < 0) {
+          vl = vh = 0.0f;
+          if (p.csi && tok0 + t0 + i < q.ntok && k >= 4 - W) {
             const float2 cs = *reinterpret_cast<const float2*>(
                 &sC[((b - b_lo) * 3 - j - 1) * kSkCh + 2 * lane]);
             vl = cs.x;
             vh = cs.y;
           }
-          al = fmaf(wl[k], vl, al);
-          ah = fmaf(wh[k], vh, ah);
         }
+        al = fmaf(wl[k], vl, al);
+        ah = fmaf(wh[k], vh, ah);
       }
-      const bool live = step < p.seqlen && tok < q.ntok && cact;
-      const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
-      const float uh = live ? ah * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-ah * kLog2e)) : 0.0f;
-      upk[i] = static_cast<uint32_t>(from_f32<bf16_t>(ul)) |
-               (static_cast<uint32_t>(from_f32<bf16_t>(uh)) << 16);
-      *reinterpret_cast<uint32_t*>(&sU[(t0 + i) * kTmPitch + 2 * lane]) = upk[i];
+      upk[i] = pack(al, ah, st < p.seqlen && tok0 + t0 + i < q.ntok && cact);
     }
   }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    *reinterpret_cast<uint32_t*>(&sU[(t0 + i) * kTmPitch + 2 * lane]) = upk[i];
   __syncthreads();
   // ---- x_proj partial: wave = tokens 16w .. 16w+15 x all e_pad columns, K = 128 ----
   f32x4 acc[NB];
@@ -452,17 +478,26 @@ __global__ __launch_bounds__(256) void conv_xproj_tm_kernel(const SkTmParams q) 
       if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c) = upk[i];
     }
   }
-  // D[token 4(lane/16) + r][column lane % 16]: part[split][token][e], 64-B row pieces
+  // partials: D[token 4(lane/16) + r][column lane % 16] through this wave's own rows of the
+  // (now unused) x tile, then whole part[split][token][0 .. ep) rows as 16-byte stores
+  // (20 scattered 4-byte stores per lane were 4.6 us of the kernel at B = 1)
+  constexpr int kPP = kSkMaxEp;  // fp32 pitch of the staged rows: 4 x 16 rows fit the x tile
+  float* sP = reinterpret_cast<float*>(sX) + wave * 16 * kPP;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int tok = tok0 + wave * 16 + (lane >> 4) * 4 + rr;
-    if (tok >= q.ntok) continue;
-    float* dst = q.part + ((long long)split * q.ntok + tok) * q.ep;
+  for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int e = j * 16 + (lane & 15);
-      if (e < p.e) dst[e] = acc[j][rr];
+      if (e < q.ep) sP[((lane >> 4) * 4 + rr) * kPP + e] = acc[j][rr];
     }
+  __builtin_amdgcn_wave_barrier();
+  const int nq = q.ep >> 2;  // float4 per row
+  for (int i = lane; i < 16 * nq; i += 64) {
+    const int r = i / nq, qd = i - r * nq;
+    const int tok = tok0 + wave * 16 + r;
+    if (tok < q.ntok)
+      *reinterpret_cast<float4*>(q.part + ((long long)split * q.ntok + tok) * q.ep + 4 * qd) =
+          *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd]);
   }
 }
 

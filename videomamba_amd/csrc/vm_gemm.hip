@@ -1,0 +1,225 @@
+// Small-M projection GEMM for the streaming-chunk latency path: out = x @ w^T (+ bias),
+// bf16 operands, fp32 accumulation on v_mfma_f32_16x16x32_bf16, bf16 out.  Replaces the
+// mixer's in_proj / out_proj nn.Linear calls (mamba_simple.py:333-339, :445-446) when the
+// token count is one clip's (B = 1: M = 3144 rows).  There the library's 256x128 tiles give
+// ~1 workgroup per CU and each walks the whole K serially (14-15 us per projection);
+// 128x128 / 64x128 tiles put 2-4 workgroups on every CU.
+//
+// Layout: x (m, k) and w (n, k) both K-contiguous (the nn.Linear layouts), out (m, n).
+// A workgroup (4 waves, 2 x 2) owns a BM x 128 output tile and walks K in 64-wide steps:
+// A / W pieces are fetched two steps ahead into two register slots while the current
+// step's MFMAs run from LDS (double-buffered, one barrier per step).  The tile leaves
+// through LDS as 16-byte row stores.  Each output row's dot products run in the same order
+// whatever m is, so a row's bits do not depend on the sequence length (chunked == full).
+
+#include "vm_common.h"
+
+namespace vm {
+
+typedef __attribute__((__vector_size__(8 * sizeof(short)))) short bf16x8_t;
+typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32x4_t;
+
+struct LinParams {
+  const bf16_t* x; long long ldx;
+  const bf16_t* w; long long ldw;
+  const float* bias;
+  bf16_t* out; long long ldo;
+  int m, n, k;
+};
+
+constexpr int kLinBN = 128;
+constexpr int kLinBK = 64;
+constexpr int kLinPitch = 72;  // bf16 per staged row: 64 + 8 pad (144 B)
+
+template <int BM, int NK>  // NK = k / 64 K-steps, fully unrolled (straight-line prefetch)
+__global__ __launch_bounds__(256) void linear_kernel(const LinParams p) {
+  constexpr int BN = kLinBN, BK = kLinBK, PITCH = kLinPitch;
+  constexpr int WM = BM / 2, WN = BN / 2;  // wave tile
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int KQ = BK / 8;                                      // 16-B pieces per row
+  constexpr int AP = BM * KQ / 256, BP = BN * KQ / 256;           // pieces per thread
+  constexpr int kStage = (BM + BN) * PITCH;                       // bf16 per LDS stage
+  constexpr int kOutPitch = BN + 8;
+  static_assert(BM * kOutPitch <= 2 * kStage, "output tile must fit the staging buffers");
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];   // [2][kStage]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  constexpr int nk = NK;
+
+  // Operands come in through buffer loads: rows past m (or n) fall outside the buffer's
+  // byte range and read as 0 with no branch, so every load of a step is issued back to back
+  // and waited for only where its registers go to LDS.  Two register slots: the loads for
+  // step s are issued at the top of step s - 2 and land in LDS at the end of step s - 1.
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.x), 0, static_cast<int>((long long)p.m * p.ldx * 2), 0x00020000);
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.w), 0, static_cast<int>((long long)p.n * p.ldw * 2), 0x00020000);
+  typedef __attribute__((__vector_size__(4 * sizeof(int)))) int i32x4_t;
+  i32x4_t ra0[AP], rb0[BP], ra1[AP], rb1[BP];
+  auto gload = [&](int kt, i32x4_t (&a)[AP], i32x4_t (&b)[BP]) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int pc = tid + 256 * i, row = pc / KQ, kq = pc % KQ;
+      const int off = ((m0 + row) * static_cast<int>(p.ldx) + k0 + kq * 8) * 2;
+      a[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int pc = tid + 256 * i, row = pc / KQ, kq = pc % KQ;
+      const int off = ((n0 + row) * static_cast<int>(p.ldw) + k0 + kq * 8) * 2;
+      b[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf, const i32x4_t (&a)[AP], const i32x4_t (&b)[BP]) {
+    bf16_t* sA = smem + buf * kStage;
+    bf16_t* sB = sA + BM * PITCH;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int pc = tid + 256 * i;
+      *reinterpret_cast<i32x4_t*>(&sA[(pc / KQ) * PITCH + (pc % KQ) * 8]) = a[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int pc = tid + 256 * i;
+      *reinterpret_cast<i32x4_t*>(&sB[(pc / KQ) * PITCH + (pc % KQ) * 8]) = b[i];
+    }
+  };
+  // workgroup barrier that waits only for this wave's LDS traffic: __syncthreads() also
+  // drains vmcnt, which would collapse the two-step prefetch to zero
+  auto lds_barrier = [&]() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const bf16_t* sA = smem + buf * kStage;
+    const bf16_t* sB = sA + BM * PITCH;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[TM], bw[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(
+            &sA[(wm * WM + i * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bw[j] = *reinterpret_cast<const bf16x8_t*>(
+            &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);
+      __builtin_amdgcn_sched_barrier(0);  // all fragment reads in flight before the MFMAs
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  gload(0, ra0, rb0);
+  if (nk > 1) gload(1, ra1, rb1);
+  lstore(0, ra0, rb0);
+  lds_barrier();
+#pragma unroll
+  for (int kt = 0; kt < nk; ++kt) {  // fully unrolled: slots and waits are static
+    // (sched_barrier: keep the step's loads at its top — the scheduler otherwise sinks
+    // them to the end of the step, which leaves one step of prefetch instead of two)
+    if (kt & 1) {
+      if (kt + 2 < nk) gload(kt + 2, ra1, rb1);  // slot 1 held step kt, already in LDS
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) lstore(0, ra0, rb0);
+    } else {
+      if (kt + 2 < nk) gload(kt + 2, ra0, rb0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) lstore(1, ra1, rb1);
+    }
+    lds_barrier();
+  }
+
+  // epilogue: D[4(lane/16) + r][lane % 16] of every 16x16 tile -> LDS -> 16-B row stores
+  // (the loop's last barrier has every wave past its final LDS reads)
+  bf16_t* sO = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WN + j * 16 + (lane & 15);
+      const float b = p.bias && n0 + col < p.n ? p.bias[n0 + col] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        sO[row * kOutPitch + col] = from_f32<bf16_t>(acc[i][j][r] + b);
+      }
+    }
+  __syncthreads();
+  constexpr int kPieces = BM * BN / 8;
+#pragma unroll
+  for (int i = 0; i < kPieces / 256; ++i) {
+    const int pc = tid + 256 * i, row = pc / (BN / 8), cq = pc % (BN / 8);
+    const int gm = m0 + row, gn = n0 + cq * 8;
+    if (gm < p.m && gn < p.n)
+      *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) =
+          *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+  }
+}
+
+}  // namespace vm
+
+using namespace vm;
+
+extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
+                             const float* bias, void* out, long long ldo, int m, int n, int k,
+                             int dtype, vm_stream_t stream) {
+  if (!x || !w || !out) {
+    vmhost::set_error("vm_linear_fwd: null required pointer");
+    return VM_E_INVALID;
+  }
+  if (dtype != VM_DTYPE_BF16 || m < 0 || n < 1 || k < kLinBK || n % 8 || k % kLinBK ||
+      ldx < k || ldw < k || ldo < n || ldx % 8 || ldw % 8 || ldo % 8 || !vmhost::aligned16(x) ||
+      !vmhost::aligned16(w) || !vmhost::aligned16(out) ||
+      (long long)m * ldx * 2 >= (1ll << 31) || (long long)n * ldw * 2 >= (1ll << 31)) {
+    vmhost::set_error("vm_linear_fwd: bf16 only; k a multiple of 64; n and the leading "
+                      "dimensions multiples of 8; 16-byte aligned operands under 2 GB");
+    return VM_E_INVALID;
+  }
+  if (m == 0) return VM_OK;
+  LinParams p{};
+  p.x = static_cast<const bf16_t*>(x); p.ldx = ldx;
+  p.w = static_cast<const bf16_t*>(w); p.ldw = ldw;
+  p.bias = bias; p.out = static_cast<bf16_t*>(out); p.ldo = ldo;
+  p.m = m; p.n = n; p.k = k;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nt = (n + kLinBN - 1) / kLinBN;
+  // 128-row tiles when that still gives >= 1.5 workgroups per CU (256 CUs), else 64-row
+  const bool big = (long long)((m + 127) / 128) * nt >= 384;
+  const int bm = big ? 128 : 64;
+  const dim3 grid((m + bm - 1) / bm, nt);
+  const size_t lds = 2 * (bm + kLinBN) * kLinPitch * sizeof(bf16_t);
+  switch (k / kLinBK) {
+#define VM_LIN(NKV)                                                                  \
+  case NKV:                                                                          \
+    if (big) hipLaunchKernelGGL((linear_kernel<128, NKV>), grid, dim3(256), lds, s, p); \
+    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p);    \
+    break;
+    VM_LIN(3) VM_LIN(6) VM_LIN(9) VM_LIN(12) VM_LIN(18) VM_LIN(24)
+#undef VM_LIN
+    default:
+      vmhost::set_error("vm_linear_fwd: k = %d (supported: 192, 384, 576, 768, 1152, 1536)", k);
+      return VM_E_INVALID;
+  }
+  return vmhost::launch_status("vm_linear_fwd");
+}

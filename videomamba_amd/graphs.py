@@ -69,6 +69,7 @@ class StreamingChunkGraph:
         self._pool = None
         self._param_key = None
         self._plist = None
+        self._tpos_offset = None  # temporal offset whose embedding slice static_tpos holds
         self._ws = None  # scan scratch owned by the captured graphs
 
     # ------------------------------------------------------------------ state
@@ -118,6 +119,7 @@ class StreamingChunkGraph:
         self._pool = None
         self._plist = None
         self._param_key = None
+        self._tpos_offset = None
 
     def _workspace(self) -> Tensor:
         """Kernel scratch (segmented scan, channel-major conv_proj partials) sized for the
@@ -166,15 +168,18 @@ class StreamingChunkGraph:
         has_cls = temporal_pos_offset <= 0
         if m.add_pool_norm:
             m._check_pool(has_cls)
-        tpos = m._get_temporal_pos_embedding(self.tt, offset=temporal_pos_offset,
-                                             dtype=self.dtype, device=self.device)
-        self.static_tpos.copy_(tpos)
-        self.static_x.copy_(x)
         key = self._params_key()
         if key != self._param_key:  # parameters changed since capture: capture again
             self._graphs.clear()
             self._pool = None
             self._param_key = key
+            self._tpos_offset = None
+        if temporal_pos_offset != self._tpos_offset:  # the slice only changes with the offset
+            tpos = m._get_temporal_pos_embedding(self.tt, offset=temporal_pos_offset,
+                                                 dtype=self.dtype, device=self.device)
+            self.static_tpos.copy_(tpos)
+            self._tpos_offset = temporal_pos_offset
+        self.static_x.copy_(x)
         if has_cls not in self._graphs:
             self._capture(has_cls)
         g, outs = self._graphs[has_cls]

@@ -258,6 +258,20 @@ def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_r
     _lib.check(rc, "vm_add_norm_fwd")
 
 
+def linear(x: Tensor, w: Tensor, b32: Optional[Tensor] = None,
+           out: Optional[Tensor] = None) -> Tensor:
+    """``x @ w.T (+ b)`` on the HIP small-M GEMM (``vm_linear_fwd``): x (m, k), w (n, k)
+    bf16 with unit column stride; ``out`` (m, n) may be a column-sliced view."""
+    m, k = x.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=x.dtype, device=x.device)
+    rc = _lib.load().vm_linear_fwd(_p(x), x.stride(0), _p(w), w.stride(0), _p(b32), _p(out),
+                                   out.stride(0), m, n, k, dtype_code(x.dtype), _stream(x))
+    _lib.check(rc, "vm_linear_fwd")
+    return out
+
+
 POOL_MODES = {"avg": 0, "cls+avg": 1, "cls_cat_avg": 2, "cls": 3}
 
 

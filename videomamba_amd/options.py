@@ -5,9 +5,9 @@ and layouts arrives as an explicit ABI argument (today: the token-major scan's s
 count).  Above it, the Python host picks the mixer layout and a few paths from this one
 documented options object; tests and sweeps change them with :func:`override`.
 
-    mixer_layout     "auto" (default) | "tm" | "cm".  "auto": token-major (channel-per-lane
-                     scan) when batch x 64-channel groups fills ~1.25 waves per SIMD, else
-                     channel-major (time-parallel scan); see mamba_simple.mixer_layout.
+    mixer_layout     "auto" (default) | "tm" | "cm".  "auto": token-major at every batch
+                     (single-pass or chunked scan); "cm" forces the channel-major layout
+                     (time-parallel scan); see mamba_simple.mixer_layout.
     scan_segments    0 (default) = the library's cost model; > 0 forces the token-major
                      scan's time-segment count (vm_selective_scan_fwd ``segments``).
     fused_conv_proj  True (default): bf16 token-major mixers run conv1d + x_proj + dt_proj
@@ -17,6 +17,9 @@ documented options object; tests and sweeps change them with :func:`override`.
                      library heuristic; "tune": record new shapes (slow, offline).
                      Initialised from ``VM_GEMM_TUNING`` when that is set (the tuning
                      script's switch); nothing else is read from the environment.
+    small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
+                     chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
+                     or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
 
 Options are process-global (not thread-local): the model is driven from one host thread.
 """
@@ -40,12 +43,15 @@ class Options:
     scan_segments: int = 0
     fused_conv_proj: bool = True
     gemm_tuning: str = "on"
+    small_gemm_rows: int = 4096
 
     def validate(self) -> None:
         if self.mixer_layout not in _LAYOUTS:
             raise ValueError(f"mixer_layout must be one of {_LAYOUTS}, got {self.mixer_layout!r}")
         if int(self.scan_segments) < 0:
             raise ValueError("scan_segments must be >= 0")
+        if int(self.small_gemm_rows) < 0:
+            raise ValueError("small_gemm_rows must be >= 0")
         if self.gemm_tuning not in _TUNING:
             raise ValueError(f"gemm_tuning must be one of {_TUNING}, got {self.gemm_tuning!r}")
 
