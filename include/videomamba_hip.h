@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 5
+#define VM_ABI_VERSION 6
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -293,7 +293,8 @@ int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
                   vm_stream_t stream);
 
 /*
- * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,P,P)):
+ * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,Ph,Pw);
+ * rectangular patches as the reference's PatchEmbed(patch_size=(ph, pw)), :340-364):
  *   tok[b, t*Gh*Gw + gh*Gw + gw, c] = e(e(e(conv + bias) + spos[gh*Gw+gw, c]) + tpos[t, c])
  * where e() rounds to the model dtype (the reference's rounding points).
  * video: (batch, cin, frames, height, width) contiguous, dtype `dtype`.
@@ -304,7 +305,8 @@ int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
 int vm_patch_embed_fwd(const void* video, const void* weight, const float* bias,
                        const void* spos, const void* tpos, void* out, long long out_sb,
                        int row0, int batch, int cin, int frames, int height, int width,
-                       int kt, int patch, int embed, int dtype, vm_stream_t stream);
+                       int kt, int patch_h, int patch_w, int embed, int dtype,
+                       vm_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -292,6 +292,7 @@ def encoder_forward(p: Dict[str, Tensor], cfg: dict, x: Tensor, *, mask=None,
     dt_ = p["patch_embed.proj.weight"].dtype
     k = cfg["kernel_size"]
     ps = cfg["patch_size"]
+    ph, pw = (ps, ps) if isinstance(ps, int) else tuple(ps)  # tuple: ``:348-363``
     img = cfg["img_size"] if isinstance(cfg["img_size"], (tuple, list)) else (cfg["img_size"],) * 2
     eps = cfg.get("norm_epsilon", 1e-5)
     is_rms = cfg["rms_norm"]
@@ -300,11 +301,11 @@ def encoder_forward(p: Dict[str, Tensor], cfg: dict, x: Tensor, *, mask=None,
     x = x.to(dt_)
     # patch embed (``:359-368``)
     pe = F.conv3d(x.float(), p["patch_embed.proj.weight"].float(),
-                  p["patch_embed.proj.bias"].float(), stride=(k, ps, ps)).to(dt_)
+                  p["patch_embed.proj.bias"].float(), stride=(k, ph, pw)).to(dt_)
     _, C, Tt, Gh, Gw = pe.shape
     pos = p["pos_embed"]
     patch_pos = pos[:, 1:]
-    bh, bw = img[0] // ps, img[1] // ps
+    bh, bw = img[0] // ph, img[1] // pw
     if bh * bw != patch_pos.shape[1]:
         bh, bw = _infer_spatial_grid(patch_pos.shape[1], (bh, bw))
     if (Gh, Gw) != (bh, bw):  # ``:621-644``

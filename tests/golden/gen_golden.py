@@ -184,6 +184,13 @@ def gen_model(vm):
         ("t_tubelet2", dict(img_size=16, patch_size=8, depth=2, embed_dim=16, kernel_size=2,
                             num_frames=8, fused_add_norm=True, rms_norm=True,
                             residual_in_fp32=True), (1, 8, 16, 16), torch.float32),
+        # rectangular patches, PatchEmbed(patch_size=(ph, pw)) (videomamba.py:340-364)
+        ("t_rect", dict(img_size=16, patch_size=(8, 4), depth=2, embed_dim=16,
+                        fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+                        num_frames=4), (2, 4, 16, 16), torch.float32),
+        ("t_rect_bf16", dict(img_size=32, patch_size=(16, 8), depth=2, embed_dim=32,
+                             fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+                             num_frames=4), (1, 4, 32, 32), torch.bfloat16),
     ]
     for i, (name, kw, (B, T, H, W), dt) in enumerate(cases):
         torch.manual_seed(3000 + i)

@@ -239,6 +239,17 @@ def test_block_and_refiner_construct():
     assert fs[0].shape == (2, 32, 4) and bs[1].shape == (2, 32, 16)
 
 
+def test_rectangular_patch_size_builds_the_reference_conv():
+    # the reference's PatchEmbed takes patch_size as (ph, pw) (videomamba.py:340-364)
+    m = video_mamba.PretrainVideoMamba(img_size=16, patch_size=(8, 4), depth=1, embed_dim=16,
+                                       num_frames=4)
+    pe = m.patch_embed
+    assert pe.patch_size == (8, 4) and pe.num_patches == 2 * 4
+    assert pe.proj.weight.shape == (16, 3, 1, 8, 4) and pe.proj.stride == (1, 8, 4)
+    assert m.pos_embed.shape == (1, 1 + 8, 16)
+    assert m._spatial_token_grid(16, 16) == (2, 4)
+
+
 # ------------------------------------------------------------------ C ABI
 def test_library_loads_and_exports_every_header_symbol():
     lib = _lib.load()

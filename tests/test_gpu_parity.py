@@ -387,13 +387,19 @@ def _patch_oracle(video, w, b, spos, tpos, kt, dt):
     (torch.bfloat16, 1, 4, 64, 48, 16, 2, 192),     # MFMA path, tubelet 2, non-square
     (torch.float32, 2, 4, 8, 8, 4, 1, 16),          # generic path (reference test model)
     (torch.bfloat16, 1, 2, 12, 12, 4, 1, 40),       # generic path, bf16
+    # rectangular patches (PatchEmbed(patch_size=(ph, pw)), videomamba.py:340-364)
+    (torch.bfloat16, 2, 4, 64, 48, (16, 8), 1, 192),  # MFMA path (pw % 8 == 0)
+    (torch.bfloat16, 1, 4, 48, 64, (8, 16), 2, 64),   # MFMA path, tubelet 2
+    (torch.float32, 2, 4, 12, 8, (4, 2), 1, 16),      # generic path
+    (torch.bfloat16, 1, 2, 24, 24, (6, 4), 1, 40),    # generic path, bf16
 ])
 def test_patch_embed_matches_oracle(dt, Bz, T, H, W, P, kt, C):
+    ph, pw = (P, P) if isinstance(P, int) else P
     g = torch.Generator().manual_seed(H + C)
     video = torch.randn(Bz, 3, T, H, W, generator=g).to(dt)
-    w = (0.02 * torch.randn(C, 3, kt, P, P, generator=g)).to(dt)
+    w = (0.02 * torch.randn(C, 3, kt, ph, pw, generator=g)).to(dt)
     b = torch.randn(C, generator=g).to(dt)
-    hw = (H // P) * (W // P)
+    hw = (H // ph) * (W // pw)
     spos = (0.02 * torch.randn(hw, C, generator=g)).to(dt)
     tpos = (0.02 * torch.randn(T // kt, C, generator=g)).to(dt)
     ref = _patch_oracle(video, w, b, spos, tpos, kt, dt)

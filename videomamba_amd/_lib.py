@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _P = c_void_p
 _LL = c_longlong
@@ -90,7 +90,7 @@ _SIGNATURES = {
          _P, _P, c_float, _P, _I, _I, _P], _I),   # LN w / b / eps, x_pool, dtype, cols
     "vm_linear_fwd": ([_P, _LL, _P, _LL, _P, _P, _LL, _I, _I, _I, _I, _P], _I),
     "vm_patch_embed_fwd": (
-        [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
+        [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
 }
 
 EXPORTED = tuple(_SIGNATURES)

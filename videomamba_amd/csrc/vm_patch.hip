@@ -1,14 +1,15 @@
-// Tubelet patch embed: Conv3d with kernel = stride = (kt, P, P) as an implicit GEMM,
+// Tubelet patch embed: Conv3d with kernel = stride = (kt, Ph, Pw) as an implicit GEMM,
 // fused with the bias, the spatial and the temporal positional embedding adds.
 // Replaces PatchEmbed.forward + the pos-embed adds of models/videomamba/videomamba.py
 // (:359-368, :806-815).  The reference materialises the conv output, the +spatial and
 // the +temporal sums in the model dtype; the epilogue rounds at the same three points.
 //
 //   tok[m, n] = sum_k video[gather(m, k)] * weight[n, k],  m = (b, t, gh, gw),
-//   k = (ci, kt_, kh, kw) in the weight's (C, Cin, kt, P, P) order.
+//   k = (ci, kt_, kh, kw) in the weight's (C, Cin, kt, Ph, Pw) order.  Rectangular
+//   patches (Ph != Pw) are the reference's PatchEmbed(patch_size=(ph, pw)) (:340-364).
 //
 // bf16 path: v_mfma_f32_16x16x32_bf16, operands loaded straight into fragments (with
-// P % 8 == 0 the 8 consecutive k of a lane are 8 contiguous pixels of one patch row:
+// Pw % 8 == 0 the 8 consecutive k of a lane are 8 contiguous pixels of one patch row:
 // one 16-byte load), block tile 64 tokens x 64 channels (2x2 waves of 32x32).
 // Other shapes / fp32: a scalar implicit-GEMM kernel (same math, fp32 accumulate).
 
@@ -25,7 +26,7 @@ struct PatchParams {
   const void* video; const void* w; const float* bias; const void* spos; const void* tpos;
   void* out;
   long long out_sb;
-  int row0, batch, cin, frames, height, width, kt, patch, embed;
+  int row0, batch, cin, frames, height, width, kt, ph, pw, embed;
   int tt, gh, gw, K, M;  // derived: temporal tokens, grid, reduction length, tokens
 };
 
@@ -53,18 +54,18 @@ __device__ __forceinline__ long long token_base(const PatchParams& p, int m) {
   const int gy = s / p.gw;
   const int gx = s - gy * p.gw;
   return ((long long)b * p.cin * p.frames + (long long)t * p.kt) * p.height * p.width +
-         (long long)gy * p.patch * p.width + (long long)gx * p.patch;
+         (long long)gy * p.ph * p.width + (long long)gx * p.pw;
 }
 
 __device__ __forceinline__ long long k_offset(const PatchParams& p, int k) {
-  const int pp = p.patch * p.patch;
+  const int pp = p.ph * p.pw;
   const int per_c = p.kt * pp;
   const int ci = k / per_c;
   const int r1 = k - ci * per_c;
   const int kz = r1 / pp;
   const int r2 = r1 - kz * pp;
-  const int ky = r2 / p.patch;
-  const int kx = r2 - ky * p.patch;
+  const int ky = r2 / p.pw;
+  const int kx = r2 - ky * p.pw;
   return ((long long)ci * p.frames + kz) * p.height * p.width + (long long)ky * p.width + kx;
 }
 
@@ -409,22 +410,23 @@ using namespace vm;
 extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const float* bias,
                                   const void* spos, const void* tpos, void* out, long long out_sb,
                                   int row0, int batch, int cin, int frames, int height, int width,
-                                  int kt, int patch, int embed, int dtype, vm_stream_t stream) {
+                                  int kt, int patch_h, int patch_w, int embed, int dtype,
+                                  vm_stream_t stream) {
   if (!video || !weight || !bias || !spos || !tpos || !out) {
     vmhost::set_error("vm_patch_embed_fwd: null required pointer");
     return VM_E_INVALID;
   }
-  if (batch < 0 || cin < 1 || kt < 1 || patch < 1 || embed < 1 || frames % kt != 0 ||
-      height < patch || width < patch || !vmhost::dtype_ok(dtype)) {
+  if (batch < 0 || cin < 1 || kt < 1 || patch_h < 1 || patch_w < 1 || embed < 1 ||
+      frames % kt != 0 || height < patch_h || width < patch_w || !vmhost::dtype_ok(dtype)) {
     vmhost::set_error("vm_patch_embed_fwd: bad shape/dtype");
     return VM_E_INVALID;
   }
   PatchParams p{};
   p.video = video; p.w = weight; p.bias = bias; p.spos = spos; p.tpos = tpos; p.out = out;
   p.out_sb = out_sb; p.row0 = row0; p.batch = batch; p.cin = cin; p.frames = frames;
-  p.height = height; p.width = width; p.kt = kt; p.patch = patch; p.embed = embed;
-  p.tt = frames / kt; p.gh = height / patch; p.gw = width / patch;
-  p.K = cin * kt * patch * patch;
+  p.height = height; p.width = width; p.kt = kt; p.ph = patch_h; p.pw = patch_w; p.embed = embed;
+  p.tt = frames / kt; p.gh = height / patch_h; p.gw = width / patch_w;
+  p.K = cin * kt * patch_h * patch_w;
   const long long M = 1LL * batch * p.tt * p.gh * p.gw;
   if (M == 0) return VM_OK;
   if (M > 0x7fffffffLL) {
@@ -433,9 +435,9 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
   }
   p.M = static_cast<int>(M);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch % 8 == 0 && width % 8 == 0 &&
+  const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch_w % 8 == 0 && width % 8 == 0 &&
                        p.K % 8 == 0 && vmhost::aligned16(video) && vmhost::aligned16(weight);
-  const bool wide_ok = mfma_ok && patch == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
+  const bool wide_ok = mfma_ok && patch_h == 16 && patch_w == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
                        out_sb % 8 == 0 && vmhost::aligned16(out) && vmhost::aligned16(spos) &&
                        vmhost::aligned16(tpos);
   // the 128-token LDS-staged tiles pay off on chip-filling batches; small ones keep more,

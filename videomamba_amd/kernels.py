@@ -536,12 +536,12 @@ def patch_embed(video: Tensor, weight: Tensor, bias: Tensor, spos: Tensor, tpos:
     rows into ``out`` (token j of batch b at ``out[b*out_batch_stride + (row0+j)*C]``)."""
     require_gpu(video, weight, bias, spos, tpos, out, what="patch_embed")
     Bsz, cin, T, H, W = video.shape
-    C, _, kt, P, _ = weight.shape
+    C, _, kt, Ph, Pw = weight.shape
     dt = dtype_code(weight.dtype)
     video = video.to(weight.dtype).contiguous()
     lib = _lib.load()
     rc = lib.vm_patch_embed_fwd(
         _p(video), _p(weight.contiguous()), _p(f32c(bias)), _p(spos.to(weight.dtype).contiguous()),
         _p(tpos.to(weight.dtype).contiguous()), _p(out), out_batch_stride, row0,
-        Bsz, cin, T, H, W, kt, P, C, dt, _stream(video))
+        Bsz, cin, T, H, W, kt, Ph, Pw, C, dt, _stream(video))
     _lib.check(rc, "vm_patch_embed_fwd")

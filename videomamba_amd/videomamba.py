@@ -178,8 +178,9 @@ def segm_init_weights(m):
 
 # ----------------------------------------------------------------------------- patch embed
 class PatchEmbed(nn.Module):
-    """Tubelet embedding Conv3d(kernel = stride = (kernel_size, P, P)); the conv runs as
-    the HIP implicit-GEMM kernel."""
+    """Tubelet embedding Conv3d(kernel = stride = (kernel_size, ph, pw)), square or
+    rectangular patches as in ``videomamba.py:340-364``; the conv runs as the HIP
+    implicit-GEMM kernel."""
 
     def __init__(self, img_size=224, patch_size=16, kernel_size=1, in_chans=3, embed_dim=768):
         super().__init__()
@@ -193,16 +194,14 @@ class PatchEmbed(nn.Module):
                               stride=(kernel_size, patch[0], patch[1]))
 
     def embed_tokens(self, x: Tensor, spos: Tensor, tpos: Tensor, out: Tensor, row0: int):
-        if self.patch_size[0] != self.patch_size[1]:
-            raise NotImplementedError("non-square patches are not supported by the HIP kernel")
         K.patch_embed(x, self.proj.weight, self.proj.bias, spos, tpos, out, row0,
                       out.stride(0))
 
     def forward(self, x: Tensor) -> Tensor:
         K.require_gpu(x, what="PatchEmbed")
         B, _, T, H, W = x.shape
-        P = self.patch_size[0]
-        Tt, Gh, Gw = T // self.tubelet_size, H // P, W // P
+        ph, pw = self.patch_size
+        Tt, Gh, Gw = T // self.tubelet_size, H // ph, W // pw
         C = self.proj.out_channels
         dt = self.proj.weight.dtype
         out = torch.empty((B, Tt * Gh * Gw, C), dtype=dt, device=x.device)
@@ -507,8 +506,8 @@ class PretrainVideoMamba(nn.Module):
         static buffer that is refilled per chunk)."""
         Bsz, _, T, H, W = x.shape
         k = self.patch_embed.tubelet_size
-        P = self.patch_embed.patch_size[0]
-        Tt, Gh, Gw = T // k, H // P, W // P
+        ph, pw = self.patch_embed.patch_size
+        Tt, Gh, Gw = T // k, H // ph, W // pw
         dt = self.patch_embed.proj.weight.dtype
         spos = self._get_spatial_pos_embedding(Gh, Gw, dtype=dt, device=x.device)
         if tpos is None:
