@@ -12,6 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
+    "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
+                   "    if (false) conv_proj_fused_launch(a, st);")],
     # small-M GEMM with 64-row tiles at every shape
     "lin64": [("vm_gemm.hip", "  const bool big = (long long)((m + 127) / 128) * nt >= 384;",
                "  const bool big = false;")],

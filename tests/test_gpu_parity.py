@@ -585,6 +585,47 @@ def test_conv_proj_split_k_matches_wide_kernel(d_model):
     _close(u1[:L].t().unsqueeze(0), ref_u, 1e-2)
 
 
+@pytest.mark.parametrize("d_model", [576, 96])
+def test_conv_proj_fused_small_batch_matches_split_k_bitwise(d_model):
+    """Small batches run conv + x_proj + dt_proj as one fused launch when out_len >= 24
+    (conv_proj_fused_kernel) and as the two split-K launches below that; both sum the same
+    fixed 128-channel x_proj partials in split order, so the same clips laid out with
+    out_len 16 (split-K) and 32 (fused) must give bit-identical u / x_dbl / dt and new conv
+    state — which keeps chunked == full bitwise whatever the chunk length.  Sequence starts
+    mid-tile, a carried conv state, 3 batch rows; d_model 96 -> a half-width last split."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(d_model + 1)
+    m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    _, _, _, cw, cb = m._fp32_params()
+    wx_pad, wdt_pad = m._padded_proj_weights()
+    st = torch.cuda.current_stream().cuda_stream
+    bsz = 3
+    for L in (2, 13, 16):
+        x3 = torch.randn(bsz, L, Dm, device=DEV).to(torch.bfloat16)
+        z3 = torch.randn(bsz, L, Dm, device=DEV).to(torch.bfloat16)
+        cs = torch.randn(bsz, Dm, W, device=DEV).to(torch.bfloat16)
+        res = []
+        for Lp in (16, 32):  # split-K form, fused form
+            n = bsz * Lp
+            xz = torch.zeros(bsz, Lp, 2 * Dm, device=DEV, dtype=torch.bfloat16)
+            xz[:, :L, :Dm] = x3
+            xz[:, :L, Dm:] = z3
+            xz = xz.reshape(n, 2 * Dm)
+            cso = torch.full((bsz, Dm, W), float("nan"), device=DEV, dtype=torch.bfloat16)
+            u = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+            xd = torch.empty(n, E, device=DEV, dtype=torch.bfloat16)
+            dt = torch.empty(n, Dm, device=DEV, dtype=torch.bfloat16)
+            K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, (Dm * W, W), cso,
+                            (Dm * W, W), wx_pad, E, wdt_pad, R, u, (Lp * Dm, Dm), xd,
+                            (Lp * E, E), dt, (Lp * Dm, Dm), Lp, bsz, Dm, L, W, st)
+            res.append((u.view(bsz, Lp, Dm)[:, :L], xd.view(bsz, Lp, E)[:, :L],
+                        dt.view(bsz, Lp, Dm)[:, :L], cso))
+        torch.cuda.synchronize()
+        for a, b in zip(*res):
+            assert torch.equal(a, b), L
+
+
 @pytest.mark.parametrize("m,n,k", [(3144, 2304, 576), (3144, 576, 1152), (1, 576, 1152),
                                    (77, 2304, 576), (600, 64, 192), (5000, 136, 384)])
 def test_small_m_linear_matches_fp32_reference(m, n, k):

@@ -426,7 +426,10 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     a.r_pad = r_pad; a.u = p.u; a.u_tl = u_sl; a.xdbl = p.xdbl; a.xd_tl = xd_sl; a.dt = p.dt;
     a.dt_tl = dt_sl; a.out_len = out_len; a.batch = batch; a.dim = dim; a.seqlen = seqlen;
     a.width = width;
-    conv_proj_sk_launch(a, static_cast<float*>(workspace), st);  // writes the conv state too
+    // one fused launch where it applies (bit-identical), else the two split-K launches;
+    // both write the conv state
+    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);
+    else conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
     return vmhost::launch_status("vm_conv_proj_fwd");
   }
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };

@@ -617,6 +617,294 @@ __global__ __launch_bounds__(256) void xdbl_dt_tm_kernel(const SkTmParams q) {
   }
 }
 
+// ================================================================ fused small-batch form
+// One launch for conv + SiLU -> x_proj -> dt_proj at small batches (B <= 8, dim <= 1152):
+// a workgroup owns kFuTok = 16 token rows and all channels, one wave per fixed 128-channel
+// split (the split-K form's splits).  Each wave runs its split's conv and its x_proj
+// partial on MFMA exactly as conv_xproj_tm_kernel does, the partials are summed through LDS
+// in split order (exactly the xdbl_dt_tm_kernel sum), and the same waves then run dt_proj
+// for their 128 channels — so u / x_dbl / dt are bit-identical to the two-kernel split-K
+// form, without its fp32 partials round trip through L2 / infinity cache and with one
+// launch fewer per layer.  B = 1 M-16f: 197 workgroups.
+//   Loads: every global load of a wave (19 x-rows of its 128 channels, its W_x fragments,
+//   conv taps, the conv-state taps of a sequence start) is issued in one round; W_dt
+//   fragments are issued right after the x_proj MFMAs and land during the LDS reduction.
+constexpr int kFuTok = 16;     // token rows per workgroup
+constexpr int kFuMaxSpl = 9;   // splits (waves) per workgroup: dim <= 1152
+constexpr int kFuUPitch = 136; // bf16 pitch of a wave's [16 tok][128 ch] u tile
+constexpr int kFuXdPitch = 72; // bf16 pitch of the [16 tok][64] x_dbl[:R] operand
+
+template <int NB>  // NB = e_pad / 16 x_proj column blocks
+__global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const SkTmParams q) {
+  const ConvProjTmArgs& p = q.a;
+  // LDS: per-wave u tiles, then (aliased) the split partials [split][tok][ep], then
+  // (aliased) the dt tile [tok][dim]; the x_dbl operand after them
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  constexpr int kUBytes = kFuMaxSpl * kFuTok * kFuUPitch * 2;
+  constexpr int kPBytes = kFuMaxSpl * kFuTok * kSkMaxEp * 4;
+  constexpr int kArea = kUBytes > kPBytes ? kUBytes : kPBytes;
+  bf16_t* sU = reinterpret_cast<bf16_t*>(fsm);
+  float* sP = reinterpret_cast<float*>(fsm);
+  bf16_t* sXD = reinterpret_cast<bf16_t*>(fsm + kArea);
+  bf16_t* sDT = reinterpret_cast<bf16_t*>(fsm);  // [16][dim + 8], after the partials
+  const int dtp = p.dim + 8;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;           // = split
+  const int nspl = blockDim.x >> 6;
+  const int tok0 = blockIdx.x * kFuTok;
+  const int c0 = wave * kSkCh;
+  const int W = p.width;
+  const int nch = min(kSkCh, p.dim - c0);
+  const bool cact = 2 * lane < nch;
+  const int c = c0 + 2 * (cact ? lane : 0);
+  const int ntok = q.ntok;
+
+  // ---- one round of loads ----
+  // x rows tok0 - 3 .. tok0 + 15 of channels c, c + 1 (zero outside [0, ntok))
+  uint32_t xw[kFuTok + 3];
+#pragma unroll
+  for (int r = 0; r < kFuTok + 3; ++r) {
+    const int tok = tok0 - 3 + r;
+    xw[r] = (tok >= 0 && tok < ntok && cact)
+                ? *reinterpret_cast<const uint32_t*>(p.x + (long long)tok * p.x_tl + c)
+                : 0u;
+  }
+  // W_x fragments of this split: column block j, k-step ks (rows e, 8 channels per lane);
+  // k-steps 0-1 with the first round, 2-3 once the x rows are consumed (register budget)
+  bf16x8 wv[4][NB];
+  auto wx_load = [&](int ks) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int kc = ks * 32 + (lane >> 4) * 8;
+      wv[ks][j] = kc < nch ? *reinterpret_cast<const bf16x8*>(
+                                 p.wx + (long long)(j * 16 + (lane & 15)) * p.dim + c0 + kc)
+                           : bf16x8{};
+    }
+  };
+  wx_load(0);
+  wx_load(1);
+  float wl[4], wh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    wl[k] = k >= 4 - W ? p.cw[c * W + k - (4 - W)] : 0.0f;
+    wh[k] = k >= 4 - W ? p.cw[(c + 1) * W + k - (4 - W)] : 0.0f;
+  }
+  const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
+  // the (at most one: out_len >= 24) sequence starting in tok0 - 2 .. tok0 + 15, whose
+  // first 3 steps may lie in this tile: its old conv-state taps for steps -1, -2, -3
+  // (state columns W - 1, W - 2, W - 3)
+  const int bs = (tok0 - 2 + p.out_len - 1) / p.out_len;  // tok0 - 2 + out_len - 1 >= 0
+  const int ts = bs * p.out_len;
+  const bool has_start = ts < tok0 + kFuTok && bs < p.batch;
+  float csl[3] = {0.f, 0.f, 0.f}, csh[3] = {0.f, 0.f, 0.f};
+  if (has_start && p.csi) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int col = W - 1 - m;
+      if (col >= 0) {
+        const long long base = (long long)bs * p.csi_sb + (long long)c * p.csi_sd + col;
+        csl[m] = load_dyn(p.csi, base, p.csi_dtype);
+        csh[m] = load_dyn(p.csi, base + p.csi_sd, p.csi_dtype);
+      }
+    }
+  }
+
+  // ---- conv + SiLU: channels c, c + 1, tokens tok0 .. tok0 + 15 ----
+  auto pack = [&](float al, float ah, bool live) -> uint32_t {
+    const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
+    const float uh = live ? ah * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-ah * kLog2e)) : 0.0f;
+    return static_cast<uint32_t>(from_f32<bf16_t>(ul)) |
+           (static_cast<uint32_t>(from_f32<bf16_t>(uh)) << 16);
+  };
+  const int b0 = tok0 / p.out_len;  // batch row and step of the tile's first token
+  const int s0 = tok0 - b0 * p.out_len;
+  uint32_t upk[kFuTok];
+#pragma unroll
+  for (int i = 0; i < kFuTok; ++i) {
+    float al = bl, ah = bh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      al = fmaf(wl[k], __uint_as_float(xw[i + k] << 16), al);
+      ah = fmaf(wh[k], __uint_as_float(xw[i + k] & 0xffff0000u), ah);
+    }
+    int st = s0 + i;
+    if (st >= p.out_len) st -= p.out_len;  // out_len >= 16: at most one wrap
+    if (st < 3) {  // uniform: the taps before the sequence start come from the old state
+      al = bl;
+      ah = bh;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = st - 3 + k;  // input step in the virtual sequence
+        float vl = __uint_as_float(xw[i + k] << 16), vh = __uint_as_float(xw[i + k] & 0xffff0000u);
+        if (j < 0) {
+          vl = vh = 0.0f;
+          if (p.csi && tok0 + i < ntok && k >= 4 - W) {
+            vl = csl[-j - 1];
+            vh = csh[-j - 1];
+          }
+        }
+        al = fmaf(wl[k], vl, al);
+        ah = fmaf(wh[k], vh, ah);
+      }
+    }
+    upk[i] = pack(al, ah, st < p.seqlen && tok0 + i < ntok && cact);
+  }
+  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----
+  if (p.cso && cact) {
+    const int be1 = min(p.batch - 1, (tok0 + kFuTok - 1) / p.out_len);
+    for (int be = b0; be <= be1; ++be) {  // the tile's (at most two) sequences
+      const int tl = be * p.out_len + p.seqlen - 1;
+      if (tl < tok0 || tl >= tok0 + kFuTok) continue;
+      for (int s2 = 0; s2 < W; ++s2) {
+        const int te = p.seqlen - W + s2;
+        float vl = 0.0f, vh = 0.0f;
+        if (te >= 0) {
+          const int r = be * p.out_len + te - (tok0 - 3);  // 0 .. kFuTok + 2
+          uint32_t v = 0u;
+#pragma unroll
+          for (int rr = 0; rr < kFuTok + 3; ++rr) v = rr == r ? xw[rr] : v;
+          vl = __uint_as_float(v << 16);
+          vh = __uint_as_float(v & 0xffff0000u);
+        } else if (p.csi) {
+          const long long base = (long long)be * p.csi_sb + (long long)c * p.csi_sd + W + te;
+          vl = load_dyn(p.csi, base, p.csi_dtype);
+          vh = load_dyn(p.csi, base + p.csi_sd, p.csi_dtype);
+        }
+        const long long ob = (long long)be * p.cso_sb + (long long)c * p.cso_sd + s2;
+        store_dyn(p.cso, ob, p.cso_dtype, vl);
+        store_dyn(p.cso, ob + p.cso_sd, p.cso_dtype, vh);
+      }
+    }
+  }
+  wx_load(2);
+  wx_load(3);
+  // ---- u: global rows and this wave's LDS tile ----
+  bf16_t* myU = sU + wave * kFuTok * kFuUPitch;
+#pragma unroll
+  for (int i = 0; i < kFuTok; ++i) {
+    *reinterpret_cast<uint32_t*>(&myU[i * kFuUPitch + 2 * lane]) = upk[i];
+    if (cact && tok0 + i < ntok)
+      *reinterpret_cast<uint32_t*>(p.u + (long long)(tok0 + i) * p.u_tl + c) = upk[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ---- x_proj partial of this split: tokens x e_pad columns, K = 128 ----
+  f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+        &myU[(lane & 15) * kFuUPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wv[ks][j], acc[j], 0, 0, 0);
+  }
+  // W_dt fragments for this wave's dt channels (128 per wave, 8 column tiles x 2 k-steps),
+  // in flight during the reduction
+  const bool do_dt = p.wdt != nullptr;
+  bf16x8 bw[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = min(c0 + i * 16 + (lane & 15), p.dim - 1);
+      bw[i][ks] = do_dt && ks * 32 < p.r_pad
+                      ? *reinterpret_cast<const bf16x8*>(p.wdt + (long long)ch * p.r_pad + ks * 32 +
+                                                         (lane >> 4) * 8)
+                      : bf16x8{};
+    }
+  __syncthreads();  // every wave's u tile is consumed: the area becomes the partials
+  const int ep = q.ep;
+  float* myP = sP + wave * kFuTok * ep;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int e = j * 16 + (lane & 15);
+      if (e < ep) myP[((lane >> 4) * 4 + rr) * ep + e] = acc[j][rr];
+    }
+  // zero the K padding of the dt operand
+  for (int i = tid; i < kFuTok * (p.r_pad - p.r); i += blockDim.x) {
+    const int t = i / (p.r_pad - p.r);
+    sXD[t * kFuXdPitch + p.r + (i - t * (p.r_pad - p.r))] = bf16_t(0);
+  }
+  __syncthreads();
+  // ---- x_dbl = bf16(sum of the partials in split order) ----
+  for (int i = tid; i < kFuTok * p.e; i += blockDim.x) {
+    const int t = i / p.e, e = i - t * p.e;
+    float sum = 0.0f;
+    for (int sp = 0; sp < nspl; ++sp) sum += sP[(sp * kFuTok + t) * ep + e];
+    const bf16_t v = from_f32<bf16_t>(sum);
+    if (e < p.r) sXD[t * kFuXdPitch + e] = v;
+    if (tok0 + t < ntok) p.xdbl[(long long)(tok0 + t) * p.xd_tl + e] = v;
+  }
+  if (!do_dt) return;
+  __syncthreads();
+  // ---- dt for channels c0 .. c0 + 127: tokens x 8 column tiles, K = r_pad ----
+  f32x4 dacc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (ks * 32 < p.r_pad) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+          &sXD[(lane & 15) * kFuXdPitch + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        dacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[i][ks], dacc[i], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ch = c0 + i * 16 + (lane & 15);
+    if (ch < p.dim) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        sDT[((lane >> 4) * 4 + rr) * dtp + ch] = from_f32<bf16_t>(dacc[i][rr]);
+    }
+  }
+  __syncthreads();
+  // 16 token rows x dim channels out, 16 B per lane-store
+  const int q8 = p.dim >> 3;
+  for (int i = tid; i < kFuTok * q8; i += blockDim.x) {
+    const int t = i / q8, qd = i - t * q8;
+    if (tok0 + t < ntok)
+      *reinterpret_cast<uint4*>(p.dt + (long long)(tok0 + t) * p.dt_tl + qd * 8) =
+          *reinterpret_cast<const uint4*>(&sDT[t * dtp + qd * 8]);
+  }
+}
+
+bool conv_proj_fused_ok(const ConvProjTmArgs& a) {
+  // e_pad <= 80 (R + 2N <= 80, every VideoMamba size up to d_model 768): wider x_proj
+  // outputs exceed the register budget of the 576-thread workgroup
+  return a.dim <= kFuMaxSpl * kSkCh && a.out_len >= 24 && a.e_pad <= 80 &&
+         (a.e + 3) / 4 * 4 <= kSkMaxEp && (a.wdt == nullptr || a.r_pad <= 64);
+}
+
+void conv_proj_fused_launch(const ConvProjTmArgs& a, hipStream_t s) {
+  SkTmParams q{};
+  q.a = a;
+  q.part = nullptr;
+  q.ntok = a.batch * a.out_len;
+  q.nsplit = (a.dim + kSkCh - 1) / kSkCh;
+  q.ep = (a.e + 3) / 4 * 4;
+  const unsigned tiles = static_cast<unsigned>((q.ntok + kFuTok - 1) / kFuTok);
+  constexpr int kUBytes = kFuMaxSpl * kFuTok * kFuUPitch * 2;
+  constexpr int kPBytes = kFuMaxSpl * kFuTok * kSkMaxEp * 4;
+  const size_t lds = static_cast<size_t>(kUBytes > kPBytes ? kUBytes : kPBytes) +
+                     kFuTok * kFuXdPitch * 2;
+  static_assert(kFuTok * (kFuMaxSpl * kSkCh + 8) * 2 <= kPBytes, "dt tile exceeds the area");
+  const dim3 grid(tiles), block(64 * q.nsplit);
+  switch (a.e_pad / 16) {
+#define VM_FU_CASE(NBV) \
+    case NBV: hipLaunchKernelGGL(conv_proj_fused_kernel<NBV>, grid, block, lds, s, q); break;
+    VM_FU_CASE(1) VM_FU_CASE(2) VM_FU_CASE(3) VM_FU_CASE(4) VM_FU_CASE(5)
+#undef VM_FU_CASE
+  }
+}
+
 long long conv_proj_sk_workspace_bytes(int batch, int out_len, int dim, int e) {
   if (batch <= 0 || out_len <= 0 || dim <= 0 || e <= 0) return 0;
   const long long ntok = 1LL * batch * out_len;

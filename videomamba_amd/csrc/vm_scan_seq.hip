@@ -476,10 +476,14 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   typedef __attribute__((address_space(4))) const uint32_t* cptr;
   constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
   constexpr int ES = sizeof(T);
+  // sH: PASS 1 segment end states; PASS 2 the staged block aggregates, then H_blk in sH[0].
+  // sA: A of the workgroup's 64 channels, transposed to [state][channel].
   __shared__ float sH[kChW][kMaxN][64];
   __shared__ float sS[kChW][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ float sA[kMaxN][64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int blk = blockIdx.y;
   const int b = blockIdx.z;
   const int d0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 64);
@@ -494,45 +498,58 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const long long rowE = ((static_cast<long long>(b) * w.nblk + blk) * kChW) * D;  // + j*D + d
   const long long rowA = (static_cast<long long>(b) * w.nblk) * D;                  // + k*D + d
   const PairSel ps = pair_sel<PAIR>(p, b);
+  const int nch = min(64, p.dim - d0);  // live channels of this group
 
-  f2 A2[kMaxN / 2], h[kMaxN / 2];
+  // Start-up loads are issued as whole-line, lane-contiguous accesses and waited for once:
+  // per-lane strided loads (A[d][n] at a 64-byte lane stride, the aggregates' state pairs)
+  // touched ~32 cache lines per wave-instruction, and with 8 waves each issuing ~80 of them
+  // the address path, not the memory, set the kernel's start-up time at B = 1.
+  //   A: the group's 64 x N floats are contiguous — 2 coalesced dwords per thread
+  float aval[2];
 #pragma unroll
-  for (int q = 0; q < kMaxN / 2; ++q) {
-    A2[q] = f2{2 * q < N ? ps.A[d * N + 2 * q] : 0.0f, 2 * q + 1 < N ? ps.A[d * N + 2 * q + 1] : 0.0f};
-    h[q] = f2{0.0f, 0.0f};
+  for (int k = 0; k < 2; ++k) {
+    const int e = tid + k * 64 * kChW;  // element of the [64][N] tile
+    aval[k] = e < nch * N ? ps.A[static_cast<long long>(d0) * N + e] : 0.0f;
   }
   const float Dv = (ps.D ? ps.D[d] : 0.0f) * kLog2e;
   const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * kLog2e;
   // states this wave composes across segments / blocks: 2 * wave, 2 * wave + 1
   const int n0 = 2 * wave;
-  const float An0 = n0 < N ? ps.A[d * N + n0] : 0.0f;
-  const float An1 = n0 + 1 < N ? ps.A[d * N + n0 + 1] : 0.0f;
 
-  // PASS 2 entry operands: loaded together with everything else below, combined after
-  // the one wait (every global load of the wave's start-up is a single round trip),
-  // including the block aggregates the block entry is walked from
-  constexpr int kCW = 16;  // block aggregates loaded with the start-up round
+  // PASS 2 entry operands: this segment's entry offset and delta prefix, the entry state's
+  // two composed states, and the aggregates of up to kCW preceding blocks (each block's 64
+  // channels x 16 states are one contiguous 4 KB row: a coalesced float2 per thread)
+  constexpr int kCW = 16;
   float Pj = 0.0f, H0 = 0.0f, H1 = 0.0f;
   f2 Ej[kMaxN / 2];
-  float cS[kCW], cH0[kCW], cH1[kCW];
+  f2 agH[kCW];
+  float agS[kCW * 64 / (64 * kChW)];
   if constexpr (PASS == 2) {
     Pj = w.segP[rowE + wave * D + d];
-    const float* ep = &w.segE[(rowE + wave * D + d) * kMaxN];
+    const float4* ep = reinterpret_cast<const float4*>(&w.segE[(rowE + wave * D + d) * kMaxN]);
 #pragma unroll
-    for (int q = 0; q < kMaxN / 2; ++q) Ej[q] = *reinterpret_cast<const f2*>(&ep[2 * q]);
+    for (int q = 0; q < kMaxN / 4; ++q) {
+      const float4 v = ep[q];
+      Ej[2 * q] = f2{v.x, v.y};
+      Ej[2 * q + 1] = f2{v.z, v.w};
+    }
     if (ps.h0) {
       if (n0 < N) H0 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0, p.h0_dtype);
       if (n0 + 1 < N) H1 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + 1, p.h0_dtype);
     }
+    const int ci = tid >> 3;  // channel of this thread's state pair
 #pragma unroll
     for (int j = 0; j < kCW; ++j) {
-      const long long row = rowA + static_cast<long long>(j < blk ? j : 0) * D + d;
-      cS[j] = w.aggS[row];
-      cH0[j] = w.aggH[row * kMaxN + n0];
-      cH1[j] = w.aggH[row * kMaxN + n0 + 1];
+      agH[j] = f2{0.0f, 0.0f};
+      if (j < blk && ci < nch)
+        agH[j] = *reinterpret_cast<const f2*>(&w.aggH[(rowA + j * D + d0) * kMaxN + 2 * tid]);
+    }
+#pragma unroll
+    for (int k = 0; k < kCW / kChW; ++k) {
+      const int j = k * kChW + (tid >> 6);
+      agS[k] = j < blk && lane < nch ? w.aggS[rowA + j * D + d0 + lane] : 0.0f;
     }
   }
-
   const int voff = lane * ES;
   const int voff_st = active ? voff : kSeqDead;
   const auto ur = uniform_rsrc(static_cast<const T*>(p.u) + b * p.u_sb + d0);
@@ -602,22 +619,68 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // one wait for every start-up load (parameters, entry operands, prologue): left pending
   // they would merge into the step loop's header waits
   __builtin_amdgcn_s_waitcnt(0);
+  // A transposed into LDS: sA[n][c] (zero for n >= N and for channels past dim)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = tid + k * 64 * kChW;
+    if (e < 64 * N) sA[e % N][e / N] = aval[k];
+    if (e >= 64 * N && e < 64 * kMaxN) sA[e >> 6][e & 63] = 0.0f;
+  }
+  if constexpr (PASS == 2) {
+    // the first kChW block aggregates go to LDS with A: [block][state][channel]
+#pragma unroll
+    for (int j = 0; j < kChW; ++j) {
+      sH[j][2 * (tid & 7)][tid >> 3] = agH[j].x;
+      sH[j][2 * (tid & 7) + 1][tid >> 3] = agH[j].y;
+    }
+    sS[tid >> 6][lane] = agS[0];
+  }
+  __syncthreads();
+  f2 A2[kMaxN / 2], h[kMaxN / 2];
+#pragma unroll
+  for (int q = 0; q < kMaxN / 2; ++q) {
+    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};
+    h[q] = f2{0.0f, 0.0f};
+  }
+  const float An0 = sA[n0][lane], An1 = sA[n0 + 1][lane];
   if constexpr (PASS == 2) {
     H0 *= kLog2e;  // log2 units
     H1 *= kLog2e;
+    // walk the preceding blocks' aggregates from h0 to this block's entry, kChW at a time
+    // through LDS (the second group from registers loaded with the start-up round)
+    for (int r0 = 0; r0 < blk; r0 += kChW) {
+      if (r0 > 0) {
+        __syncthreads();  // every wave is done reading the previous group
+        if (r0 < kCW) {
 #pragma unroll
-    for (int j = 0; j < kCW; ++j) {
-      if (j < blk) {
-        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * cS[j]), H0, cH0[j]);
-        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * cS[j]), H1, cH1[j]);
+          for (int j = 0; j < kChW; ++j) {
+            sH[j][2 * (tid & 7)][tid >> 3] = agH[kChW + j].x;
+            sH[j][2 * (tid & 7) + 1][tid >> 3] = agH[kChW + j].y;
+          }
+          sS[tid >> 6][lane] = agS[1];
+        } else {  // long sequences: later groups are loaded here
+          const int ci = tid >> 3;
+#pragma unroll
+          for (int j = 0; j < kChW; ++j) {
+            f2 v{0.0f, 0.0f};
+            if (r0 + j < blk && ci < nch)
+              v = *reinterpret_cast<const f2*>(&w.aggH[(rowA + (r0 + j) * D + d0) * kMaxN + 2 * tid]);
+            sH[j][2 * (tid & 7)][ci] = v.x;
+            sH[j][2 * (tid & 7) + 1][ci] = v.y;
+          }
+          const int j = r0 + (tid >> 6);
+          sS[tid >> 6][lane] = j < blk && lane < nch ? w.aggS[rowA + j * D + d0 + lane] : 0.0f;
+        }
+        __syncthreads();
+      }
+      const int nj = min(kChW, blk - r0);
+      for (int j = 0; j < nj; ++j) {
+        const float Sj = sS[j][lane];
+        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, sH[j][n0][lane]);
+        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, sH[j][n0 + 1][lane]);
       }
     }
-    for (int k = kCW; k < blk; ++k) {  // long sequences: the remaining blocks, one by one
-      const long long row = rowA + static_cast<long long>(k) * D + d;
-      const float Sk = w.aggS[row];
-      H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sk), H0, w.aggH[row * kMaxN + n0]);
-      H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sk), H1, w.aggH[row * kMaxN + n0 + 1]);
-    }
+    __syncthreads();  // sH[0] is rewritten with the block entry
     sH[0][n0][lane] = H0;
     sH[0][n0 + 1][lane] = H1;
     __syncthreads();
@@ -833,20 +896,36 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
   }
 }
 
-// Segment count.  A chip-filling batch (>= 1.25 waves per SIMD of 64-channel groups) runs
-// single-pass; below that the sequence is cut so the chunked form has ~1.75 waves per SIMD
-// (every step then runs twice, once per pass), with segments of at least 8 steps.  Measured
-// at B = 1, M-16f (scripts/diag/b1_layouts.py, hipGraph chunk p50): 1,728 waves 4.55 ms,
-// 1,152 waves 4.78 ms, 4,104 waves 4.72 ms.  Depends on (batch, dim, seqlen) only.
+// Segment count.  A chip-filling batch (>= 1,280 waves of 64-channel groups) runs
+// single-pass.  Below that the chunked form's time is modelled from a sweep of forced
+// segment counts at M-16f geometry (scripts/diag/scan_segments_sweep.py, B = 1 .. 64,
+// L = 3,137 and 12,545; profiles/r02_scan_segments_sweep.jsonl):
+//   time ~ 16.6 us + 0.69 us x k x T + 0.43 us x nblk
+// with T steps per segment, nblk = blocks of kChW segments per sequence and
+// k = ceil(workgroups / 256): a CU holding k of the 512-thread workgroups runs their waves'
+// steps k-fold interleaved (the passes are issue-bound), and every block adds one aggregate
+// to the entry walk.  The model is within ~6 % of the sweep; the round-1 rule (a fixed
+// ~1,792-wave target) picked 2-3x slower counts at B >= 4 (T = 126 .. 1,569 steps).
+// Depends on (batch, dim, seqlen) only.
 static int choose_segments(int batch, int dim, int seqlen) {
   if (seqlen < 64) return 1;
   const long long groups = (dim + 63) / 64;
-  const long long waves = batch * groups;
-  if (waves >= 1280) return 1;
-  long long S = (1792 + waves - 1) / waves;
-  const long long max_s = (seqlen + 7) / 8;
-  if (S > max_s) S = max_s;
-  return S < 2 ? 1 : static_cast<int>(S);
+  if (batch * groups >= 1280) return 1;
+  const int max_s = (seqlen + 7) / 8;  // segments of at least 8 steps
+  int best = 1;
+  double best_cost = 1e30;
+  for (int S = 2; S <= max_s && S <= 2048; S += (S < 64 ? 1 : 8)) {
+    const int T = (seqlen + S - 1) / S;
+    const int segs = (seqlen + T - 1) / T;
+    const long long nblk = (segs + kChW - 1) / kChW;
+    const long long k = (batch * groups * nblk + 255) / 256;
+    const double cost = 0.69 * static_cast<double>(k * T) + 0.43 * static_cast<double>(nblk);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  return best;
 }
 
 // segments > 0 (an explicit ABI argument: tests and sweeps) forces the segment count;
