@@ -12,6 +12,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # scan grids without (sc_xcd: single pass) / with (ch_xcd: chunked) the XCD renumbering
+    "sc_xcd": [("vm_scan_seq.hip", "constexpr bool kSeqXcdRemap = true;", "constexpr bool kSeqXcdRemap = false;")],
+    "ch_xcd": [("vm_scan_seq.hip", "constexpr bool kChunkXcdRemap = false;", "constexpr bool kChunkXcdRemap = true;")],
+    # chunked-scan fixed cost: PASS 1 / PASS 2 without their step loops (results wrong)
+    "sc_noloop1": [("vm_scan_seq.hip", "  for (int tg = t_beg; tg < t_end; tg += kPF) {",
+                    "  for (int tg = t_beg; PASS == 2 && tg < t_end; tg += kPF) {")],
+    "sc_noloop2": [("vm_scan_seq.hip", "  for (int tg = t_beg; tg < t_end; tg += kPF) {",
+                    "  for (int tg = t_beg; PASS == 1 && tg < t_end; tg += kPF) {")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],

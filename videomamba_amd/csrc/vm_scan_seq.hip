@@ -35,6 +35,8 @@ constexpr int kTS = 32;       // steps per LDS block
 constexpr int kPF = 8;        // u / delta / z prefetch distance in steps
 constexpr int kMaxSeg = 256;  // segments per sequence
 constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
+constexpr bool kSeqXcdRemap = true;  // grids renumbered per XCD (see scan_seq_kernel)
+constexpr bool kChunkXcdRemap = false;
 
 // Buffer descriptor over a wave-uniform base: per-step byte offsets go in soffset (SGPR),
 // the lane's channel offset in voffset, so no per-lane 64-bit address math runs per step.
@@ -49,6 +51,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base)
   void* ub = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(ub, 0, kSeqRange, 0x00020000);
 }
+// Logical workgroup ids in XCD order: the hardware hands workgroup H to XCD H % 8, so the
+// renumbering H -> (H % 8) * (n / 8) + H / 8 gives each XCD a contiguous range of logical
+// ids (n % 8 == 0; otherwise the ids are left alone).
+__device__ __forceinline__ void xcd_order(int& gx, int& gy, int& gz) {
+  const int n = gridDim.x * gridDim.y * gridDim.z;
+  if ((n & 7) != 0) return;
+  const int h = gx + gridDim.x * (gy + gridDim.y * gz);
+  const int l = (h & 7) * (n >> 3) + (h >> 3);
+  gx = l % gridDim.x;
+  gy = (l / gridDim.x) % gridDim.y;
+  gz = l / (gridDim.x * gridDim.y);
+}
+
 template <typename T>
 __device__ __forceinline__ uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   if constexpr (sizeof(T) == 2)
@@ -90,9 +105,14 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int seg = blockIdx.y;
-  const int b = blockIdx.z;
-  const int d_raw = (blockIdx.x * NW + wave) * 64 + lane;
+  // XCD order: the channel groups of one batch row (consecutive logical ids) share an
+  // XCD, so their common B / C rows come into one L2 instead of up to eight (calibrated
+  // fetch 9.9 -> 7.6 GB per launch at B = 336, time unchanged; profiles/r02_scan_xcd_pmc.txt)
+  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;
+  if constexpr (kSeqXcdRemap) xcd_order(gx, gy, gz);
+  const int seg = gy;
+  const int b = gz;
+  const int d_raw = (gx * NW + wave) * 64 + lane;
   const bool active = d_raw < p.dim;
   const int d = active ? d_raw : p.dim - 1;
   const int N = p.dstate;
@@ -133,8 +153,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   const float Dv = (ps.D ? ps.D[d] : 0.0f) * lg_in;
   const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * lg_in;
   // Wave-uniform row bases (buffer descriptors) + the lane's channel byte offset.
-  const int d0 = __builtin_amdgcn_readfirstlane((blockIdx.x * NW + wave) * 64 < p.dim
-                                                    ? (blockIdx.x * NW + wave) * 64
+  const int d0 = __builtin_amdgcn_readfirstlane((gx * NW + wave) * 64 < p.dim
+                                                    ? (gx * NW + wave) * 64
                                                     : p.dim - 1);
   constexpr int ES = sizeof(T);
   const int voff = (d - d0) * ES;
@@ -484,9 +504,11 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int blk = blockIdx.y;
-  const int b = blockIdx.z;
-  const int d0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 64);
+  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;
+  if constexpr (kChunkXcdRemap) xcd_order(gx, gy, gz);  // a block's channel groups share an XCD
+  const int blk = gy;
+  const int b = gz;
+  const int d0 = __builtin_amdgcn_readfirstlane(gx * 64);
   const int d_raw = d0 + lane;
   const bool active = d_raw < p.dim;
   const int d = active ? d_raw : p.dim - 1;
