@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 6
+#define VM_ABI_VERSION 7
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -97,7 +97,7 @@ int vm_selective_scan_fwd(const void* u, long long u_sb, long long u_sd, long lo
                           void* out, long long o_sb, long long o_sd, long long o_sl,
                           int out_len, int batch, int dim, int seqlen, int dstate, int dtype,
                           int segments, void* workspace, long long workspace_bytes,
-                          vm_stream_t stream);
+                          void* sync, long long sync_bytes, vm_stream_t stream);
 
 /*
  * Both directions of a bidirectional block in one scan (BiMambaRefinerBlock,
@@ -126,12 +126,23 @@ int vm_selective_scan_bidir_fwd(
     int batch, int dim, int seqlen, int dstate, int dtype,
     int split, const float* A_bwd, const float* D_bwd, const float* delta_bias_bwd,
     const void* h0_bwd, void* h_last_bwd, int frame_len,
-    int segments, void* workspace, long long workspace_bytes, vm_stream_t stream);
+    int segments, void* workspace, long long workspace_bytes, void* sync,
+    long long sync_bytes, vm_stream_t stream);
 
 /* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape and
  * segment request (0 = the cost model's choice). */
 long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int dstate,
                                             int segments);
+
+/* Sync-buffer bytes for the one-launch segmented form (0 when the single pass runs).
+ * `sync` (ABI v7, both scan entry points; NULL = the two-launch segmented form) must be
+ * zero-filled before its first use; every launch leaves it zero again.  One sync buffer
+ * must not serve two launches that can run at the same time (e.g. on two streams).  The
+ * one-launch form runs when the buffer is large enough and the segmented grid fits one
+ * workgroup per CU (blocks then wait on earlier, resident blocks' published aggregates);
+ * results are identical to the two-launch form. */
+long long vm_selective_scan_sync_bytes(int batch, int dim, int seqlen, int dstate,
+                                       int segments);
 
 /*
  * One-token scan step on `state` (updated in place, own dtype; fp32 math).

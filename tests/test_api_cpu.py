@@ -266,7 +266,7 @@ def test_abi_rejects_bad_arguments_without_gpu():
     lib = _lib.load()
     rc = lib.vm_selective_scan_fwd(*([None, 0, 0, 0] * 2), None, *([None, 0, 0, 0] * 2),
                                    None, None, 0, 0, 0, None, 0, None, 0, 0, 0, None, 0, 0, 0,
-                                   None, 0, 0, 0, 0, 1, 1, 1, 16, 0, 0, None, 0, None)
+                                   None, 0, 0, 0, 0, 1, 1, 1, 16, 0, 0, None, 0, None, 0, None)
     assert rc == -1
     assert b"null required pointer" in lib.vm_last_error()
     rc = lib.vm_add_norm_fwd(None, 0, None, 0, None, None, None, 0, None, 0, 1, 8, 1e-5, 1, None)
@@ -288,6 +288,10 @@ def test_scan_workspace_query_without_gpu():
     chunked = 2 * (9 * 64 * 17) * 4
     legacy = 2 * 4 * 64 * (2 * 16 + 1) * 4
     assert one == 0 and four == max(chunked, legacy)
+    # the one-launch form's sync flags: (nblk + 1) counters per (row, 64-channel group)
+    assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 2 * 1 * (1 + 1) * 4
+    assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
+    assert lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0) > 0
 
 
 def test_library_reads_no_environment():

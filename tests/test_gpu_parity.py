@@ -254,6 +254,55 @@ def _mixer_layout_scan(Bz, D, L, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Bz,D,L,segments", [(1, 1152, 3137, 0), (2, 1152, 3137, 0),
+                                              (1, 40, 3137, 0), (3, 64, 1000, 24),
+                                              (1, 192, 12545, 0)])
+def test_scan_one_launch_matches_two_launch_bitwise(Bz, D, L, segments, dt):
+    """The segmented token-major scan as ONE launch (blocks publish their aggregates and
+    wait on the earlier blocks' flags in a zeroed sync buffer) against the two-launch form:
+    bit-identical y and h_last, over repeated launches on the same sync buffer (every
+    launch must leave it zeroed for the next), with the flags checked zero afterwards."""
+    N, R = 16, 8
+    E = R + 2 * N
+    Lp = (L + 7) // 8 * 8
+    n = Bz * Lp
+    u, delta, A, Bm, Cm, Dv, z, bias, init = _rand_scan(Bz, D, L, N, dt, 7 + D + L)
+    rows = lambda t: t.transpose(1, 2)  # noqa: E731
+    U = torch.zeros(Bz, Lp, D, dtype=dt)
+    DL = torch.zeros(Bz, Lp, D, dtype=dt)
+    XZ = torch.zeros(Bz, Lp, 2 * D, dtype=dt)
+    XD = torch.zeros(Bz, Lp, E, dtype=dt)
+    U[:, :L], DL[:, :L], XZ[:, :L, D:] = rows(u), rows(delta), rows(z)
+    XD[:, :L, R:R + N], XD[:, :L, R + N:] = rows(Bm), rows(Cm)
+    U, DL, XZ, XD = (t.reshape(n, -1).to(DEV) for t in (U, DL, XZ, XD))
+    s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * E, 1, E)
+    A_, Dv_, bias_ = A.to(DEV).contiguous(), Dv.to(DEV), bias.to(DEV)
+    sync = torch.zeros(max(K.scan_sync_bytes(Bz, D, L, N, segments), 4), dtype=torch.uint8,
+                       device=DEV)
+    assert K.scan_sync_bytes(Bz, D, L, N, segments) > 0
+
+    def run(one):
+        y = torch.full((n, D), 7.0, dtype=dt, device=DEV)
+        h = init.to(DEV).contiguous()
+        with options.override(scan_one_launch=one, scan_segments=segments), \
+                K.sync_override(sync):
+            K.scan_raw(U, s_u, DL, s_u, A_, XD[:, R:R + N], s_bc, XD[:, R + N:], s_bc, Dv_,
+                       XZ[:, D:], s_z, bias_, True, h, (D * N, N), h, (D * N, N), y, s_u, Lp,
+                       Bz, D, L, N, K.dtype_code(dt), torch.cuda.current_stream().cuda_stream)
+        return y, h
+
+    y2, h2 = run(False)
+    for _ in range(3):
+        y1, h1 = run(True)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2) and torch.equal(h1, h2)
+        assert not sync.any()
+    ref_y, _ = orc.selective_scan(u.float(), delta.float(), A, Bm.float(), Cm.float(), Dv,
+                                  z.float(), bias, True, init, True)
+    _close(y1.view(Bz, Lp, D)[:, :L].transpose(1, 2), ref_y, 1e-4 if dt == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_scan_token_major_softplus_both_branches(dt):
     """The single-pass token-major kernel carries delta in log2 units, log2(1 + 2^x) with
     a pass-through above x = 20*log2(e) (vm_scan_seq.hip, LG).  Per-channel biases over

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _P = c_void_p
 _LL = c_longlong
@@ -42,14 +42,16 @@ _SIGNATURES = {
          _P, _LL, _LL, _LL, _I,   # out, out_len
          _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
          _I, _P, _LL,             # segments, workspace, workspace_bytes
+         _P, _LL,                 # sync, sync_bytes
          _P], _I),
     "vm_selective_scan_bidir_fwd": (
         [_P, _LL, _LL, _LL, _P, _LL, _LL, _LL, _P, _P, _LL, _LL, _LL, _P, _LL, _LL, _LL,
          _P, _P, _LL, _LL, _LL, _P, _I, _P, _I, _LL, _LL, _P, _I, _LL, _LL,
          _P, _LL, _LL, _LL, _I, _I, _I, _I, _I, _I,
          _I, _P, _P, _P, _P, _P, _I,              # split, A/D/bias/h0/h_last bwd, frame_len
-         _I, _P, _LL, _P], _I),
+         _I, _P, _LL, _P, _LL, _P], _I),
     "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
+    "vm_selective_scan_sync_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_state_update": (
         [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
          _P, _LL, _I, _I, _I, _I, _P], _I),

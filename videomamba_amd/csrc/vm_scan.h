@@ -58,7 +58,9 @@ size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* ch
 // the operands do not fit the token-major kernels (the caller reports the error).
 bool seq_supported(const ScanParams& p, int dtype);
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
-                size_t workspace_bytes, hipStream_t s);
+                size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s);
+// Bytes of the zeroed sync buffer the one-launch chunked form needs (0: single pass).
+size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments);
 // Paired scans need the scalar-B/C kernels and, when segmented, the chunked form.
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes);
 

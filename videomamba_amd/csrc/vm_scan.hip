@@ -480,7 +480,8 @@ static int scan_entry(
     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
     void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
     int batch, int dim, int seqlen, int dstate, int dtype, const PairArgs* pair,
-    int segments, void* workspace, long long workspace_bytes, vm_stream_t stream) {
+    int segments, void* workspace, long long workspace_bytes, void* sync, long long sync_bytes,
+    vm_stream_t stream) {
   if (!u || !delta || !A || !B || !C || !out) {
     vmhost::set_error("%s: null required pointer", name);
     return VM_E_INVALID;
@@ -535,7 +536,8 @@ static int scan_entry(
   }
   // Token-major operands (channel stride 1): channel-per-lane sequential kernels.
   if (seq_supported(p, dtype)) {
-    seq_launch(p, dtype, segments, workspace, ws_bytes, s);
+    seq_launch(p, dtype, segments, workspace, ws_bytes, sync,
+               sync_bytes > 0 ? static_cast<size_t>(sync_bytes) : 0, s);
     return vmhost::launch_status(name);
   }
   // Channel-major operands (step stride 1): time-parallel kernels.
@@ -574,19 +576,21 @@ static int scan_entry(
       seqlen, dstate, dtype
 
 extern "C" int vm_selective_scan_fwd(VM_SCAN_ARGS, int segments, void* workspace,
-                                     long long workspace_bytes, vm_stream_t stream) {
+                                     long long workspace_bytes, void* sync,
+                                     long long sync_bytes, vm_stream_t stream) {
   return scan_entry("vm_selective_scan_fwd", VM_SCAN_PASS, nullptr, segments, workspace,
-                    workspace_bytes, stream);
+                    workspace_bytes, sync, sync_bytes, stream);
 }
 
 extern "C" int vm_selective_scan_bidir_fwd(VM_SCAN_ARGS, int split, const float* A_bwd,
                                            const float* D_bwd, const float* delta_bias_bwd,
                                            const void* h0_bwd, void* h_last_bwd, int frame_len,
                                            int segments, void* workspace,
-                                           long long workspace_bytes, vm_stream_t stream) {
+                                           long long workspace_bytes, void* sync,
+                                           long long sync_bytes, vm_stream_t stream) {
   const PairArgs pair{split, A_bwd, D_bwd, delta_bias_bwd, h0_bwd, h_last_bwd, frame_len};
   return scan_entry("vm_selective_scan_bidir_fwd", VM_SCAN_PASS, &pair, segments, workspace,
-                    workspace_bytes, stream);
+                    workspace_bytes, sync, sync_bytes, stream);
 }
 #undef VM_SCAN_ARGS
 #undef VM_SCAN_PASS
@@ -595,6 +599,12 @@ extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int s
                                                        int dstate, int segments) {
   if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN) return 0;
   return static_cast<long long>(seq_workspace_bytes(batch, dim, seqlen, segments, nullptr));
+}
+
+extern "C" long long vm_selective_scan_sync_bytes(int batch, int dim, int seqlen, int dstate,
+                                                  int segments) {
+  if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN) return 0;
+  return static_cast<long long>(seq_sync_bytes(batch, dim, seqlen, segments));
 }
 
 extern "C" int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long long s_sd,

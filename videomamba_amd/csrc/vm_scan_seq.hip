@@ -489,7 +489,11 @@ struct ChunkWork {
   float* aggS;  // [B][nblk][D]               block delta' sums
   int T;        // steps per segment
   int nblk;     // blocks per sequence
+  unsigned* flags;  // one-launch form: [B][groups][nblk] block-published flags (0 between launches)
+  unsigned* done;   // one-launch form: [B][groups] count of blocks past their wait
 };
+
+template <bool V> struct BoolTag { static constexpr bool value = V; };
 
 template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>
 __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w) {
@@ -546,6 +550,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   f2 Ej[kMaxN / 2];
   f2 agH[kCW];
   float agS[kCW * 64 / (64 * kChW)];
+  if constexpr (PASS == 3) {
+    if (ps.h0) {
+      if (n0 < N) H0 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0, p.h0_dtype);
+      if (n0 + 1 < N) H1 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + 1, p.h0_dtype);
+    }
+  }
   if constexpr (PASS == 2) {
     Pj = w.segP[rowE + wave * D + d];
     const float4* ep = reinterpret_cast<const float4*>(&w.segE[(rowE + wave * D + d) * kMaxN]);
@@ -596,7 +606,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
 #pragma unroll
       for (int i = 0; i < NWD; ++i) {
         dst[i] = bp[i];
-        if constexpr (PASS == 2) dst[NWD + i] = cp[i];
+        if constexpr (PASS != 1) dst[NWD + i] = cp[i];
       }
     }
   };
@@ -618,7 +628,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       if constexpr (!BC1) {
         const char* cb = reinterpret_cast<const char*>(Cq) + static_cast<long long>(bt0) * csl;
         const int cspan = (bt1 - bt0 - 1) * static_cast<int>(csl) + kMaxN * ES;
-        if (PASS == 2 && line < cspan) {
+        if (PASS != 1 && line < cspan) {
           const uint32_t v = *reinterpret_cast<const uint32_t*>(cb + line);
           asm volatile("" ::"v"(v));
         }
@@ -714,91 +724,71 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
                 fmaf(__builtin_amdgcn_exp2f(x.y), sH[0][2 * q + 1][lane], Ej[q].y)};
     }
   }
-  for (int tg = t_beg; tg < t_end; tg += kPF) {
+  // The step loop: EMIT runs the PASS 2 form (z gate, y stores), otherwise the PASS 1 form
+  // (end state and delta sum only).  The prefetch registers hold steps t_beg .. + kPF.
+  auto run_steps = [&](auto emit_tag) {
+    constexpr bool EMIT = decltype(emit_tag)::value;
+    for (int tg = t_beg; tg < t_end; tg += kPF) {
 #pragma unroll
-    for (int j = 0; j < kPF; ++j) {
-      const int t = tg + j;
-      const bool live = t < t_end;
-      const float uu = raw_f32<T>(ru[j]);
-      const float dr = raw_f32<T>(rd[j]);
-      const float zz = raw_f32<T>(rz[j]);
-      const int tn = min(t + kPF, tlast);
-      ru[j] = bload<T>(ur, voff, tn * us);
-      rd[j] = bload<T>(dr_, voff, tn * ds);
-      if (HZ && PASS == 2) rz[j] = bload<T>(zr, voff, tn * zs);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
-      bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
-      float dl;
-      if constexpr (SP) {
-        const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
-        dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
-      } else {
-        dl = fmaf(dr, kLog2e, bias);
-      }
-      dl = live ? dl : 0.0f;
-      const float du = dl * uu;
-      const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
-      const f2 dl2 = {dl, dl}, du2 = {du, du};
-      f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
-#pragma unroll
-      for (int q = 0; q < kMaxN / 2; ++q) {
-        f2 Bp, Cp;
-        if constexpr (sizeof(T) == 2) {
-          Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
-          Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
+      for (int j = 0; j < kPF; ++j) {
+        const int t = tg + j;
+        const bool live = t < t_end;
+        const float uu = raw_f32<T>(ru[j]);
+        const float dr = raw_f32<T>(rd[j]);
+        const float zz = raw_f32<T>(rz[j]);
+        const int tn = min(t + kPF, tlast);
+        ru[j] = bload<T>(ur, voff, tn * us);
+        rd[j] = bload<T>(dr_, voff, tn * ds);
+        if (HZ && EMIT) rz[j] = bload<T>(zr, voff, tn * zs);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
+        bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
+        float dl;
+        if constexpr (SP) {
+          const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
+          dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
         } else {
-          Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
-          Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
+          dl = fmaf(dr, kLog2e, bias);
         }
-        const f2 x = dl2 * A2[q];
-        const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-        h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
-        if constexpr (PASS == 2) {
-          if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
-          else ya = __builtin_elementwise_fma(h[q], Cp, ya);
+        dl = live ? dl : 0.0f;
+        const float du = dl * uu;
+        const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+        const f2 dl2 = {dl, dl}, du2 = {du, du};
+        f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < kMaxN / 2; ++q) {
+          f2 Bp, Cp;
+          if constexpr (sizeof(T) == 2) {
+            Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
+            Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
+          } else {
+            Bp = f2{__uint_as_float(cw[2 * q]), __uint_as_float(cw[2 * q + 1])};
+            Cp = f2{__uint_as_float(cw[NWD + 2 * q]), __uint_as_float(cw[NWD + 2 * q + 1])};
+          }
+          const f2 x = dl2 * A2[q];
+          const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          h[q] = __builtin_elementwise_fma(a, h[q], du2 * Bp);
+          if constexpr (EMIT) {
+            if (q & 1) yb = __builtin_elementwise_fma(h[q], Cp, yb);
+            else ya = __builtin_elementwise_fma(h[q], Cp, ya);
+          }
+        }
+        if constexpr (!EMIT) {
+          sdel += dl;
+        } else {
+          const f2 ys = ya + yb;
+          float y = ys.x + ys.y;
+          // output gate with y's ln2 factor: z / ((1 + e) * log2e)
+          y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
+                                 fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
+                 : y * kLn2f;
+          bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
         }
       }
-      if constexpr (PASS == 1) {
-        sdel += dl;
-      } else {
-        const f2 ys = ya + yb;
-        float y = ys.x + ys.y;
-        // output gate with y's ln2 factor: z / ((1 + e) * log2e)
-        y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
-                               fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
-               : y * kLn2f;
-        bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
-      }
     }
-  }
-
-  if constexpr (PASS == 1) {
-#pragma unroll
-    for (int q = 0; q < kMaxN / 2; ++q) {
-      sH[wave][2 * q][lane] = h[q].x;
-      sH[wave][2 * q + 1][lane] = h[q].y;
-    }
-    sS[wave][lane] = sdel;
-    __syncthreads();
-    // compose the block's segments for states n0, n0 + 1 (wave 0 also writes the prefixes)
-    float E0 = 0.0f, E1 = 0.0f, P = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kChW; ++j) {
-      const float Sj = sS[j][lane];
-      if (active) {
-        *reinterpret_cast<f2*>(&w.segE[(rowE + j * D + d) * kMaxN + n0]) = f2{E0, E1};
-        if (wave == 0) w.segP[rowE + j * D + d] = P;
-      }
-      E0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), E0, sH[j][n0][lane]);
-      E1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), E1, sH[j][n0 + 1][lane]);
-      P += Sj;
-    }
-    if (active) {
-      *reinterpret_cast<f2*>(&w.aggH[(rowA + blk * D + d) * kMaxN + n0]) = f2{E0, E1};
-      if (wave == 0) w.aggS[rowA + blk * D + d] = P;
-    }
-  } else {
+  };
+  // the final segment's h_last and the zeroed padding steps (PASS 2 / the one-launch form)
+  auto finish = [&]() {
     if (t_beg <= tlast && tlast < t_end && active && L > 0) {  // the segment that ends the sequence
       if (ps.hl) {
 #pragma unroll
@@ -809,6 +799,153 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       }
       for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
     }
+  };
+
+  if constexpr (PASS == 2) {
+    run_steps(BoolTag<true>{});
+    finish();
+    return;
+  }
+  run_steps(BoolTag<false>{});
+#pragma unroll
+  for (int q = 0; q < kMaxN / 2; ++q) {
+    sH[wave][2 * q][lane] = h[q].x;
+    sH[wave][2 * q + 1][lane] = h[q].y;
+  }
+  sS[wave][lane] = sdel;
+  __syncthreads();
+  // compose the block's segments for states n0, n0 + 1: entry offsets E_j, delta prefixes
+  // P_j and the block aggregate (PASS 1: all to the workspace; one-launch form: E_j back into
+  // sH[j] in place, the aggregate to the workspace for the blocks after this one)
+  float E0 = 0.0f, E1 = 0.0f, P = 0.0f, Pw = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kChW; ++j) {
+    const float Sj = sS[j][lane];
+    const float Hj0 = sH[j][n0][lane], Hj1 = sH[j][n0 + 1][lane];
+    if constexpr (PASS == 1) {
+      if (active) {
+        *reinterpret_cast<f2*>(&w.segE[(rowE + j * D + d) * kMaxN + n0]) = f2{E0, E1};
+        if (wave == 0) w.segP[rowE + j * D + d] = P;
+      }
+    } else {
+      sH[j][n0][lane] = E0;
+      sH[j][n0 + 1][lane] = E1;
+      if (j == wave) Pw = P;
+    }
+    E0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), E0, Hj0);
+    E1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), E1, Hj1);
+    P += Sj;
+  }
+  if (active) {
+    float* ah = &w.aggH[(rowA + blk * D + d) * kMaxN + n0];
+    if constexpr (PASS == 3) {  // agent-coherent stores: no L2 write-back needed to publish
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(ah),
+                         static_cast<unsigned long long>(__float_as_uint(E0)) |
+                             (static_cast<unsigned long long>(__float_as_uint(E1)) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wave == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned*>(&w.aggS[rowA + blk * D + d]),
+                           __float_as_uint(P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *reinterpret_cast<f2*>(ah) = f2{E0, E1};
+      if (wave == 0) w.aggS[rowA + blk * D + d] = P;
+    }
+  }
+  if constexpr (PASS == 3) {
+    // ---- publish this block's aggregate, then wait for the blocks before it ----
+    unsigned* fl = w.flags + (static_cast<long long>(b) * gridDim.x + gx) * w.nblk;
+    unsigned* dn = w.done + static_cast<long long>(b) * gridDim.x + gx;
+    // Publication without cache maintenance: the aggregates went out as agent-coherent
+    // stores (straight to the coherence point) and the barrier waits until every wave's
+    // stores are acknowledged, so thread 0's agent-coherent flag store follows them there;
+    // readers use agent-coherent loads for the flags and the aggregates.  (Agent-scope
+    // release / acquire fences — an L2 write-back and an L2 invalidate per workgroup — cost
+    // ~10 us at B = 1; the invalidates evicted the other blocks' operands.)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();  // also: every wave's E_j is in sH
+    if (tid == 0) __hip_atomic_store(&fl[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // this segment's entry offsets (composed by the 8 waves) into registers
+    f2 Ew[kMaxN / 2];
+#pragma unroll
+    for (int q = 0; q < kMaxN / 2; ++q) Ew[q] = f2{sH[wave][2 * q][lane], sH[wave][2 * q + 1][lane]};
+    // PASS 2 operands of the first kPF steps, in flight during the wait
+    if (t_beg < t_end) {
+      bc_load(t_beg, bcw[0]);
+#pragma unroll
+      for (int j = 0; j < kPF; ++j) {
+        const int t = min(t_beg + j, tlast);
+        ru[j] = bload<T>(ur, voff, t * us);
+        rd[j] = bload<T>(dr_, voff, t * ds);
+        rz[j] = HZ ? bload<T>(zr, voff, t * zs) : 0u;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // Blocks are dispatched in order and the host launches this form only when the whole
+    // grid is co-resident, so every block waited on is running or done; the bounded spin
+    // still ends (with wrong output, never a hung GPU) if that assumption were broken.
+    // The spin reads are relaxed (coherent loads, no cache invalidation: an acquiring read
+    // per iteration invalidated the L2 under every other block of the XCD, 45 -> 134 us at
+    // B = 1); one acquire fence follows the wait.
+    if (tid == 0) {
+      for (int j = 0; j < blk; ++j) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(&fl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+               ++spins < (1u << 22))
+          __builtin_amdgcn_s_sleep(2);
+      }
+      // the last block past its wait resets the flags for the next launch
+      if (__hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          static_cast<unsigned>(w.nblk - 1)) {
+        for (int j = 0; j < w.nblk; ++j)
+          __hip_atomic_store(&fl[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();  // every wave's reads below follow the flags thread 0 saw
+    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
+    H0 *= kLog2e;  // log2 units
+    H1 *= kLog2e;
+    const int ci = tid >> 3;
+    for (int r0 = 0; r0 < blk; r0 += kChW) {
+      if (r0 > 0) __syncthreads();  // every wave is done reading the previous group
+#pragma unroll
+      for (int j = 0; j < kChW; ++j) {
+        unsigned long long v = 0ull;
+        if (r0 + j < blk && ci < nch)
+          v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                    &w.aggH[(rowA + (r0 + j) * D + d0) * kMaxN + 2 * tid]),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sH[j][2 * (tid & 7)][ci] = __uint_as_float(static_cast<unsigned>(v));
+        sH[j][2 * (tid & 7) + 1][ci] = __uint_as_float(static_cast<unsigned>(v >> 32));
+      }
+      const int jj = r0 + (tid >> 6);
+      sS[tid >> 6][lane] =
+          jj < blk && lane < nch
+              ? __uint_as_float(__hip_atomic_load(
+                    reinterpret_cast<unsigned*>(&w.aggS[rowA + jj * D + d0 + lane]),
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              : 0.0f;
+      __syncthreads();
+      const int nj = min(kChW, blk - r0);
+      for (int j = 0; j < nj; ++j) {
+        const float Sj = sS[j][lane];
+        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, sH[j][n0][lane]);
+        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, sH[j][n0 + 1][lane]);
+      }
+    }
+    __syncthreads();  // sH[0] is rewritten with the block entry
+    sH[0][n0][lane] = H0;
+    sH[0][n0 + 1][lane] = H1;
+    __syncthreads();
+    // this segment's entry: exp2(A P_j) * H_blk + E_j
+#pragma unroll
+    for (int q = 0; q < kMaxN / 2; ++q) {
+      const f2 x = A2[q] * f2{Pw, Pw};
+      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), sH[0][2 * q][lane], Ew[q].x),
+                fmaf(__builtin_amdgcn_exp2f(x.y), sH[0][2 * q + 1][lane], Ew[q].y)};
+    }
+    run_steps(BoolTag<true>{});
+    finish();
   }
 }
 
@@ -998,6 +1135,11 @@ bool seq_supported(const ScanParams& p, int dtype) {
 template <typename T, bool SP, bool HZ, bool BC1, bool PAIR>
 static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
+  if (w.flags) {  // one launch: blocks hand their aggregates on through the sync flags
+    hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
+                       p, w);
+    return;
+  }
   hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
                      p, w);
   hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
@@ -1026,6 +1168,30 @@ static void launch_chunk(const ScanParams& p, const ChunkWork& w, hipStream_t s)
 #undef VM_CH
 }
 
+// One-launch chunked form: sync flags per (row, channel group, block) plus a counter per
+// (row, channel group).  Used when the caller passes a zeroed sync buffer this large and
+// the whole grid fits one workgroup per CU (so every block it waits on is resident).
+size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments) {
+  const int S = segments_for(batch, dim, seqlen, segments);
+  if (S <= 1) return 0;
+  int T, nblk;
+  chunk_geometry(seqlen, S, &T, &nblk);
+  const size_t groups = (dim + 63) / 64;
+  return static_cast<size_t>(batch) * groups * (nblk + 1) * sizeof(unsigned);
+}
+
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes) {
   int S = 1;
   const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
@@ -1033,13 +1199,19 @@ bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t wor
 }
 
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
-                size_t workspace_bytes, hipStream_t s) {
+                size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s) {
   int S = 1;
   const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
   const int es = dtype == VM_DTYPE_BF16 ? 2 : 4;
   if (S > 1 && workspace && workspace_bytes >= need && seq_sgpr_bc(p, es)) {
     ChunkWork w{};
     chunk_geometry(p.seqlen, S, &w.T, &w.nblk);
+    const long long grid = static_cast<long long>((p.dim + 63) / 64) * w.nblk * p.batch;
+    if (sync && sync_bytes >= seq_sync_bytes(p.batch, p.dim, p.seqlen, segments) &&
+        grid <= device_cus()) {
+      w.flags = static_cast<unsigned*>(sync);
+      w.done = w.flags + static_cast<size_t>(p.batch) * ((p.dim + 63) / 64) * w.nblk;
+    }
     const size_t nb = static_cast<size_t>(p.batch) * w.nblk;
     w.segE = static_cast<float*>(workspace);
     w.segP = w.segE + nb * kChW * p.dim * kMaxN;

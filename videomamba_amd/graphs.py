@@ -71,6 +71,7 @@ class StreamingChunkGraph:
         self._plist = None
         self._tpos_offset = None  # temporal offset whose embedding slice static_tpos holds
         self._ws = None  # scan scratch owned by the captured graphs
+        self._sync = None  # the one-launch scan's sync flags (zeroed; replays leave them zeroed)
 
     # ------------------------------------------------------------------ state
     @property
@@ -140,6 +141,11 @@ class StreamingChunkGraph:
                    for mx in m._mixers())
         if self._ws is None or self._ws.numel() < max(need, 1):
             self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+        # the one-launch scan's sync flags: zeroed once, left zeroed by every replay
+        sync_need = max(K.scan_sync_bytes(self.batch, mx.d_inner, L, mx.d_state)
+                        for mx in m._mixers())
+        if self._sync is None or self._sync.numel() < max(sync_need, 1):
+            self._sync = torch.zeros(max(sync_need, 4096), dtype=torch.uint8, device=self.device)
         return self._ws
 
     def _capture(self, has_cls: bool):
@@ -147,12 +153,14 @@ class StreamingChunkGraph:
         ws = self._workspace()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.no_grad(), torch.cuda.stream(side), K.scratch_override(ws):
+        with torch.no_grad(), torch.cuda.stream(side), K.scratch_override(ws), \
+                K.sync_override(self._sync):
             for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
                 self._body(has_cls)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws):
+        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws), \
+                K.sync_override(self._sync):
             outs = self._body(has_cls)
         self._pool = g.pool()
         self.load_state(saved)  # warm-up passes advanced the state: restore it

@@ -140,6 +140,51 @@ def scratch(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
     return buf
 
 
+_SYNC = {}
+_SYNC_OVERRIDE = [None]
+
+
+class sync_override:
+    """Within the block the one-launch segmented scan uses ``buf`` (a zero-filled uint8
+    device tensor owned by the caller, e.g. a captured graph) as its sync buffer instead of
+    the per-stream one.  The library leaves the buffer zeroed after every launch."""
+
+    def __init__(self, buf: Tensor):
+        self.buf = buf
+
+    def __enter__(self):
+        self.prev = _SYNC_OVERRIDE[0]
+        _SYNC_OVERRIDE[0] = self.buf
+        return self.buf
+
+    def __exit__(self, *exc):
+        _SYNC_OVERRIDE[0] = self.prev
+        return False
+
+
+def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
+    """The one-launch scan's sync buffer: zero-filled when allocated, left zeroed by every
+    launch, one per (device, stream) so no two concurrent launches share it; grown (a new
+    zeroed buffer) when a shape needs more."""
+    if nbytes <= 0:
+        return None
+    ov = _SYNC_OVERRIDE[0]
+    if ov is not None:
+        return ov if ov.numel() >= nbytes else None
+    key = (device.type, device.index, stream)
+    buf = _SYNC.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(nbytes, 4096), dtype=torch.uint8, device=device)
+        _SYNC[key] = buf
+    return buf
+
+
+def scan_sync_bytes(batch: int, dim: int, seqlen: int, dstate: int,
+                    segments: Optional[int] = None) -> int:
+    seg = options.get().scan_segments if segments is None else segments
+    return int(_lib.load().vm_selective_scan_sync_bytes(batch, dim, seqlen, dstate, seg))
+
+
 def scan_workspace_bytes(batch: int, dim: int, seqlen: int, dstate: int,
                          segments: Optional[int] = None) -> int:
     seg = options.get().scan_segments if segments is None else segments
@@ -158,6 +203,7 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
     seg = int(options.get().scan_segments)
     ws_bytes = 0
     ws = None
+    sync, sync_bytes = None, 0
     if u_s[1] == 1:
         ws_bytes = scan_workspace_bytes(batch, dim, seqlen, dstate, seg)
         if workspace is not None:
@@ -166,6 +212,11 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
             ws = workspace
         else:
             ws = scratch(u.device, int(stream), ws_bytes)
+        if options.get().scan_one_launch:
+            sync_bytes = scan_sync_bytes(batch, dim, seqlen, dstate, seg)
+            sync = sync_buffer(u.device, int(stream), sync_bytes)
+            if sync is None:
+                sync_bytes = 0
     args = (_p(u), u_s[0], u_s[1], u_s[2], _p(delta), dl_s[0], dl_s[1], dl_s[2], _p(A32),
             _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
             _p(D32), _p(z), z_s[0], z_s[1], z_s[2], _p(bias32), int(softplus),
@@ -173,12 +224,14 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
             _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0],
             hl_s[1], _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate, dtype)
     if pair is None:
-        rc = lib.vm_selective_scan_fwd(*args, seg, _p(ws), ws_bytes, stream)
+        rc = lib.vm_selective_scan_fwd(*args, seg, _p(ws), ws_bytes, _p(sync), sync_bytes,
+                                       stream)
         _lib.check(rc, "vm_selective_scan_fwd")
         return
     split, a_b, d_b, bias_b, h0_b, hl_b, frame = pair
     rc = lib.vm_selective_scan_bidir_fwd(*args, split, _p(a_b), _p(d_b), _p(bias_b), _p(h0_b),
-                                         _p(hl_b), frame, seg, _p(ws), ws_bytes, stream)
+                                         _p(hl_b), frame, seg, _p(ws), ws_bytes, _p(sync),
+                                         sync_bytes, stream)
     _lib.check(rc, "vm_selective_scan_bidir_fwd")
 
 

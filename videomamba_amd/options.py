@@ -17,6 +17,10 @@ documented options object; tests and sweeps change them with :func:`override`.
                      library heuristic; "tune": record new shapes (slow, offline).
                      Initialised from ``VM_GEMM_TUNING`` when that is set (the tuning
                      script's switch); nothing else is read from the environment.
+    scan_one_launch  True (default): a segmented token-major scan whose grid fits one
+                     workgroup per CU runs as one launch (blocks hand their aggregates on
+                     through a zeroed sync buffer, vm_selective_scan_fwd ``sync``); False:
+                     the two-launch form (identical results).
     small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -42,6 +46,7 @@ class Options:
     mixer_layout: str = "auto"
     scan_segments: int = 0
     fused_conv_proj: bool = True
+    scan_one_launch: bool = True
     gemm_tuning: str = "on"
     small_gemm_rows: int = 4096
 
