@@ -12,6 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # small-M GEMM with 32-row tiles where 64-row tiles run (out_proj at B = 1: 495 workgroups)
+    "lin32": [("vm_gemm.hip", "  const int bm = big ? 128 : 64;", "  const int bm = big ? 128 : 32;"),
+              ("vm_gemm.hip", "    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p);    \\",
+               "    else hipLaunchKernelGGL((linear_kernel<32, NKV>), grid, dim3(256), lds, s, p);    \\")],
     # scan grids without (sc_xcd: single pass) / with (ch_xcd: chunked) the XCD renumbering
     "sc_xcd": [("vm_scan_seq.hip", "constexpr bool kSeqXcdRemap = true;", "constexpr bool kSeqXcdRemap = false;")],
     "ch_xcd": [("vm_scan_seq.hip", "constexpr bool kChunkXcdRemap = false;", "constexpr bool kChunkXcdRemap = true;")],
