@@ -1,4 +1,4 @@
 set -o pipefail
-for v in product lin32 product lin32; do
-  timeout -k 10 120 python -u scripts/diag/variant_linear.py $v 2>&1 | grep '{' || exit 1
+for a in "" "small_gemm_max_n=4096" "" "small_gemm_max_n=4096"; do
+  timeout -k 10 180 python -u scripts/diag/b1_chunk_graph.py 50 $a 2>&1 | grep "graph replays" || exit 1
 done

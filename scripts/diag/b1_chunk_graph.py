@@ -11,6 +11,11 @@ from videomamba_amd.graphs import StreamingChunkGraph  # noqa: E402
 from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+if len(sys.argv) > 2:  # option overrides, e.g. small_gemm_max_n=4096
+    from videomamba_amd import options
+    for kv in sys.argv[2:]:
+        k, v = kv.split("=")
+        options._OPTS = options.dataclasses.replace(options.get(), **{k: type(getattr(options.get(), k))(v)})
 torch.manual_seed(0)
 model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16).cuda().to(torch.bfloat16).eval()
 x = torch.randn(1, 3, 16, 224, 224, device="cuda").to(torch.bfloat16)

@@ -59,7 +59,8 @@ def _small_gemm_ok(x: Tensor, w: Tensor, b: Optional[Tensor], out: Optional[Tens
     ok16 = lambda t: t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(1) == 1  # noqa: E731
     return (0 < x.shape[0] <= lim and b is None and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.is_cuda and x.shape[1] in _SMALL_GEMM_K
-            and w.shape[0] % 8 == 0 and w.shape[0] <= 1024 and ok16(x) and ok16(w) and (out is None or ok16(out)))
+            and w.shape[0] % 8 == 0 and w.shape[0] <= options.get().small_gemm_max_n and ok16(x)
+            and ok16(w) and (out is None or ok16(out)))
 
 
 def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:

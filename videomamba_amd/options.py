@@ -24,6 +24,8 @@ documented options object; tests and sweeps change them with :func:`override`.
     small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
+    small_gemm_max_n ... and at most this many output columns (default 1024: out_proj;
+                     in_proj's N = 2 * d_inner stays on the library GEMM).
 
 Options are process-global (not thread-local): the model is driven from one host thread.
 """
@@ -49,6 +51,7 @@ class Options:
     scan_one_launch: bool = True
     gemm_tuning: str = "on"
     small_gemm_rows: int = 4096
+    small_gemm_max_n: int = 1024
 
     def validate(self) -> None:
         if self.mixer_layout not in _LAYOUTS:
