@@ -12,6 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # single-pass scan without the one-step-early delta (kSeqDeltaAhead)
+    "sc_noahead": [("vm_scan_seq.hip", "constexpr bool kSeqDeltaAhead = true;", "constexpr bool kSeqDeltaAhead = false;")],
     # small-M GEMM with 32-row tiles where 64-row tiles run (out_proj at B = 1: 495 workgroups)
     "lin32": [("vm_gemm.hip", "  const int bm = big ? 128 : 64;", "  const int bm = big ? 128 : 32;"),
               ("vm_gemm.hip", "    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p);    \\",

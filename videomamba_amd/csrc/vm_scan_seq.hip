@@ -37,6 +37,7 @@ constexpr int kMaxSeg = 256;  // segments per sequence
 constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
 constexpr bool kSeqXcdRemap = true;  // grids renumbered per XCD (see scan_seq_kernel)
 constexpr bool kChunkXcdRemap = false;
+constexpr bool kSeqDeltaAhead = true;  // single-pass: next step's delta computed a step early
 
 // Buffer descriptor over a wave-uniform base: per-step byte offsets go in soffset (SGPR),
 // the lane's channel offset in voffset, so no per-lane 64-bit address math runs per step.
@@ -250,6 +251,23 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 
   float sdel = 0.0f;
+  // delta of a step from its raw dt (log2 units under LG)
+  auto delta_of = [&](uint32_t raw) {
+    const float dr = raw_f32<T>(raw);
+    float dl;
+    if constexpr (LG) {
+      const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
+      dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
+    } else {
+      dl = dr + bias;
+      if (SP) dl = softplus_fast(dl);
+    }
+    return dl;
+  };
+  // The next step's delta is computed at the end of the current step (its dt landed kPF - 1
+  // steps ago), so the softplus chain shares a scheduling region with this step's y
+  // reduction instead of heading the next step's dependent chain (kSeqDeltaAhead).
+  float dl_nx = 0.0f;
   // One step of the recurrence (step t, prefetch slot j): consume the registers loaded
   // kPF steps ago and refill the slot at the given (per-lane voffset, SGPR soffset) pairs.
   const float* blk = &sbc[0][0][0];
@@ -258,7 +276,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
                   const int j, const bool live, const int vu, const int su, const int vd,
                   const int sd, const int vz, const int sz) {
       const float uu = raw_f32<T>(ru[j]);
-      const float dr = raw_f32<T>(rd[j]);
+      const uint32_t rdj = rd[j];
       const float zz = raw_f32<T>(rz[j]);
       ru[j] = bload<T>(ur, vu, su);
       rd[j] = bload<T>(dr_, vd, sd);
@@ -273,14 +291,8 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       // sink them below all eight steps, collapsing the prefetch distance to zero
       // (letting ALU work cross this barrier, mask 0x787, measured 10-25 % slower)
       __builtin_amdgcn_sched_barrier(0);
-      float dl;
-      if constexpr (LG) {
-        const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
-        dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
-      } else {
-        dl = dr + bias;
-        if (SP) dl = softplus_fast(dl);
-      }
+      float dl = kSeqDeltaAhead ? dl_nx : delta_of(rdj);
+      if constexpr (kSeqDeltaAhead) dl_nx = delta_of(rd[(j + 1) & (kPF - 1)]);
       dl = live ? dl : 0.0f;
       const float du = dl * uu;
       // output gate; under LG it also carries y's ln2 factor: z / ((1 + e) * log2e)
@@ -374,6 +386,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       }
   };
 
+  if constexpr (kSeqDeltaAhead) dl_nx = delta_of(rd[0]);
   int k0 = 0;
   if constexpr (SB) {
     // Main loop: whole 8-step groups that are all live and whose refills (kPF steps
@@ -410,6 +423,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         tz[j] = HZ && MODE != 1 ? bload<T>(zr, voff, t * zs) : 0u;
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (kSeqDeltaAhead) dl_nx = delta_of(td[0]);
       for (int tb = t0; tb < t_end; tb += kPF) {
 #pragma unroll
         for (int j = 0; j < kPF; ++j) {
@@ -726,15 +740,22 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   }
   // The step loop: EMIT runs the PASS 2 form (z gate, y stores), otherwise the PASS 1 form
   // (end state and delta sum only).  The prefetch registers hold steps t_beg .. + kPF.
+  auto delta_of = [&](uint32_t raw) {  // delta' = softplus(dt + bias) * log2e
+    const float x = fmaf(raw_f32<T>(raw), kLog2e, bias);  // (dt + bias) * log2e
+    if constexpr (SP)
+      return x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
+    return x;
+  };
   auto run_steps = [&](auto emit_tag) {
     constexpr bool EMIT = decltype(emit_tag)::value;
+    // the next step's delta is computed a step early (as in scan_seq_kernel)
+    float dl_nx = delta_of(rd[0]);
     for (int tg = t_beg; tg < t_end; tg += kPF) {
 #pragma unroll
       for (int j = 0; j < kPF; ++j) {
         const int t = tg + j;
         const bool live = t < t_end;
         const float uu = raw_f32<T>(ru[j]);
-        const float dr = raw_f32<T>(rd[j]);
         const float zz = raw_f32<T>(rz[j]);
         const int tn = min(t + kPF, tlast);
         ru[j] = bload<T>(ur, voff, tn * us);
@@ -743,13 +764,8 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
         bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
-        float dl;
-        if constexpr (SP) {
-          const float x = fmaf(dr, kLog2e, bias);  // (dt + bias) * log2e
-          dl = x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
-        } else {
-          dl = fmaf(dr, kLog2e, bias);
-        }
+        float dl = dl_nx;
+        dl_nx = delta_of(rd[(j + 1) & (kPF - 1)]);
         dl = live ? dl : 0.0f;
         const float du = dl * uu;
         const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
