@@ -12,6 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # scans without the one-step-early gate factor (kSeqGateAhead)
+    "sc_nogate": [("vm_scan_seq.hip", "constexpr bool kSeqGateAhead = true;", "constexpr bool kSeqGateAhead = false;")],
     # single-pass scan without the one-step-early delta (kSeqDeltaAhead)
     "sc_noahead": [("vm_scan_seq.hip", "constexpr bool kSeqDeltaAhead = true;", "constexpr bool kSeqDeltaAhead = false;")],
     # small-M GEMM with 32-row tiles where 64-row tiles run (out_proj at B = 1: 495 workgroups)

@@ -37,7 +37,8 @@ constexpr int kMaxSeg = 256;  // segments per sequence
 constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
 constexpr bool kSeqXcdRemap = true;  // grids renumbered per XCD (see scan_seq_kernel)
 constexpr bool kChunkXcdRemap = false;
-constexpr bool kSeqDeltaAhead = true;  // single-pass: next step's delta computed a step early
+constexpr bool kSeqDeltaAhead = true;  // next step's delta computed a step early
+constexpr bool kSeqGateAhead = true;   // next step's output-gate factor computed a step early
 
 // Buffer descriptor over a wave-uniform base: per-step byte offsets go in soffset (SGPR),
 // the lane's channel offset in voffset, so no per-lane 64-bit address math runs per step.
@@ -268,6 +269,13 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   // steps ago), so the softplus chain shares a scheduling region with this step's y
   // reduction instead of heading the next step's dependent chain (kSeqDeltaAhead).
   float dl_nx = 0.0f;
+  // likewise the output gate's factor z / ((1 + e^-z) log2e) of the next step (LG with z)
+  constexpr bool kGA = kSeqGateAhead && LG && HZ && MODE != 1;
+  auto gate_of = [&](uint32_t raw) {
+    const float zz = raw_f32<T>(raw);
+    return zz * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e));
+  };
+  float g_nx = 0.0f;
   // One step of the recurrence (step t, prefetch slot j): consume the registers loaded
   // kPF steps ago and refill the slot at the given (per-lane voffset, SGPR soffset) pairs.
   const float* blk = &sbc[0][0][0];
@@ -293,11 +301,17 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
       __builtin_amdgcn_sched_barrier(0);
       float dl = kSeqDeltaAhead ? dl_nx : delta_of(rdj);
       if constexpr (kSeqDeltaAhead) dl_nx = delta_of(rd[(j + 1) & (kPF - 1)]);
+      float gf = 0.0f;
+      if constexpr (kGA) {
+        gf = g_nx;
+        g_nx = gate_of(rz[(j + 1) & (kPF - 1)]);
+      }
       dl = live ? dl : 0.0f;
       const float du = dl * uu;
       // output gate; under LG it also carries y's ln2 factor: z / ((1 + e) * log2e)
       auto gate = [&](float y) {
         if constexpr (LG) {
+          if constexpr (kGA) return y * gf;
           if (HZ)
             return y * (zz * __builtin_amdgcn_rcpf(
                                  fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)));
@@ -387,6 +401,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   };
 
   if constexpr (kSeqDeltaAhead) dl_nx = delta_of(rd[0]);
+  if constexpr (kGA) g_nx = gate_of(rz[0]);
   int k0 = 0;
   if constexpr (SB) {
     // Main loop: whole 8-step groups that are all live and whose refills (kPF steps
@@ -424,6 +439,7 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (kSeqDeltaAhead) dl_nx = delta_of(td[0]);
+      if constexpr (kGA) g_nx = gate_of(tz[0]);
       for (int tb = t0; tb < t_end; tb += kPF) {
 #pragma unroll
         for (int j = 0; j < kPF; ++j) {
@@ -748,8 +764,15 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   };
   auto run_steps = [&](auto emit_tag) {
     constexpr bool EMIT = decltype(emit_tag)::value;
-    // the next step's delta is computed a step early (as in scan_seq_kernel)
+    // the next step's delta and output-gate factor are computed a step early (as in
+    // scan_seq_kernel)
+    constexpr bool GA = kSeqGateAhead && EMIT && HZ;
+    auto gate_of = [&](uint32_t raw) {
+      const float zz = raw_f32<T>(raw);
+      return zz * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e));
+    };
     float dl_nx = delta_of(rd[0]);
+    float g_nx = GA ? gate_of(rz[0]) : 0.0f;
     for (int tg = t_beg; tg < t_end; tg += kPF) {
 #pragma unroll
       for (int j = 0; j < kPF; ++j) {
@@ -767,6 +790,11 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         float dl = dl_nx;
         dl_nx = delta_of(rd[(j + 1) & (kPF - 1)]);
         dl = live ? dl : 0.0f;
+        float gf = 0.0f;
+        if constexpr (GA) {
+          gf = g_nx;
+          g_nx = gate_of(rz[(j + 1) & (kPF - 1)]);
+        }
         const float du = dl * uu;
         const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
         const f2 dl2 = {dl, dl}, du2 = {du, du};
@@ -795,9 +823,11 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
           const f2 ys = ya + yb;
           float y = ys.x + ys.y;
           // output gate with y's ln2 factor: z / ((1 + e) * log2e)
-          y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
-                                 fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
-                 : y * kLn2f;
+          if constexpr (GA) y *= gf;
+          else
+            y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
+                                   fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
+                   : y * kLn2f;
           bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
         }
       }
