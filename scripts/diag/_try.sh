@@ -1,3 +1,4 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t8.log 2>&1; rc=$?; tail -2 gpurun_out/t8.log; [ $rc -eq 0 ] || exit $rc
-for v in product sc_nogate product sc_nogate product sc_nogate; do timeout -k 10 120 python -u scripts/diag/variant_scan.py $v 336 1 2>&1 | grep '{' || exit 1; done
+for b in 288 336 392 448 504; do
+  timeout -k 10 300 python -u bench.py --batch $b --steps 8 --warmup 3 --no-cpu-baseline --p50-chunks 5 --scan-reps 3 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($b, d['value'], d['ms_per_step'])" || exit 1
+done
