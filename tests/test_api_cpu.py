@@ -294,6 +294,20 @@ def test_scan_workspace_query_without_gpu():
     assert lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0) > 0
 
 
+def test_scan_segment_cost_model_choices_without_gpu():
+    """The measured segment cost model (vm_scan_seq.hip::choose_segments, fitted to
+    profiles/r02_scan_segments_sweep.jsonl) as seen through the sync-buffer query:
+    (nblk + 1) flags per (row, 64-channel group) at M-16f (D = 1152, 18 groups).  B = 1:
+    S = 112 -> 14 blocks of 8 segments (252 workgroups, one per CU); B = 2 .. 8: S = 56 ->
+    7 blocks (the round-1 wave-target rule chose 2-3x slower counts there); B >= 72 (1,280+
+    waves): single pass, no segments."""
+    lib = _lib.load()
+    nblk = lambda B, L: lib.vm_selective_scan_sync_bytes(B, 1152, L, 16, 0) // (B * 18 * 4) - 1  # noqa: E731
+    assert nblk(1, 3137) == 14 and nblk(1, 12545) == 14
+    assert nblk(2, 3137) == nblk(4, 3137) == nblk(8, 3137) == 7
+    assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
+
+
 def test_library_reads_no_environment():
     """The C library has no configuration channel besides its arguments:
     no getenv in any product source."""
