@@ -11,10 +11,12 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
-Other configs: --config m32 (VideoMamba-M 32x224^2, C4: a GLOBAL batch, --global-batch,
-default 672 clips, split across ranks with sharding.shard_range — strong scaling; run under
-torchrun for the 8-GPU case), --config ti8 --full-sequence (C2).  The roofline block is
-always the scan at the M-16f shape.
+Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 336 clips per rank by default, so
+the 1/2/4/8-GPU curve keeps every GPU at the batch where the scan holds its occupancy —
+weak scaling; --global-batch G instead splits G clips across ranks with
+sharding.shard_range — strong scaling; run under torchrun for the 8-GPU case), --config ti8
+--full-sequence (C2).  The metric name follows the config ("<model> <T>f 224").  The
+roofline block is always the scan at the M-16f shape.
 
 --stub-cpu replaces the encoder by a trivial CPU op and runs the same rank / barrier /
 max-over-ranks / JSON-line control flow on the gloo backend (tests/test_sharding_gloo.py
@@ -54,8 +56,7 @@ LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
     "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),  # C3 (default)
-    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M",  # C4
-                global_batch=672),
+    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M"),  # C4
     "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti",  # C1 / C2 shape
                 batch=512),
 }
@@ -75,7 +76,9 @@ def _args():
     ap.add_argument("--p50-chunks", type=int, default=100)
     ap.add_argument("--scan-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads (0: the CPUs this process may run on, at most 16 — "
+                         "a one-GPU box's share)")
     ap.add_argument("--full-sequence", action="store_true",
                     help="stateless full-sequence forward (C2) instead of a stateful chunk")
     a = ap.parse_args()
@@ -93,17 +96,18 @@ def _sync_barrier(world):
 
 
 def _pmc_traffic(shape, kernel):
-    """HBM bytes per scan launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-    (profiles/scan_traffic_*.json, gfx950 read correction applied) when they were taken
-    at this shape; None otherwise.  PMC collection needs its own profiler run, so it is
-    not repeated inside the timed bench."""
+    """(HBM bytes per scan launch, source file) from the committed rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes (profiles/scan_traffic_*.json, calibrated gfx950 read /
+    write ratios applied) when they were taken at this shape and kernel form; (None, None)
+    otherwise.  PMC collection needs its own profiler run, so it is not repeated inside the
+    timed bench: the JSON line says where the number comes from."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "scan_traffic_*.json")))[::-1]:
         with open(path) as f:
             rec = json.load(f)
         if rec.get("shape") == shape and rec.get("kernel", "").startswith(kernel):
-            return int(rec["hbm_bytes_per_launch"])
-    return None
+            return int(rec["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def scan_roofline(batch, reps, device, layout="tm"):
@@ -163,9 +167,13 @@ def scan_roofline(batch, reps, device, layout="tm"):
     floor_s = batch * D * L * N / 64 * (CYC_EXP + 4 * CYC_FMA) / SIMDS / CLOCK_HZ
     shape = f"B={batch} D={D} L={L} N={N} bf16, stateful"
     kname = "vm::scan_seq_kernel" if layout == "tm" else "vm::scan_v5_kernel"
+    traffic, tsrc = _pmc_traffic(shape, kname)
     return {"bound": "hbm", "kernel": kname, "layout": layout, "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": _pmc_traffic(shape, kname), "avg_us": round(avg_s * 1e6, 2),
+            "traffic": traffic,
+            "traffic_source": (f"committed rocprofv3 PMC passes at this shape ({tsrc}), not "
+                               "measured in this run" if tsrc else None),
+            "avg_us": round(avg_s * 1e6, 2),
             "bytes_per_launch": algo, "shape": shape,
             "valu_model": {"floor_us": round(floor_s * 1e6, 2),
                            "frac_of_valu_floor": round(floor_s / avg_s, 4),
@@ -282,23 +290,59 @@ def _oracle_clip_seconds(cfg, runs=3):
     return statistics.median(times)
 
 
-# The timed oracle against the reference's own CPU path, both on 8 threads of the build
-# container (profiles/r02_cpu_calibration.json, scripts/cpu_calibration.py): the port runs
-# within the survey's +-15 % band of the reference, so its rate stands in for the reference's.
-CPU_CALIBRATION = {"threads": 8, "oracle_over_reference_s_per_clip": {"ti8": 1.161, "m16": 0.895},
-                   "reference_s_per_clip": {"ti8": 3.32, "m16": 24.9},
-                   "source": "profiles/r02_cpu_calibration.json"}
+# The timed oracle against the reference's own CPU path, both timed warm in one session on
+# the same 8 threads of the build container (scripts/cpu_calibration.py): the port's time
+# over the reference's, per config.  Read from the committed record at run time.
+CPU_CALIBRATION_FILE = os.path.join(ROOT, "profiles", "r03_cpu_calibration.json")
+
+
+def _cpu_calibration():
+    try:
+        with open(CPU_CALIBRATION_FILE) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {"threads": rec.get("threads"), "cpu_model": rec.get("cpu_model"),
+            "oracle_over_reference_s_per_clip": {
+                k: v["oracle_over_reference"] for k, v in rec.get("configs", {}).items()},
+            "reference_s_per_clip": {
+                k: v["reference_s_per_clip"] for k, v in rec.get("configs", {}).items()},
+            "source": os.path.relpath(CPU_CALIBRATION_FILE, ROOT)}
+
+
+def _cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count()
+    return model, affinity
 
 
 def cpu_baseline(cfg, threads):
     """the oracle (the CPU restatement pinned to the reference) on the host
-    cores, median of 3 after 1 warm-up, fp32 B=1: the bench clip, and C1 (Ti 8x224^2)."""
+    cores, median of 3 after 1 warm-up, fp32 B=1: the bench clip, and C1 (Ti 8x224^2).
+    ``threads`` 0 = the CPUs this process may run on, capped at 16 (a one-GPU box's share of
+    the host: os.cpu_count() there counts the whole machine, shared with other jobs)."""
+    model, affinity = _cpu_info()
+    if threads <= 0:
+        threads = max(1, min(16, affinity or 1))
     torch.set_num_threads(threads)
     dt = _oracle_clip_seconds(cfg)
     ti = CONFIGS["ti8"]
     dt_c1 = _oracle_clip_seconds(ti)
     return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
-            "cores": threads, "kind": "port", "calibration": CPU_CALIBRATION,
+            "cores": threads, "kind": "port", "cpu_model": model,
+            "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+            "calibration": _cpu_calibration(),
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
                       f"median of 3 after 1 warm-up ({dt:.2f} s), oracle/videomamba_oracle.py",
             "c1": {"value": round(ti["frames"] * 196 / dt_c1, 2), "unit": "video-tokens/s",
@@ -330,12 +374,19 @@ def _timed_steps(step, steps, warmup, world, device, sync):
     return max_over_ranks(elapsed, device), out
 
 
+def metric_name(cfg):
+    """BASELINE.json's metric, named for the workload actually run (the headline string
+    exactly for the C3 default, VideoMamba-M 16f)."""
+    return (f"video-tokens/sec per GPU + streaming-chunk p50 latency, "
+            f"{cfg['name']} {cfg['frames']}f 224")
+
+
 def _base_line(args, cfg, world, global_batch, per_rank, elapsed, strong):
     T = cfg["frames"]
     ms_per_step = elapsed / args.steps * 1e3
     value = global_batch * T * 196 * args.steps / elapsed
     return {
-        "metric": "video-tokens/sec per GPU + streaming-chunk p50 latency, VideoMamba-M 16f 224",
+        "metric": metric_name(cfg),
         "value": round(value, 1), "unit": "video-tokens/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "strong" if strong else "weak",
@@ -404,8 +455,8 @@ def main():
                                num_frames=cfg["frames"], pool_type="cls+avg")
     model = model.to(device=device, dtype=torch.bfloat16).eval()
     T = cfg["frames"]
-    global_batch = args.global_batch or (cfg.get("global_batch") if args.batch_default else None)
-    if global_batch:  # C4: one global batch split across ranks (strong scaling)
+    global_batch = args.global_batch
+    if global_batch:  # --global-batch: one global batch split across ranks (strong scaling)
         a, b = shard_range(global_batch, world, rank)
         B, strong = b - a, True
     else:  # C3: a fixed batch per rank (weak scaling)
@@ -422,6 +473,8 @@ def main():
     elapsed, out = _timed_steps(step, args.steps, args.warmup, world, device,
                                 torch.cuda.synchronize)
     assert torch.isfinite(out[1].float()).all()
+    from videomamba_amd import kernels as K
+    K.check_scan_sync()  # no one-launch scan hand-off timed out (outside the timed region)
     line = _base_line(args, cfg, world, global_batch, B, elapsed, strong)
 
     # streaming-chunk p50 latency at B=1 (one stateful chunk of the same clip shape):

@@ -39,7 +39,10 @@
  *   - Work is enqueued on `stream` (a hipStream_t); nothing synchronises, so calls are
  *     safe to capture into a hipGraph.
  *   - Return 0 on success, a negative VM_E* code otherwise; vm_last_error() gives the
- *     message.  Nothing is thrown across the ABI.  Kernels are deterministic (no atomics).
+ *     message.  Nothing is thrown across the ABI.
+ *   - Outputs are deterministic (bitwise repeatable).  The only atomics are the one-launch
+ *     segmented scan's block hand-off flags (agent-scope, in the caller's sync buffer; see
+ *     vm_selective_scan_sync_bytes) — they order work, never accumulate values.
  */
 #ifndef VIDEOMAMBA_HIP_H
 #define VIDEOMAMBA_HIP_H
@@ -48,7 +51,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 7
+#define VM_ABI_VERSION 8
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -136,13 +139,22 @@ long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int 
 
 /* Sync-buffer bytes for the one-launch segmented form (0 when the single pass runs).
  * `sync` (ABI v7, both scan entry points; NULL = the two-launch segmented form) must be
- * zero-filled before its first use; every launch leaves it zero again.  One sync buffer
- * must not serve two launches that can run at the same time (e.g. on two streams).  The
- * one-launch form runs when the buffer is large enough and the segmented grid fits one
- * workgroup per CU (blocks then wait on earlier, resident blocks' published aggregates);
- * results are identical to the two-launch form. */
+ * zero-filled before its first use; every launch leaves its flags zero again.  One sync
+ * buffer must not serve two launches that can run at the same time (e.g. on two streams).
+ * The one-launch form runs when the buffer is large enough and the segmented grid fits one
+ * workgroup per CU of the stream's device (blocks then wait on earlier, resident blocks'
+ * published aggregates); results are identical to the two-launch form.
+ * ABI v8: word 0 of the buffer is a sticky error word.  Each wait is bounded (it never
+ * hangs the GPU); a block whose wait runs out sets word 0 and writes NaN for every output
+ * and last state it owns.  The library never clears word 0: read it with
+ * vm_selective_scan_sync_status on a host copy, and zero it to re-arm. */
 long long vm_selective_scan_sync_bytes(int batch, int dim, int seqlen, int dstate,
                                        int segments);
+
+/* Host-side check of a sync buffer: `sync_host` is a HOST copy of at least the first 16
+ * bytes of the device buffer.  Returns 0 (no hand-off ever timed out), 1 (some launch timed
+ * out: its outputs are NaN), or VM_E_INVALID.  Pure host code (no HIP call). */
+int vm_selective_scan_sync_status(const void* sync_host, long long bytes);
 
 /*
  * One-token scan step on `state` (updated in place, own dtype; fp32 math).

@@ -288,8 +288,9 @@ def test_scan_workspace_query_without_gpu():
     chunked = 2 * (9 * 64 * 17) * 4
     legacy = 2 * 4 * 64 * (2 * 16 + 1) * 4
     assert one == 0 and four == max(chunked, legacy)
-    # the one-launch form's sync flags: (nblk + 1) counters per (row, 64-channel group)
-    assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 2 * 1 * (1 + 1) * 4
+    # the one-launch form's sync buffer: a 16-byte header (the sticky error word), then
+    # (nblk + 1) counters per (row, 64-channel group)
+    assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 16 + 2 * 1 * (1 + 1) * 4
     assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
     assert lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0) > 0
 
@@ -302,7 +303,7 @@ def test_scan_segment_cost_model_choices_without_gpu():
     7 blocks (the round-1 wave-target rule chose 2-3x slower counts there); B >= 72 (1,280+
     waves): single pass, no segments."""
     lib = _lib.load()
-    nblk = lambda B, L: lib.vm_selective_scan_sync_bytes(B, 1152, L, 16, 0) // (B * 18 * 4) - 1  # noqa: E731
+    nblk = lambda B, L: (lib.vm_selective_scan_sync_bytes(B, 1152, L, 16, 0) - 16) // (B * 18 * 4) - 1  # noqa: E731
     assert nblk(1, 3137) == 14 and nblk(1, 12545) == 14
     assert nblk(2, 3137) == nblk(4, 3137) == nblk(8, 3137) == 7
     assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
@@ -326,3 +327,46 @@ def test_options_override_and_validation():
     with pytest.raises(ValueError):
         with options.override(mixer_layout="xx"):
             pass
+
+
+def test_scan_sync_error_word_is_reported_on_the_host():
+    """The one-launch scan's bounded hand-off (vm_scan_seq.hip, PASS 3): a block whose wait
+    runs out sets word 0 of the sync buffer (and writes NaN outputs).  The host-side check
+    reads that word from a host copy — no GPU involved: a clean header is 0, a set word is
+    1, a short buffer is rejected, and check paths raise."""
+    from videomamba_amd import kernels as K
+    lib = _lib.load()
+    nbytes = lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0)
+    buf = torch.zeros(nbytes, dtype=torch.uint8)
+    assert K.scan_sync_status(buf) == 0
+    buf.view(torch.int32)[0] = 1  # what a timed-out block stores
+    assert K.scan_sync_status(buf) == 1
+    buf.view(torch.int32)[0] = 0
+    buf[16:] = 7  # flags / counters do not count as errors
+    assert K.scan_sync_status(buf) == 0
+    assert lib.vm_selective_scan_sync_status(buf.data_ptr(), 8) == -1
+    assert b"sync header" in lib.vm_last_error()
+
+
+@pytest.mark.parametrize("embed_dim,depth", [(192, 24), (384, 24), (576, 32)])
+@pytest.mark.parametrize("frames", [8, 16])
+def test_graph_workspace_covers_first_and_continuation_chunks(embed_dim, depth, frames):
+    """StreamingChunkGraph's scratch must fit both chunk kinds: the first chunk scans
+    L = T*196 + 1 tokens, continuation chunks L - 1, and the segment cost model may choose
+    more segments (more scratch) for L - 1 (Ti-16f at B = 1 needed 11.35 MB for
+    L - 1 against 10.14 MB sized for L).  Ti / S / M at 224 px, B = 1 .. 8."""
+    from videomamba_amd import kernels as K
+    from videomamba_amd.graphs import chunk_workspace_bytes
+    m = PretrainVideoMamba(depth=depth, embed_dim=embed_dim, num_frames=frames)
+    mx = next(iter(m._mixers()))
+    short_wins = 0
+    for B in range(1, 9):
+        need, sync_need = chunk_workspace_bytes(m, B, frames, 14, 14)
+        for L in (frames * 196 + 1, frames * 196):
+            assert need >= K.scan_workspace_bytes(B, mx.d_inner, L, mx.d_state), (B, L)
+            assert sync_need >= K.scan_sync_bytes(B, mx.d_inner, L, mx.d_state), (B, L)
+        L = frames * 196 + 1
+        short_wins += (K.scan_workspace_bytes(B, mx.d_inner, L - 1, mx.d_state)
+                       > K.scan_workspace_bytes(B, mx.d_inner, L, mx.d_state))
+    if (embed_dim, frames) == (192, 16):
+        assert short_wins > 0  # the case the first-chunk-only sizing missed

@@ -447,6 +447,36 @@ def test_refiner_paired_scan_matches_flipped_blocks(shape, dt, segments):
     torch.testing.assert_close(sb, ref_states[3], rtol=tol, atol=tol)  # bwd state in place
 
 
+@pytest.mark.parametrize("shape", [(2, 37, 64), (2, 3, 10, 64)])
+def test_refiner_fallback_d_state_8_matches_oracle(shape):
+    """Configurations outside the paired kernels' preconditions (here d_state = 8: the
+    paired scan takes 16 scalar-loaded states) run the reference's per-block composition
+    (refiner_backbone.py:98-135) instead of raising; fp32 vs the oracle's
+    refiner restatement at 1e-4, carried forward state and the backward state in place."""
+    torch.manual_seed(3)
+    C = shape[-1]
+    blk = video_mamba.BiMambaRefinerBlock(C, ssm_cfg={"d_state": 8}, layer_idx=0).eval()
+    assert blk.block_fwd.mixer.d_state == 8
+    p = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    x = torch.randn(*shape)
+    B = shape[0]
+    (cf, sf), (cb, sb) = blk.allocate_state(B, dtype=torch.float32)
+    for t in (cf, sf, cb, sb):
+        t.copy_(0.3 * torch.randn_like(t))
+    ref_out, (rc, rs) = orc.refiner_forward(p, x, state_fwd=(cf.clone(), sf.clone()),
+                                            state_bwd_init=(cb.clone(), sb.clone()),
+                                            d_state=8)
+    blk = blk.to(DEV)
+    st_f = (cf.to(DEV), sf.to(DEV))
+    with torch.no_grad():
+        out, (nc, ns) = blk(x.to(DEV), state_fwd=st_f, state_bwd_init=(cb.to(DEV), sb.to(DEV)))
+    assert not blk._paired_ok(x.reshape(B, -1, C).to(DEV))
+    assert ns is st_f[1]
+    _close(out, ref_out, 1e-4)
+    _close(nc, rc, 1e-4)
+    _close(ns, rs, 1e-4)
+
+
 def test_refiner_block_runs_and_reverses_time():
     blk = video_mamba.BiMambaRefinerBlock(16, layer_idx=0).cuda().eval()
     x = torch.randn(2, 3, 4, 16, device=DEV)
@@ -488,11 +518,18 @@ def _ti_8f_case():
 
 
 def test_ti_8f_fp32_matches_oracle(layout):
-    """C1/C2 geometry (VideoMamba-Ti, d192, depth 24, 8x224^2) in fp32: HIP vs oracle."""
+    """C1/C2 geometry (VideoMamba-Ti, d192, depth 24, 8x224^2) in fp32: HIP vs oracle.
+    The north star's fp32 tolerance, 1e-4, on the relative L2 norm of x_vis and x_pool;
+    elementwise 1e-3 (fp32 GEMM / scan association orders differ from torch's CPU kernels
+    and the differences compound through 24 residual layers)."""
     model, x, ref_v, ref_p = _ti_8f_case()
     model = model.to(DEV)
     with torch.no_grad():
         xv, xp = model(x.to(DEV))
+    rv, rp = _rel(xv.cpu(), ref_v), _rel(xp.cpu(), ref_p)
+    print(f"Ti-8f fp32 {layout}: rel x_vis {rv:.3e} x_pool {rp:.3e} max abs "
+          f"{(xv.cpu() - ref_v).abs().max().item():.3e}")
+    assert rv < 1e-4 and rp < 1e-4, (rv, rp)
     _close(xv, ref_v, 1e-3)
     _close(xp, ref_p, 1e-3)
 
@@ -689,6 +726,69 @@ def test_c4_m_32f_chunked_equals_full_and_token_major_batch():
         outs[bsz] = full[:1]
         del x, full, c1, c2, st, stitched
     assert _rel(outs[72], outs[1]) < 1e-2, _rel(outs[72], outs[1])
+
+
+def test_c5_full_1024_frames_16_chunks_match_full():
+    """C5 at its stated size (BASELINE.json configs[4]): VideoMamba-M built with
+    num_frames=1024 (temporal embedding sliced, never interpolated: SURVEY F7), 16 x chunk64
+    streamed with a carried fp32 state — temporal offsets 0, 64, ..., 960; L = 12,545 then
+    12,544 per chunk — against ONE 1,024-frame forward (L = 200,705), B = 1, bf16.  North
+    star: < 1e-4 relative on every chunk (reference: videomamba.py:655-675 offset slicing,
+    README.md:99-107, scripts/check_streaming_state.py:55)."""
+    model = _m_model(1024)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.randn(1, 3, 1024, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        full = model(x)
+        assert full.shape[1] == 200705
+        st = model.allocate_state(1, dtype=torch.float32)
+        worst = 0.0
+        for c in range(16):
+            out, st = model(x[:, :, 64 * c:64 * (c + 1)], ssm_state=st,
+                            temporal_pos_offset=64 * c)
+            lo = 0 if c == 0 else 1 + 12544 * c
+            ref = full[:, lo:1 + 12544 * (c + 1)]
+            assert out.shape == ref.shape == (1, 12545 if c == 0 else 12544, 576)
+            r = _rel(out, ref)
+            worst = max(worst, r)
+            assert r < 1e-4, (c, r)
+            assert torch.isfinite(out.float()).all()
+    print(f"C5 16 x chunk64 vs 1024-frame forward: worst chunk rel {worst:.3e}")
+
+
+def test_c3_m_16f_bf16_bench_kernels_match_oracle():
+    """The headline config C3 end to end vs the oracle: VideoMamba-M (d576, depth 32)
+    16x224^2 bf16, one stateful chunk (bf16 zero state, offset 0, pool cls+avg) — the
+    bench's call — with the bench's kernel selection forced: batch 9 > 8 runs the wide
+    conv_proj_kernel and scan_segments=1 the single-pass scan_seq_kernel.  Clip 0 vs
+    orc.encoder_forward on the same weights, clip and state (bf16 at the reference's
+    rounding points, fp32 math).  C2's tolerances: relative L2 <= 1e-2 on x_vis, x_pool and
+    the returned ssm states; every x_vis element within 5e-2 abs + 5e-2 rel."""
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
+    with torch.no_grad():
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    model = model.to(torch.bfloat16).eval()
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(9, 3, 16, 224, 224, generator=g).to(torch.bfloat16)
+    cfg = dict(img_size=224, patch_size=16, depth=32, kernel_size=1, num_frames=16,
+               fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+               pool_type="cls+avg", norm_epsilon=1e-5, d_state=16, d_conv=4)
+    ost = [(torch.zeros(1, 1152, 4, dtype=torch.bfloat16),
+            torch.zeros(1, 1152, 16, dtype=torch.bfloat16)) for _ in range(32)]
+    torch.set_num_threads(16)
+    ref_v, ref_p, ref_st = orc.encoder_forward(p, cfg, x[:1], state=ost, temporal_pos_offset=0)
+    model = model.to(DEV)
+    state = model.allocate_state(9, dtype=torch.bfloat16, device=DEV)
+    with options.override(scan_segments=1), torch.no_grad():
+        xv, xp, st = model(x.to(DEV), ssm_state=state, temporal_pos_offset=0)
+    rv, rp = _rel(xv[:1].cpu(), ref_v), _rel(xp[:1].cpu(), ref_p)
+    rs = max(_rel(st[i][1][:1].cpu(), ref_st[i][1]) for i in range(32))
+    rc = max(_rel(st[i][0][:1].cpu(), ref_st[i][0]) for i in range(32))
+    print(f"C3 M-16f bf16 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e} conv {rc:.3e}")
+    assert rv <= 1e-2 and rp <= 1e-2 and rs <= 1e-2 and rc <= 1e-2, (rv, rp, rs, rc)
+    torch.testing.assert_close(xv[:1].float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
 
 
 def test_c5_long_video_chunk64_streaming_matches_full():

@@ -93,6 +93,28 @@ def test_bench_control_flow_world2_weak_scaling():
     assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
 
 
+def test_bench_control_flow_world2_m32_default_is_weak_336_per_rank():
+    """C4 (--config m32) without --global-batch keeps 336 clips per rank (the batch where
+    the scan holds its occupancy; 84 per GPU at N = 8 from a fixed 672 would have measured
+    the batch choice, not the sharding): weak scaling, global batch = world x 336, and the
+    metric names the workload actually run."""
+    line = _bench_stub(["--config", "m32"])
+    assert line["scaling"] == "weak"
+    assert line["config"]["per_gpu_batch"] == 336 and line["config"]["global_batch"] == 672
+    assert line["metric"].endswith("VideoMamba-M 32f 224")
+    assert _bench_stub(["--config", "ti8"])["metric"].endswith("VideoMamba-Ti 8f 224")
+
+
+def test_bench_metric_name_is_the_baseline_metric_for_c3():
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    want = json.load(open(os.path.join(root, "BASELINE.json")))["metric"]
+    assert bench.metric_name(bench.CONFIGS["m16"]) == want
+
+
 def test_bench_control_flow_world2_global_batch_split():
     """--global-batch (C4): one global batch split by shard_range — 5 clips on 2 ranks is
     3 + 2; scaling is strong and value counts the global batch once."""

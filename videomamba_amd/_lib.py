@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _P = c_void_p
 _LL = c_longlong
@@ -52,6 +52,7 @@ _SIGNATURES = {
          _I, _P, _LL, _P, _LL, _P], _I),
     "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_scan_sync_bytes": ([_I, _I, _I, _I, _I], _LL),
+    "vm_selective_scan_sync_status": ([_P, _LL], _I),
     "vm_selective_state_update": (
         [_P, _I, _LL, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _I,
          _P, _LL, _I, _I, _I, _I, _P], _I),

@@ -52,15 +52,20 @@ __device__ __forceinline__ PairSel pair_sel(const ScanParams& p, int b) {
 
 // Token-major path (vm_scan_seq.hip).  Workspace for the time-segmented form, in bytes;
 // 0 when the single-pass form is chosen.  `segments` receives the chosen segment count.
-// segments: 0 = cost model, > 0 forced.
-size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen);
+// segments: 0 = cost model, > 0 forced.  cus: the CU count the cost model sizes for
+// (0 = the current device's; kCalibCUs = 256 when no device can be queried).
+size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen,
+                           int cus = 0);
 // Launch; `workspace` must hold seq_workspace_bytes() (or be larger).  Returns false when
 // the operands do not fit the token-major kernels (the caller reports the error).
 bool seq_supported(const ScanParams& p, int dtype);
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
                 size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s);
 // Bytes of the zeroed sync buffer the one-launch chunked form needs (0: single pass).
-size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments);
+// Word 0 is the sticky error word (non-zero after a launch whose block handoff timed out;
+// vm_selective_scan_sync_status), words 1..kSyncHeaderWords-1 pad, then flags / counters.
+constexpr int kSyncHeaderWords = 4;
+size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus = 0);
 // Paired scans need the scalar-B/C kernels and, when segmented, the chunked form.
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes);
 

@@ -607,6 +607,18 @@ extern "C" long long vm_selective_scan_sync_bytes(int batch, int dim, int seqlen
   return static_cast<long long>(seq_sync_bytes(batch, dim, seqlen, segments));
 }
 
+// Host-side read of a sync buffer's sticky error word (a host copy of at least its first
+// kSyncHeaderWords words): 0 = every one-launch scan that used the buffer handed its block
+// aggregates on in time, 1 = some block's bounded wait ran out (its outputs are NaN).
+extern "C" int vm_selective_scan_sync_status(const void* sync_host, long long bytes) {
+  if (!sync_host || bytes < static_cast<long long>(kSyncHeaderWords * sizeof(unsigned))) {
+    vmhost::set_error("vm_selective_scan_sync_status: need a host copy of the sync header "
+                      "(%d bytes)", static_cast<int>(kSyncHeaderWords * sizeof(unsigned)));
+    return VM_E_INVALID;
+  }
+  return static_cast<const unsigned*>(sync_host)[0] != 0u ? 1 : 0;
+}
+
 extern "C" int vm_selective_state_update(void* state, int state_dtype, long long s_sb, long long s_sd,
                                          const void* x, long long x_sb, const void* dt, long long dt_sb,
                                          const float* A, const void* B, long long b_sb,

@@ -521,6 +521,7 @@ struct ChunkWork {
   int nblk;     // blocks per sequence
   unsigned* flags;  // one-launch form: [B][groups][nblk] block-published flags (0 between launches)
   unsigned* done;   // one-launch form: [B][groups] count of blocks past their wait
+  unsigned* err;    // one-launch form: sticky error word (word 0 of the sync buffer)
 };
 
 template <bool V> struct BoolTag { static constexpr bool value = V; };
@@ -535,6 +536,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   __shared__ float sH[kChW][kMaxN][64];
   __shared__ float sS[kChW][64];
   __shared__ float sA[kMaxN][64];
+  __shared__ int s_fail;  // one-launch form: this block's wait timed out
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -927,18 +929,34 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       }
     }
     // Blocks are dispatched in order and the host launches this form only when the whole
-    // grid is co-resident, so every block waited on is running or done; the bounded spin
-    // still ends (with wrong output, never a hung GPU) if that assumption were broken.
-    // The spin reads are relaxed (coherent loads, no cache invalidation: an acquiring read
-    // per iteration invalidated the L2 under every other block of the XCD, 45 -> 134 us at
-    // B = 1); one acquire fence follows the wait.
+    // grid is co-resident, so every block waited on is running or done.  The spin is
+    // bounded anyway so a broken assumption can never hang the GPU: a block whose wait runs
+    // out sets the sticky error word (word 0 of the sync buffer, read on the host with
+    // vm_selective_scan_sync_status) and poisons its entry state with NaN, so every output
+    // and h_last it writes is NaN — never a plausible wrong value.
+    //
+    // Memory ordering (no fences; gfx942 / gfx950 memory model, LLVM AMDGPUUsage "Memory
+    // Model GFX942"): every cross-workgroup value — aggregates, flags, the done counter —
+    // is written and read ONLY with agent-scope atomics, which the backend emits as
+    // sc1 global stores / loads that go to the agent's coherence point instead of a
+    // (per-XCD, non-coherent) L2 line, so no L2 write-back or invalidate is needed for them
+    // to be seen.  Ordering: the publisher's s_waitcnt vmcnt(0) completes (acknowledges) its
+    // aggregate stores before s_barrier lets thread 0 store the flag; the reader issues its
+    // aggregate loads only after thread 0's flag load has returned 1 (control dependency)
+    // and the following s_barrier.  An agent-scope release / acquire fence pair would add a
+    // buffer_wbl2 / buffer_inv per workgroup for data that never sits in L2: measured
+    // 45 -> 134 us at B = 1 with them.
     if (tid == 0) {
+      bool timed_out = false;
       for (int j = 0; j < blk; ++j) {
         unsigned spins = 0;
         while (__hip_atomic_load(&fl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
                ++spins < (1u << 22))
           __builtin_amdgcn_s_sleep(2);
+        if (spins >= (1u << 22)) timed_out = true;
       }
+      s_fail = timed_out ? 1 : 0;
+      if (timed_out) __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the last block past its wait resets the flags for the next launch
       if (__hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
           static_cast<unsigned>(w.nblk - 1)) {
@@ -951,6 +969,10 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
     H0 *= kLog2e;  // log2 units
     H1 *= kLog2e;
+    if (s_fail) {  // a timed-out wait: make every output of this block NaN
+      H0 = __builtin_nanf("");
+      H1 = __builtin_nanf("");
+    }
     const int ci = tid >> 3;
     for (int r0 = 0; r0 < blk; r0 += kChW) {
       if (r0 > 0) __syncthreads();  // every wave is done reading the previous group
@@ -1101,6 +1123,28 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
   }
 }
 
+// CU count of the device that owns `stream` (the current device for the null stream);
+// 0 when it cannot be queried (no device: the size queries then assume kCalibCUs).
+static int device_cus(hipStream_t stream) {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (stream) {
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return 0;
+  }
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+static constexpr int kCalibCUs = 256;  // the part the cost model below was swept on
+static int cus_or_calib(int cus) { return cus > 0 ? cus : kCalibCUs; }
+
 // Segment count.  A chip-filling batch (>= 1,280 waves of 64-channel groups) runs
 // single-pass.  Below that the chunked form's time is modelled from a sweep of forced
 // segment counts at M-16f geometry (scripts/diag/scan_segments_sweep.py, B = 1 .. 64,
@@ -1111,11 +1155,12 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
 // steps k-fold interleaved (the passes are issue-bound), and every block adds one aggregate
 // to the entry walk.  The model is within ~6 % of the sweep; the round-1 rule (a fixed
 // ~1,792-wave target) picked 2-3x slower counts at B >= 4 (T = 126 .. 1,569 steps).
-// Depends on (batch, dim, seqlen) only.
-static int choose_segments(int batch, int dim, int seqlen) {
+// Depends on (batch, dim, seqlen) and the device's CU count only (the sweep ran on a
+// 256-CU MI355X; `cus` rescales k and the chip-filling threshold for other parts).
+static int choose_segments(int batch, int dim, int seqlen, int cus) {
   if (seqlen < 64) return 1;
   const long long groups = (dim + 63) / 64;
-  if (batch * groups >= 1280) return 1;
+  if (batch * groups >= 5 * cus) return 1;
   const int max_s = (seqlen + 7) / 8;  // segments of at least 8 steps
   int best = 1;
   double best_cost = 1e30;
@@ -1123,7 +1168,7 @@ static int choose_segments(int batch, int dim, int seqlen) {
     const int T = (seqlen + S - 1) / S;
     const int segs = (seqlen + T - 1) / T;
     const long long nblk = (segs + kChW - 1) / kChW;
-    const long long k = (batch * groups * nblk + 255) / 256;
+    const long long k = (batch * groups * nblk + cus - 1) / cus;
     const double cost = 0.69 * static_cast<double>(k * T) + 0.43 * static_cast<double>(nblk);
     if (cost < best_cost) {
       best_cost = cost;
@@ -1135,8 +1180,10 @@ static int choose_segments(int batch, int dim, int seqlen) {
 
 // segments > 0 (an explicit ABI argument: tests and sweeps) forces the segment count;
 // 0 lets the cost model choose.
-static int segments_for(int batch, int dim, int seqlen, int segments) {
-  int S = segments > 0 ? segments : choose_segments(batch, dim, seqlen);
+// `cus` = the launch device's CU count (0: the current device's, or kCalibCUs).
+static int segments_for(int batch, int dim, int seqlen, int segments, int cus = 0) {
+  if (cus <= 0) cus = cus_or_calib(device_cus(nullptr));
+  int S = segments > 0 ? segments : choose_segments(batch, dim, seqlen, cus);
   if (S > seqlen) S = seqlen > 0 ? seqlen : 1;
   return S < 1 ? 1 : S;
 }
@@ -1160,8 +1207,9 @@ static size_t legacy_bytes(int batch, int dim, int S) {
   return static_cast<size_t>(batch) * S * dim * (2 * kMaxN + 1) * sizeof(float);
 }
 
-size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen) {
-  const int S = segments_for(batch, dim, seqlen, segments);
+size_t seq_workspace_bytes(int batch, int dim, int seqlen, int segments, int* chosen,
+                           int cus) {
+  const int S = segments_for(batch, dim, seqlen, segments, cus);
   if (chosen) *chosen = S;
   if (S <= 1) return 0;
   const size_t a = chunk_bytes(batch, dim, seqlen, S), b = legacy_bytes(batch, dim, S);
@@ -1214,28 +1262,18 @@ static void launch_chunk(const ScanParams& p, const ChunkWork& w, hipStream_t s)
 #undef VM_CH
 }
 
-// One-launch chunked form: sync flags per (row, channel group, block) plus a counter per
-// (row, channel group).  Used when the caller passes a zeroed sync buffer this large and
-// the whole grid fits one workgroup per CU (so every block it waits on is resident).
-size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments) {
-  const int S = segments_for(batch, dim, seqlen, segments);
+// One-launch chunked form: the sticky error word (word 0; words 1-3 pad to 16 bytes), then
+// sync flags per (row, channel group, block) plus a counter per (row, channel group).  Used
+// when the caller passes a zeroed sync buffer this large and the whole grid fits one
+// workgroup per CU (so every block it waits on is resident).
+size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus) {
+  const int S = segments_for(batch, dim, seqlen, segments, cus);
   if (S <= 1) return 0;
   int T, nblk;
   chunk_geometry(seqlen, S, &T, &nblk);
   const size_t groups = (dim + 63) / 64;
-  return static_cast<size_t>(batch) * groups * (nblk + 1) * sizeof(unsigned);
-}
-
-static int device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      cached[dev] = n;
-  }
-  return cached[dev];
+  return kSyncHeaderWords * sizeof(unsigned) +
+         static_cast<size_t>(batch) * groups * (nblk + 1) * sizeof(unsigned);
 }
 
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes) {
@@ -1246,16 +1284,20 @@ bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t wor
 
 void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
                 size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s) {
+  // the stream's device decides the segment count and whether the grid is co-resident
+  const int dev_cus = device_cus(s);
+  const int cus = cus_or_calib(dev_cus);
   int S = 1;
-  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
+  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S, cus);
   const int es = dtype == VM_DTYPE_BF16 ? 2 : 4;
   if (S > 1 && workspace && workspace_bytes >= need && seq_sgpr_bc(p, es)) {
     ChunkWork w{};
     chunk_geometry(p.seqlen, S, &w.T, &w.nblk);
     const long long grid = static_cast<long long>((p.dim + 63) / 64) * w.nblk * p.batch;
-    if (sync && sync_bytes >= seq_sync_bytes(p.batch, p.dim, p.seqlen, segments) &&
-        grid <= device_cus()) {
-      w.flags = static_cast<unsigned*>(sync);
+    if (sync && sync_bytes >= seq_sync_bytes(p.batch, p.dim, p.seqlen, segments, cus) &&
+        grid <= dev_cus) {
+      w.err = static_cast<unsigned*>(sync);
+      w.flags = w.err + kSyncHeaderWords;
       w.done = w.flags + static_cast<size_t>(p.batch) * ((p.dim + 63) / 64) * w.nblk;
     }
     const size_t nb = static_cast<size_t>(p.batch) * w.nblk;

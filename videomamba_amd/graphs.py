@@ -40,7 +40,29 @@ from torch import Tensor
 
 from . import kernels as K
 
-__all__ = ["StreamingChunkGraph"]
+__all__ = ["StreamingChunkGraph", "chunk_workspace_bytes"]
+
+
+def chunk_workspace_bytes(model, batch: int, tt: int, gh: int, gw: int) -> Tuple[int, int]:
+    """(scratch bytes, sync bytes) one streaming chunk of ``tt`` temporal tokens on a
+    ``gh`` x ``gw`` grid needs, over BOTH chunk kinds: the first chunk scans
+    L = tt*gh*gw + 1 tokens (CLS row), continuation chunks L - 1, and the scan's cost model
+    may pick a larger segment count (more scratch) for the shorter one.  The max over the
+    scan, the conv_proj forms and the pooling sums of every mixer."""
+    C = model.embed_dim
+    need, sync_need = 0, 0
+    for L in (tt * gh * gw + 1, tt * gh * gw):
+        Lp = (L + 7) // 8 * 8
+        need = max(need, K.norm_pool_workspace_bytes(batch, 1, L, C),
+                   K.norm_pool_workspace_bytes(batch, tt, gh * gw, C))
+        for mx in model._mixers():
+            E = mx.dt_rank + 2 * mx.d_state
+            need = max(need, K.scan_workspace_bytes(batch, mx.d_inner, L, mx.d_state))
+            if mx.d_inner % 64 == 0:
+                need = max(need, K.conv_proj_cm_workspace_bytes(batch, Lp, mx.d_inner, E),
+                           K.conv_proj_workspace_bytes(batch, Lp, mx.d_inner, E))
+            sync_need = max(sync_need, K.scan_sync_bytes(batch, mx.d_inner, L, mx.d_state))
+    return need, sync_need
 
 
 class StreamingChunkGraph:
@@ -123,30 +145,26 @@ class StreamingChunkGraph:
         self._tpos_offset = None
 
     def _workspace(self) -> Tensor:
-        """Kernel scratch (segmented scan, channel-major conv_proj partials) sized for the
-        largest consumer of a chunk; allocated once per capture set, owned by this runner."""
+        """Kernel scratch (segmented scan, conv_proj partials, pooling sums) sized for the
+        largest consumer of either chunk kind; allocated once per capture set, owned by this
+        runner (with the one-launch scan's sync flags)."""
         m = self.model
         gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
-        L = self.tt * gh * gw + 1
-        Lp = (L + 7) // 8 * 8
-        need = max(max(K.scan_workspace_bytes(self.batch, mx.d_inner, L, mx.d_state),
-                       K.norm_pool_workspace_bytes(self.batch, 1, L, m.embed_dim),
-                       K.norm_pool_workspace_bytes(self.batch, self.tt, gh * gw, m.embed_dim),
-                       K.conv_proj_cm_workspace_bytes(self.batch, Lp, mx.d_inner,
-                                                      mx.dt_rank + 2 * mx.d_state)
-                       if mx.d_inner % 64 == 0 else 0,
-                       K.conv_proj_workspace_bytes(self.batch, Lp, mx.d_inner,
-                                                   mx.dt_rank + 2 * mx.d_state)
-                       if mx.d_inner % 64 == 0 else 0)
-                   for mx in m._mixers())
+        need, sync_need = chunk_workspace_bytes(m, self.batch, self.tt, gh, gw)
         if self._ws is None or self._ws.numel() < max(need, 1):
             self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
         # the one-launch scan's sync flags: zeroed once, left zeroed by every replay
-        sync_need = max(K.scan_sync_bytes(self.batch, mx.d_inner, L, mx.d_state)
-                        for mx in m._mixers())
         if self._sync is None or self._sync.numel() < max(sync_need, 1):
             self._sync = torch.zeros(max(sync_need, 4096), dtype=torch.uint8, device=self.device)
         return self._ws
+
+    def check(self) -> None:
+        """Raise if a replayed one-launch scan ever timed out on a block hand-off (its
+        outputs were NaN); synchronises with the queued replays.  See K.check_scan_sync."""
+        if self._sync is not None and K.scan_sync_status(self._sync):
+            self._sync[:K.SYNC_HEADER_BYTES].zero_()
+            raise RuntimeError("StreamingChunkGraph: a replayed one-launch scan timed out on a "
+                               "block hand-off; the affected outputs were NaN")
 
     def _capture(self, has_cls: bool):
         saved = [(c.clone(), s.clone()) for c, s in self._state]

@@ -19,6 +19,7 @@ its padded channel-major layouts.
 
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -142,6 +143,7 @@ def scratch(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
 
 _SYNC = {}
 _SYNC_OVERRIDE = [None]
+_SYNC_SEEN = weakref.WeakValueDictionary()  # id -> caller-owned sync buffer (sync_override)
 
 
 class sync_override:
@@ -155,6 +157,7 @@ class sync_override:
     def __enter__(self):
         self.prev = _SYNC_OVERRIDE[0]
         _SYNC_OVERRIDE[0] = self.buf
+        _SYNC_SEEN[id(self.buf)] = self.buf
         return self.buf
 
     def __exit__(self, *exc):
@@ -177,6 +180,39 @@ def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tens
         buf = torch.zeros(max(nbytes, 4096), dtype=torch.uint8, device=device)
         _SYNC[key] = buf
     return buf
+
+
+SYNC_HEADER_BYTES = 16  # the sync buffer's sticky error word + padding (ABI v8)
+
+
+def scan_sync_status(buf: Tensor) -> int:
+    """0 when no one-launch scan that used ``buf`` (a sync buffer, device or host copy)
+    timed out waiting for an earlier block, 1 when one did (its outputs are NaN).  Reads
+    the header through ``vm_selective_scan_sync_status``; a device buffer is copied to the
+    host first (this synchronises with the work queued on it)."""
+    head = buf.detach().reshape(-1)[:SYNC_HEADER_BYTES].to(torch.uint8)
+    head = head.cpu().contiguous() if head.is_cuda else head.contiguous()
+    rc = int(_lib.load().vm_selective_scan_sync_status(head.data_ptr(), head.numel()))
+    if rc < 0:
+        _lib.check(rc, "vm_selective_scan_sync_status")
+    return rc
+
+
+def check_scan_sync(clear: bool = True) -> None:
+    """Raise RuntimeError if any sync buffer this process has used (the per-stream ones and
+    those passed through :class:`sync_override`, e.g. a captured graph's) recorded a
+    timed-out block hand-off.  ``clear`` re-arms the buffers' error words first.  The
+    kernels never hang and never write plausible wrong values on a timeout (the affected
+    outputs are NaN); this turns the event into an exception."""
+    bad = 0
+    for buf in list(_SYNC.values()) + list(_SYNC_SEEN.values()):
+        if scan_sync_status(buf):
+            bad += 1
+            if clear:
+                buf.reshape(-1)[:SYNC_HEADER_BYTES].zero_()
+    if bad:
+        raise RuntimeError(f"one-launch selective scan: {bad} sync buffer(s) recorded a "
+                           "timed-out block hand-off; the affected outputs are NaN")
 
 
 def scan_sync_bytes(batch: int, dim: int, seqlen: int, dstate: int,

@@ -17,6 +17,11 @@ forward, [B, 2B) backward) with no flipped copies of the sequence:
 
 The reference's flipped copies of the input and of the backward output
 (``refiner_backbone.py:121``, ``:128``) are folded into the norm's load and the scan's store.
+
+Configurations the paired kernels do not take (d_state != 16, forward / backward mixers of
+different geometry, widths the fused norm rejects, odd bf16 x_dbl rows, unaligned input)
+run the reference's composition instead — the forward block, the backward block on a
+flipped copy, the flip back and the gate — on the same per-block HIP kernels.
 """
 
 from __future__ import annotations
@@ -85,18 +90,47 @@ class BiMambaRefinerBlock(nn.Module):
         st_b = self._ensure_state(self.block_bwd, state_bwd_init, bsz, seq.device)
         frame = 1 if packed is None else packed[2]
         with torch.no_grad():
-            out, new_f = self._forward_paired(seq, frame, st_f, st_b)
+            if self._paired_ok(seq):
+                out, new_f = self._forward_paired(seq, frame, st_f, st_b)
+            else:
+                out, new_f = self._forward_blocks(seq, packed, st_f, st_b)
         return self._unpack_tokens(out, packed), new_f
+
+    def _paired_ok(self, seq: Tensor) -> bool:
+        """The one-launch paired pipeline's preconditions (else :meth:`_forward_blocks`):
+        equal mixer geometry, 16 states (the paired scan's scalar B/C rows), a width the
+        fused norm takes (C % 4 == 0, C <= 2048) with a 16-byte aligned input, and B|C rows
+        of x_dbl on 4-byte boundaries."""
+        mf, mb = self.block_fwd.mixer, self.block_bwd.mixer
+        if any(getattr(mf, a) != getattr(mb, a) for a in ("d_inner", "d_state", "dt_rank", "d_conv")):
+            return False
+        C = seq.shape[-1]
+        es = seq.element_size() if self.block_fwd.fused_add_norm else \
+            self.block_fwd.norm.weight.element_size()
+        return (mf.d_state == 16 and C % 4 == 0 and 4 <= C <= 2048
+                and ((mf.dt_rank + 2 * mf.d_state) * es) % 4 == 0
+                and (not seq.is_contiguous() or seq.data_ptr() % 16 == 0))
+
+    def _forward_blocks(self, seq: Tensor, packed, st_f: LayerState, st_b: LayerState):
+        """The reference's composition (``refiner_backbone.py:98-135``) on the per-block
+        HIP path: forward block, backward block over the time-flipped sequence (frame order
+        flipped for 4-D input, ``:61-68``), flip back, sigmoid gate, Linear."""
+        def flip(t: Tensor) -> Tensor:
+            if packed is None:
+                return torch.flip(t, dims=[1])
+            b, tt, n = packed
+            return torch.flip(t.reshape(b, tt, n, t.shape[-1]), dims=[1]).reshape(b, tt * n, -1)
+
+        out_f, _, new_f = self.block_fwd(seq, state=st_f, return_state=True)
+        out_b_rev, _, _ = self.block_bwd(flip(seq), state=st_b, return_state=True)
+        out_b = flip(out_b_rev)
+        gate = self.fusion_gate(torch.cat([out_f, out_b], dim=-1))
+        return self.out_proj(gate * out_f + (1.0 - gate) * out_b), new_f
 
     def _forward_paired(self, seq: Tensor, frame: int, st_f: LayerState, st_b: LayerState):
         bf, bb = self.block_fwd, self.block_bwd
         mf, mb = bf.mixer, bb.mixer
         B, L, C = seq.shape
-        for a in ("d_inner", "d_state", "dt_rank", "d_conv"):
-            if getattr(mf, a) != getattr(mb, a):
-                raise ValueError(f"forward / backward mixers differ in {a}")
-        if mf.d_state != 16:
-            raise NotImplementedError("the paired bidirectional scan takes d_state == 16")
         Dm, N, R, W = mf.d_inner, mf.d_state, mf.dt_rank, mf.d_conv
         for blk, (cs, ss) in ((bf, st_f), (bb, st_b)):
             blk.mixer._check_state(cs, W, "conv_state", B)
