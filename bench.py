@@ -79,6 +79,8 @@ def _args():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle threads (0: the CPUs this process may run on, at most 16 — "
                          "a one-GPU box's share)")
+    ap.add_argument("--scan-dt-proj", default="auto", choices=("auto", "on", "off"),
+                    help="options.scan_dt_proj: dt_proj inside the scan at chip-filling batches")
     ap.add_argument("--full-sequence", action="store_true",
                     help="stateless full-sequence forward (C2) instead of a stateful chunk")
     a = ap.parse_args()
@@ -110,12 +112,17 @@ def _pmc_traffic(shape, kernel):
     return None, None
 
 
-def scan_roofline(batch, reps, device, layout="tm"):
+def scan_roofline(batch, reps, device, layout="tm", dtp=False):
     """Time the scan kernel at the bench shape (layer-0 geometry, padded layout) with HIP
     events on the launch stream; algorithmic bytes per launch per SURVEY.md 8(d).  The
     scan activates delta itself (the model's call: delta_bias, delta_softplus=True).
     layout "tm": the model's token-major buffers (u, dt: (B*Lp, D); z inside xz (B*Lp, 2D);
-    B/C inside x_dbl (B*Lp, R+2N)); "cm": channel-major (D, B*Lp) buffers."""
+    B/C inside x_dbl (B*Lp, R+2N)); "cm": channel-major (D, B*Lp) buffers.
+    dtp: the kernel the bf16 mixer runs at this batch with dt_proj folded in
+    (vm_selective_scan_dtproj_fwd: dt from the x_dbl rows, no dt rows).  ``frac`` stays on
+    the SURVEY 8(d) byte formula (which counts a delta stream); ``own_bytes_per_launch`` /
+    ``frac_own_bytes`` price what the fused kernel itself must move (u, z, y, B|C rows,
+    dt_low rows, states)."""
     from videomamba_amd import kernels as K
     from videomamba_amd.layers import round_up
 
@@ -151,6 +158,17 @@ def scan_roofline(batch, reps, device, layout="tm"):
                    h, (h.stride(0), h.stride(1)), h, (h.stride(0), h.stride(1)), y, s_u, Lp,
                    batch, D, L, N, 1, stream)
 
+    if dtp:
+        xdbl[:, :R] = (0.5 * torch.randn(n, R, device=device, generator=g)).to(bf)
+        wdt = torch.zeros(D, 64, device=device, dtype=bf)
+        wdt[:, :R] = (torch.randn(D, R, device=device, generator=g) / R ** 0.5).to(bf)
+        E = R + 2 * N
+
+        def launch():  # noqa: F811
+            K.scan_dtproj_raw(u, s_u, xdbl, (Lp * E, E), R, wdt, A, Bm, s_bc, Cm, s_bc, Dv, z,
+                              s_z, bias, h, (h.stride(0), h.stride(1)), h,
+                              (h.stride(0), h.stride(1)), y, s_u, Lp, batch, D, L, N, stream)
+
     for _ in range(5):
         launch()
     torch.cuda.synchronize()
@@ -165,8 +183,11 @@ def scan_roofline(batch, reps, device, layout="tm"):
     algo = batch * D * L * 4 * e + 2 * batch * N * L * e + 4 * D * N + 8 * D + 2 * batch * D * N * e
     achieved = algo / avg_s / 1e9
     floor_s = batch * D * L * N / 64 * (CYC_EXP + 4 * CYC_FMA) / SIMDS / CLOCK_HZ
+    own = (batch * D * L * 3 * e + 2 * batch * N * L * e + batch * L * R * e + 4 * D * N
+           + 8 * D + 2 * batch * D * N * e + D * R * e) if dtp else algo
     shape = f"B={batch} D={D} L={L} N={N} bf16, stateful"
-    kname = "vm::scan_seq_kernel" if layout == "tm" else "vm::scan_v5_kernel"
+    kname = ("vm::scan_seq_dtp_kernel" if dtp else "vm::scan_seq_kernel") if layout == "tm" \
+        else "vm::scan_v5_kernel"
     traffic, tsrc = _pmc_traffic(shape, kname)
     return {"bound": "hbm", "kernel": kname, "layout": layout, "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -175,6 +196,8 @@ def scan_roofline(batch, reps, device, layout="tm"):
                                "measured in this run" if tsrc else None),
             "avg_us": round(avg_s * 1e6, 2),
             "bytes_per_launch": algo, "shape": shape,
+            "own_bytes_per_launch": own,
+            "frac_own_bytes": round(own / avg_s / 1e9 / HBM_PEAK_GBS, 4),
             "valu_model": {"floor_us": round(floor_s * 1e6, 2),
                            "frac_of_valu_floor": round(floor_s / avg_s, 4),
                            "no_memory_us": round(LAB_NO_MEMORY_US_PER_CLIP_LAYER * batch, 1),
@@ -447,8 +470,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
+    from videomamba_amd import options
     from videomamba_amd.videomamba import PretrainVideoMamba
 
+    options.get().scan_dt_proj = args.scan_dt_proj
     cfg = CONFIGS[args.config]
     torch.manual_seed(0)
     model = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],
@@ -499,8 +524,11 @@ def main():
         p50_eager = chunk_lat(lambda: model(x1, ssm_state=st1, temporal_pos_offset=0))
         p50_graph = chunk_lat(lambda: runner.run(x1, temporal_pos_offset=0))
         from videomamba_amd.mamba_simple import mixer_layout
+        mx0 = model.layers[0].mixer
+        hn0 = torch.empty((max(B, 1), 8, cfg["embed_dim"]), device=device, dtype=torch.bfloat16)
         roof = scan_roofline(max(B, 1), args.scan_reps, device,
-                             mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device))
+                             mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device),
+                             dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))
         b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 else None
 
     if rank == 0:

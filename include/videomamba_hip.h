@@ -9,6 +9,8 @@
  *                                 (models/videomamba/mamba_simple.py:122-152, stateless and
  *                                  initial_state forms; also replaces the per-token
  *                                  selective_state_update loop at :153-172)
+ *   vm_selective_scan_dtproj_fwd <- dt_proj (mamba_simple.py:409-413) + selective_scan_fn,
+ *                                 dt computed inside the scan on the matrix cores
  *   vm_selective_scan_bidir_fwd <- the forward + flipped backward scans of
  *                                 BiMambaRefinerBlock (models/refiner_backbone.py:98-135)
  *   vm_selective_state_update  <- mamba_ssm selective_state_update  (mamba_simple.py:483-494)
@@ -131,6 +133,33 @@ int vm_selective_scan_bidir_fwd(
     const void* h0_bwd, void* h_last_bwd, int frame_len,
     int segments, void* workspace, long long workspace_bytes, void* sync,
     long long sync_bytes, vm_stream_t stream);
+
+/*
+ * dt_proj folded into the scan (ABI v8): the mixer's  dt = dt_proj.weight @ x_dbl[:, :R]^T
+ * (models/videomamba/mamba_simple.py:409-413, rounded to bf16 there) followed by
+ * selective_scan_fn(u, dt, A, B, C, D, z, delta_bias, delta_softplus=True)
+ * (:423-435), with dt never written to memory: each 16-step block's dt is computed on the
+ * matrix cores from the x_dbl rows the scan already reads for B|C.
+ *   dt_low: rows of the x_dbl buffer (batch stride dtl_sb, row stride dtl_sl elements;
+ *           dt_low = the first dt_rank columns), 8-byte aligned rows;
+ *   w_dt:   (dim, w_dt_ld) bf16 with columns >= dt_rank zero, w_dt_ld >= 16*ceil(r/16);
+ * everything else as vm_selective_scan_fwd.  Single pass only (no segments, no
+ * workspace): bf16, token-major, 16 states with C directly after B in the x_dbl row (the
+ * mixer's layout), z present, delta_softplus = 1, dim % 128 == 0, dt_rank <= 64.  Each
+ * token's dt is computed from its own row in a fixed order (sequence-length independent).
+ */
+int vm_selective_scan_dtproj_fwd(
+    const void* u, long long u_sb, long long u_sd, long long u_sl,
+    const void* dt_low, long long dtl_sb, long long dtl_sl, int dt_rank,
+    const void* w_dt, int w_dt_ld, const float* A,
+    const void* B, long long b_sb, long long b_sn, long long b_sl,
+    const void* C, long long c_sb, long long c_sn, long long c_sl,
+    const float* D, const void* z, long long z_sb, long long z_sd, long long z_sl,
+    const float* delta_bias, int delta_softplus,
+    const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
+    void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
+    void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
+    int batch, int dim, int seqlen, int dstate, int dtype, vm_stream_t stream);
 
 /* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape and
  * segment request (0 = the cost model's choice). */

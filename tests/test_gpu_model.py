@@ -815,13 +815,14 @@ def test_c5_long_video_chunk64_streaming_matches_full():
     assert torch.isfinite(full.float()).all()
 
 
-@pytest.mark.parametrize("segments", [1, 0])
-def test_m_mixer_token_major_bench_kernels_match_oracle(segments):
+@pytest.mark.parametrize("segments,dtp", [(1, "off"), (0, "off"), (1, "on")])
+def test_m_mixer_token_major_bench_kernels_match_oracle(segments, dtp):
     """The bench's exact mixer kernels at VideoMamba-M width (d_model 576: D = 1152,
     R = 36, N = 16, bf16): token-major layout, fused conv + x_proj + dt_proj, and the
     channel-per-lane scan reading z inside xz and B|C inside x_dbl with one scalar load
-    (scan_seq_kernel<bf16, ..., BC1>); segments=1 is the single-pass form the B=336 bench
-    runs, 0 the cost model's choice at this batch.  vs the oracle's bf16 mixer (same
+    (scan_seq_kernel<bf16, ..., BC1>); segments=1 is the single-pass form, 0 the cost
+    model's choice at this batch; dtp="on" the B=336 bench's form: conv_proj without dt
+    rows and dt_proj inside the single-pass scan (scan_seq_dtp_kernel).  vs the oracle's bf16 mixer (same
     rounding points), full sequence and two stateful chunks.  Tolerance 5e-2 abs+rel per
     element, 1e-2 relative norm."""
     torch.manual_seed(11)
@@ -838,7 +839,9 @@ def test_m_mixer_token_major_bench_kernels_match_oracle(segments):
     r2, _ = orc.mamba_mixer(p, "", x[:, 601:], d_state=16, d_conv=4, state=(rc1, rs1),
                             return_state=True)
     xd = x.to(DEV)
-    with options.override(mixer_layout="tm", scan_segments=segments), torch.no_grad():
+    with options.override(mixer_layout="tm", scan_segments=segments, scan_dt_proj=dtp), \
+            torch.no_grad():
+        assert m._dtp_ok(xd, 1000) == (dtp == "on")
         full = m(xd)
         st = m.allocate_state(2, dtype=torch.float32)
         o1, st = m(xd[:, :601], state=st, return_state=True)

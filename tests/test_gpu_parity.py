@@ -253,6 +253,99 @@ def _mixer_layout_scan(Bz, D, L, dt):
     _close(h, ref_h, 1e-4)
 
 
+def _dtproj_case(Bz, D, L, R, seed, exact):
+    """Mixer-layout operands for vm_selective_scan_dtproj_fwd: x_dbl rows [dt_low | B | C],
+    z inside xz, padded (Lp) rows zero, a zero-padded (D, 32|64) W_dt.  ``exact``: dt_low
+    small integers and W_dt multiples of 1/64, so every dt sum is exact in fp32 whatever
+    the accumulation order, and dt_ref = bf16(dt_low @ W_dt^T) is the kernel's own dt."""
+    N = 16
+    E = R + 2 * N
+    Lp = (L + 7) // 8 * 8
+    g = torch.Generator().manual_seed(seed)
+    bf = torch.bfloat16
+    if exact:
+        dtl = torch.randint(-2, 3, (Bz, L, R), generator=g).float()
+        wdt = torch.randint(-4, 5, (D, R), generator=g).float() / 64
+    else:
+        dtl = torch.randn(Bz, L, R, generator=g)
+        wdt = torch.randn(D, R, generator=g) / R ** 0.5
+    dtl, wdt = dtl.to(bf), wdt.to(bf)
+    dt_ref = (dtl.double() @ wdt.double().t()).float().to(bf)  # (Bz, L, D)
+    u = torch.randn(Bz, L, D, generator=g).to(bf)
+    z = torch.randn(Bz, L, D, generator=g).to(bf)
+    Bm = torch.randn(Bz, L, N, generator=g).to(bf)
+    Cm = torch.randn(Bz, L, N, generator=g).to(bf)
+    A = -torch.exp(torch.log(torch.arange(1, N + 1).float()).repeat(D, 1)
+                   + 0.1 * torch.randn(D, N, generator=g))
+    Dv = torch.randn(D, generator=g)
+    bias = 0.5 * torch.randn(D, generator=g) - 2.0
+    h0 = torch.randn(Bz, D, N, generator=g)
+    XD = torch.zeros(Bz, Lp, E, dtype=bf)
+    XD[:, :L, :R], XD[:, :L, R:R + N], XD[:, :L, R + N:] = dtl, Bm, Cm
+    U = torch.zeros(Bz, Lp, D, dtype=bf)
+    XZ = torch.zeros(Bz, Lp, 2 * D, dtype=bf)
+    DT = torch.zeros(Bz, Lp, D, dtype=bf)
+    U[:, :L], XZ[:, :L, D:], DT[:, :L] = u, z, dt_ref
+    wpad = torch.zeros(D, 32 if R <= 32 else 64, dtype=bf)
+    wpad[:, :R] = wdt
+    dev = lambda t: t.reshape(Bz * Lp, -1).to(DEV) if t.dim() == 3 else t.to(DEV)  # noqa: E731
+    return dict(N=N, E=E, Lp=Lp, U=dev(U), XZ=dev(XZ), XD=dev(XD), DT=dev(DT),
+                wpad=wpad.to(DEV), A=A.to(DEV).contiguous(), Dv=Dv.to(DEV),
+                bias=bias.to(DEV), h0=h0, cpu=(u, dt_ref, z, Bm, Cm, A, Dv, bias))
+
+
+def _run_dtproj(c, Bz, D, L, R, dtp):
+    N, E, Lp = c["N"], c["E"], c["Lp"]
+    s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * E, 1, E)
+    XD, XZ = c["XD"], c["XZ"]
+    y = torch.full((Bz * Lp, D), 7.0, dtype=torch.bfloat16, device=DEV)
+    h = c["h0"].to(DEV).contiguous()
+    hs = (D * N, N)
+    stream = torch.cuda.current_stream().cuda_stream
+    if dtp:
+        K.scan_dtproj_raw(c["U"], s_u, XD, (Lp * E, E), R, c["wpad"], c["A"], XD[:, R:R + N],
+                          s_bc, XD[:, R + N:], s_bc, c["Dv"], XZ[:, D:], s_z, c["bias"], h, hs,
+                          h, hs, y, s_u, Lp, Bz, D, L, N, stream)
+    else:
+        with options.override(scan_segments=1):
+            K.scan_raw(c["U"], s_u, c["DT"], s_u, c["A"], XD[:, R:R + N], s_bc, XD[:, R + N:],
+                       s_bc, c["Dv"], XZ[:, D:], s_z, c["bias"], True, h, hs, h, hs, y, s_u, Lp,
+                       Bz, D, L, N, K.dtype_code(torch.bfloat16), stream)
+    return y.view(Bz, Lp, D), h
+
+
+@pytest.mark.parametrize("Bz,D,L,R", [(2, 256, 301, 36), (3, 128, 20, 12), (1, 384, 1000, 24),
+                                      (2, 1152, 3137, 36), (2, 128, 1, 36), (1, 128, 40, 64)])
+def test_scan_dtproj_bitwise_equals_dt_rows_then_scan(Bz, D, L, R):
+    """vm_selective_scan_dtproj_fwd (dt_proj on the matrix cores inside the scan) on dt sums
+    that are exact in fp32 in any order: bit-identical to the single-pass scan reading
+    precomputed dt rows bf16(dt_low @ W_dt^T) — the same per-step arithmetic — including
+    the 16-step blocks' main loop (L >= 24), the clamped tail (L = 1, 20, ragged ends),
+    in-place fp32 state, zeroed padded rows, and every K-chunk count (R = 12 / 24 / 36 /
+    64 -> 1 / 2 / 3 / 4 chunks of 16)."""
+    c = _dtproj_case(Bz, D, L, R, 100 + L, exact=True)
+    y1, h1 = _run_dtproj(c, Bz, D, L, R, True)
+    y0, h0 = _run_dtproj(c, Bz, D, L, R, False)
+    assert torch.equal(y1, y0)
+    assert torch.equal(h1, h0)
+    assert not y1[:, L:].float().abs().any()
+
+
+@pytest.mark.parametrize("Bz,D,L,R", [(2, 256, 301, 36), (1, 1152, 777, 36)])
+def test_scan_dtproj_matches_oracle(Bz, D, L, R):
+    """Real-valued dt_low / W_dt: the fused dt_proj + scan against the oracle's scan of
+    dt = bf16(dt_low @ W_dt^T) (mamba_simple.py:409-435).  bf16 output 2e-2 abs+rel (an
+    fp32 accumulation-order difference can flip a dt rounding); state 1e-3."""
+    c = _dtproj_case(Bz, D, L, R, 7 + L, exact=False)
+    y, h = _run_dtproj(c, Bz, D, L, R, True)
+    u, dt_ref, z, Bm, Cm, A, Dv, bias = c["cpu"]
+    tr = lambda t: t.transpose(1, 2).float()  # noqa: E731
+    ref_y, ref_h = orc.selective_scan(tr(u), tr(dt_ref), A, tr(Bm), tr(Cm), Dv, tr(z), bias,
+                                      True, c["h0"], True)
+    _close(y[:, :L].transpose(1, 2), ref_y, 2e-2)
+    _close(h, ref_h, 1e-3)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Bz,D,L,segments", [(1, 1152, 3137, 0), (2, 1152, 3137, 0),
                                               (1, 40, 3137, 0), (3, 64, 1000, 24),

@@ -50,6 +50,20 @@ _SIGNATURES = {
          _P, _LL, _LL, _LL, _I, _I, _I, _I, _I, _I,
          _I, _P, _P, _P, _P, _P, _I,              # split, A/D/bias/h0/h_last bwd, frame_len
          _I, _P, _LL, _P, _LL, _P], _I),
+    "vm_selective_scan_dtproj_fwd": (
+        [_P, _LL, _LL, _LL,       # u (sb, sd, sl)
+         _P, _LL, _LL, _I,        # dt_low (sb, sl), dt_rank
+         _P, _I,                  # W_dt padded, its leading dimension
+         _P,                      # A
+         _P, _LL, _LL, _LL,       # B (sb, sn, sl)
+         _P, _LL, _LL, _LL,       # C
+         _P, _P, _LL, _LL, _LL,   # D, z
+         _P, _I,                  # delta_bias, softplus
+         _P, _I, _LL, _LL,        # h0
+         _P, _I, _LL, _LL,        # h_last
+         _P, _LL, _LL, _LL, _I,   # out, out_len
+         _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
+         _P], _I),
     "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_scan_sync_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_scan_sync_status": ([_P, _LL], _I),

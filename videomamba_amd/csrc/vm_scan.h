@@ -69,4 +69,16 @@ size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus = 0)
 // Paired scans need the scalar-B/C kernels and, when segmented, the chunked form.
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes);
 
+// dt_proj folded into the single-pass token-major scan (vm_selective_scan_dtproj_fwd):
+// delta = bf16(dt_low @ W_dt^T) computed per 16-step block on the matrix cores.
+struct DtpArgs {
+  const bf16_t* dtl;  // dt_low = the first dt_rank columns of the x_dbl rows
+  long long dtl_sb;   // batch stride (elements)
+  long long dtl_sl;   // row (step) stride (elements)
+  const bf16_t* wdt;  // W_dt padded: (dim, wdt_ld) bf16, columns >= dt_rank zero
+  int wdt_ld;
+};
+bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_rank);
+void seq_dtp_launch(const ScanParams& p, const DtpArgs& q, int dt_rank, hipStream_t s);
+
 }  // namespace vm

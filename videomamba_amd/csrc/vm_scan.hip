@@ -595,6 +595,51 @@ extern "C" int vm_selective_scan_bidir_fwd(VM_SCAN_ARGS, int split, const float*
 #undef VM_SCAN_ARGS
 #undef VM_SCAN_PASS
 
+extern "C" int vm_selective_scan_dtproj_fwd(
+    const void* u, long long u_sb, long long u_sd, long long u_sl, const void* dt_low,
+    long long dtl_sb, long long dtl_sl, int dt_rank, const void* w_dt, int w_dt_ld,
+    const float* A, const void* B, long long b_sb, long long b_sn, long long b_sl,
+    const void* C, long long c_sb, long long c_sn, long long c_sl, const float* D,
+    const void* z, long long z_sb, long long z_sd, long long z_sl, const float* delta_bias,
+    int delta_softplus, const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
+    void* h_last, int hl_dtype, long long hl_sb, long long hl_sd, void* out, long long o_sb,
+    long long o_sd, long long o_sl, int out_len, int batch, int dim, int seqlen, int dstate,
+    int dtype, vm_stream_t stream) {
+  const char* name = "vm_selective_scan_dtproj_fwd";
+  if (!u || !dt_low || !w_dt || !A || !B || !C || !z || !out) {
+    vmhost::set_error("%s: null required pointer", name);
+    return VM_E_INVALID;
+  }
+  if (batch < 0 || dim < 0 || seqlen < 0 || out_len < seqlen || dstate != kMaxN ||
+      (h0 && !vmhost::dtype_ok(h0_dtype)) || (h_last && !vmhost::dtype_ok(hl_dtype))) {
+    vmhost::set_error("%s: bad shape or state dtype (dstate must be %d)", name, kMaxN);
+    return VM_E_INVALID;
+  }
+  if (batch == 0 || dim == 0) return VM_OK;
+  ScanParams p{};
+  p.u = u; p.delta = nullptr; p.A = A; p.B = B; p.C = C; p.D = D; p.z = z; p.dbias = delta_bias;
+  p.h0 = h0; p.hl = h_last; p.out = out;
+  p.u_sb = u_sb; p.u_sd = u_sd; p.dl_sb = 0; p.dl_sd = 1;
+  p.b_sb = b_sb; p.b_sn = b_sn; p.c_sb = c_sb; p.c_sn = c_sn;
+  p.z_sb = z_sb; p.z_sd = z_sd; p.o_sb = o_sb; p.o_sd = o_sd;
+  p.u_sl = u_sl; p.dl_sl = 0; p.b_sl = b_sl; p.c_sl = c_sl; p.z_sl = z_sl; p.o_sl = o_sl;
+  p.h0_sb = h0_sb; p.h0_sd = h0_sd; p.hl_sb = hl_sb; p.hl_sd = hl_sd;
+  p.batch = batch; p.dim = dim; p.seqlen = seqlen; p.out_len = out_len; p.dstate = dstate;
+  p.softplus = delta_softplus; p.h0_dtype = h0_dtype; p.hl_dtype = hl_dtype;
+  p.split = batch;
+  DtpArgs q{};
+  q.dtl = static_cast<const bf16_t*>(dt_low); q.dtl_sb = dtl_sb; q.dtl_sl = dtl_sl;
+  q.wdt = static_cast<const bf16_t*>(w_dt); q.wdt_ld = w_dt_ld;
+  if (!seq_dtp_supported(p, q, dtype, dt_rank)) {
+    vmhost::set_error("%s: needs bf16 token-major operands with z, softplus, 16 states, C "
+                      "directly after B in the x_dbl rows, dim %% 128 == 0, dt_rank <= 64, "
+                      "8-byte aligned dt_low rows and a (dim, >= 16*ceil(r/16)) W_dt", name);
+    return VM_E_INVALID;
+  }
+  seq_dtp_launch(p, q, dt_rank, static_cast<hipStream_t>(stream));
+  return vmhost::launch_status(name);
+}
+
 extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen,
                                                        int dstate, int segments) {
   if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN) return 0;

@@ -493,6 +493,257 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
   }
 }
 
+// ============================================================ dt_proj inside the scan
+// scan_seq_dtp_kernel: the single-pass bench kernel (MODE 0, scalar B|C rows, packed state
+// pairs, delta in log2 units) with dt_proj folded in.  Instead of reading a precomputed
+// dt row (written by conv_proj and read straight back: 2 * B*L*D bytes of HBM traffic per
+// layer), every wave computes the dt of its 64 channels for 16 steps at a time on the
+// matrix cores,  dt[t][c] = bf16( sum_k dt_low[t][k] * W_dt[c][k] )  (mamba_simple.py:
+// 409-413: dt = dt_proj.weight @ x_dbl[:, :R]^T, rounded to the model dtype there), from
+// the x_dbl rows the scan already reads for B|C:
+//   A = dt_low rows (16 steps x 16*NKS k, v_mfma_f32_16x16x16_bf16 fragments by buffer
+//       load, one block ahead), B = W_dt^T (this wave's 64 channels, staged in LDS once),
+//   D (16 steps x 16 channels per tile, 4 tiles) -> bf16 pairs -> an LDS block
+//   [channel][16 steps], from which each lane reads its own channel's steps 4 at a time.
+// Per step the arithmetic is the single-pass kernel's; the buffer load of dt becomes an
+// LDS read, and per 16 steps a wave adds 4 * NKS MFMAs, 8 bf16 packs and 4 + 4 LDS ops.
+// Every token's dt is computed from its own x_dbl row in a fixed order, so the result does
+// not depend on the sequence length (chunked == full stays exact).
+constexpr int kDtG = 16;    // steps per dt block
+constexpr int kDtRow = 10;  // dwords per channel row of the LDS dt block (16 bf16 + pad)
+
+typedef short dtp_s4 __attribute__((ext_vector_type(4)));
+typedef __bf16 dtp_b2 __attribute__((ext_vector_type(2)));
+typedef float dtp_f2 __attribute__((ext_vector_type(2)));
+// two fp32 -> two bf16 (round to nearest even) in one v_cvt_pk_bf16_f32: lo = a, hi = b
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(dtp_f2{a, b}, dtp_b2));
+}
+typedef float dtp_f4 __attribute__((ext_vector_type(4)));
+
+template <int NKS>
+__global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanParams p,
+                                                                    const DtpArgs q) {
+  typedef __attribute__((address_space(4))) const uint32_t* cptr;
+  typedef bf16_t T;
+  constexpr int NW = kSeqNW;
+  constexpr int NWD = kMaxN * 2 / 4;  // 32-bit words per B (or C) row
+  constexpr int ES = 2;
+  constexpr int KP = 16 * NKS + 4;    // bf16 per LDS W_dt row (8-byte pad: fewer bank conflicts)
+  __shared__ __attribute__((aligned(16))) bf16_t sW[NW][64 * KP];
+  __shared__ __attribute__((aligned(16))) uint32_t sD[NW][64 * kDtRow];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;
+  xcd_order(gx, gy, gz);
+  const int b = gz;
+  const int d0 = __builtin_amdgcn_readfirstlane((gx * NW + wave) * 64);  // dim % 128 == 0
+  const int d = d0 + lane;
+  const int L = p.seqlen;
+  const int tlast = L > 0 ? L - 1 : 0;
+
+  // W_dt rows of this wave's channels -> LDS (lane = channel, 16*NKS bf16)
+  {
+    const bf16_t* wrow = q.wdt + static_cast<long long>(d) * q.wdt_ld;
+    bf16_t* srow = &sW[wave][lane * KP];
+#pragma unroll
+    for (int i = 0; i < 2 * NKS; ++i) {
+      const uint2 v = *reinterpret_cast<const uint2*>(wrow + 4 * i);
+      *reinterpret_cast<uint2*>(srow + 4 * i) = v;
+    }
+  }
+
+  f2 A2[kMaxN / 2], h[kMaxN / 2];
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) {
+    const float a = p.A[d * kMaxN + n];
+    const float h_init =
+        p.h0 ? load_dyn(p.h0, b * p.h0_sb + d * p.h0_sd + n, p.h0_dtype) * kLog2e : 0.0f;
+    if (n & 1) {
+      A2[n >> 1].y = a;
+      h[n >> 1].y = h_init;
+    } else {
+      A2[n >> 1].x = a;
+      h[n >> 1].x = h_init;
+    }
+  }
+  const float Dv = (p.D ? p.D[d] : 0.0f) * kLog2e;
+  const float bias = (p.dbias ? p.dbias[d] : 0.0f) * kLog2e;
+  const int voff = lane * ES;
+  const auto ur = uniform_rsrc(static_cast<const T*>(p.u) + b * p.u_sb + d0);
+  const auto zr = uniform_rsrc(static_cast<const T*>(p.z) + b * p.z_sb + d0);
+  const auto orr = uniform_rsrc(static_cast<T*>(p.out) + b * p.o_sb + d0);
+  // dt_low rows of this batch row; rows past out_len read as 0 (bounded descriptor)
+  const auto dtr = [&]() {
+    const uint64_t a = reinterpret_cast<uint64_t>(q.dtl + b * q.dtl_sb);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+    void* ub = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(
+        ub, 0, static_cast<int>(static_cast<long long>(p.out_len) * q.dtl_sl * ES), 0x00020000);
+  }();
+  const int us = static_cast<int>(p.u_sl) * ES, zs = static_cast<int>(p.z_sl) * ES;
+  const int os = static_cast<int>(p.o_sl) * ES, dls = static_cast<int>(q.dtl_sl) * ES;
+  const T* Bq = static_cast<const T*>(p.B) + b * p.b_sb;
+  const uint32_t bsl = static_cast<uint32_t>(p.b_sl * ES);
+  uint32_t bcw[2][2 * NWD];
+  auto bc_load = [&](int t, uint32_t (&dst)[2 * NWD]) {
+    const cptr bp = (cptr)(reinterpret_cast<const char*>(Bq) + static_cast<uint32_t>(t) * bsl);
+#pragma unroll
+    for (int i = 0; i < 2 * NWD; ++i) dst[i] = bp[i];
+  };
+
+  // ---- the dt block: A fragments (dt_low rows tg .. tg+15) in `af`, W_dt^T from LDS ----
+  const int a_voff = ((lane & 15) * static_cast<int>(q.dtl_sl) + 4 * (lane >> 4)) * ES;
+  auto a_load = [&](int tg, uint2 (&af)[NKS]) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(dtr, a_voff + 16 * ks * ES, tg * dls, 0);
+      af[ks] = uint2{v[0], v[1]};
+    }
+  };
+  auto dt_block = [&](const uint2 (&af)[NKS]) {
+#pragma unroll
+    for (int tile = 0; tile < 4; ++tile) {
+      dtp_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      const bf16_t* wb = &sW[wave][(16 * tile + (lane & 15)) * KP + 4 * (lane >> 4)];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const uint2 bw = *reinterpret_cast<const uint2*>(wb + 16 * ks);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(
+            __builtin_bit_cast(dtp_s4, af[ks]), __builtin_bit_cast(dtp_s4, bw), acc, 0, 0, 0);
+      }
+      // D[4 (lane>>4) + i][lane & 15] -> channel 16 tile + (lane & 15), steps 4 (lane>>4) + i
+      const uint32_t p01 = cvt_pk_bf16(acc[0], acc[1]);
+      const uint32_t p23 = cvt_pk_bf16(acc[2], acc[3]);
+      *reinterpret_cast<uint2*>(&sD[wave][(16 * tile + (lane & 15)) * kDtRow + 2 * (lane >> 4)]) =
+          uint2{p01, p23};
+    }
+  };
+  // a lane's own channel, steps 4k .. 4k+3 of the block
+  auto dq_read = [&](int k) {
+    return *reinterpret_cast<const uint2*>(&sD[wave][lane * kDtRow + 2 * k]);
+  };
+  auto dt_of = [&](const uint2& dq, int j) {  // step j % 4 of a quad
+    const uint32_t w = (j & 2) ? dq.y : dq.x;
+    return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
+  };
+  auto delta_of = [&](float dr) {  // delta' = softplus(dt + bias) * log2e (log2 units)
+    const float x = fmaf(dr, kLog2e, bias);
+    return x > 20.0f * kLog2e ? x : __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(x));
+  };
+  auto gate_of = [&](uint32_t raw) {
+    const float zz = raw_f32<T>(raw);
+    return zz * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e));
+  };
+
+  // prologue: block 0's dt, the first quad, u / z / B|C of the first kPF steps
+  uint2 af[NKS];
+  a_load(0, af);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();  // sW is written (each wave reads only its own rows; one barrier is cheap)
+  dt_block(af);
+  uint2 dqa[4];  // the block's four quads (steps 4k .. 4k+3), each read a quad ahead
+  dqa[0] = dq_read(0);
+  dqa[1] = dqa[2] = dqa[3] = dqa[0];
+  uint32_t ru[kPF], rz[kPF];
+  bc_load(0, bcw[0]);
+#pragma unroll
+  for (int j = 0; j < kPF; ++j) {
+    const int t = min(j, tlast);
+    ru[j] = bload<T>(ur, voff, t * us);
+    rz[j] = bload<T>(zr, voff, t * zs);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  float dl_nx = delta_of(dt_of(dqa[0], 0));
+  float g_nx = gate_of(rz[0]);
+
+  // One step: t, slot j = t % 16 within the dt block; refill slot j % kPF at (vu, su)/(vz, sz).
+  auto step = [&](const int t, const int j, const bool live, const int vu, const int su,
+                  const int vz, const int sz) {
+    const int s = j & (kPF - 1);
+    const float uu = raw_f32<T>(ru[s]);
+    ru[s] = bload<T>(ur, vu, su);
+    rz[s] = bload<T>(zr, vz, sz);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B|C rows have landed
+    bc_load(t + 1 < tlast ? t + 1 : tlast, bcw[(j + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    // the next step's delta and gate a step early (as scan_seq_kernel); its dt sits in the
+    // current quad, the next quad (j % 4 == 3), or the next block's first quad (j == 15)
+    float dl = dl_nx;
+    dl_nx = delta_of(dt_of(dqa[((j + 1) >> 2) & 3], (j + 1) & 3));
+    const float gf = g_nx;
+    g_nx = gate_of(rz[(s + 1) & (kPF - 1)]);
+    dl = live ? dl : 0.0f;
+    const float du = dl * uu;
+    const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+    const f2 dl2 = {dl, dl}, du2 = {du, du};
+    f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
+#pragma unroll
+    for (int qq = 0; qq < kMaxN / 2; ++qq) {
+      const f2 Bp = f2{__uint_as_float(cw[qq] << 16), __uint_as_float(cw[qq] & 0xffff0000u)};
+      const f2 Cp = f2{__uint_as_float(cw[NWD + qq] << 16),
+                       __uint_as_float(cw[NWD + qq] & 0xffff0000u)};
+      const f2 x = dl2 * A2[qq];
+      const f2 a = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+      h[qq] = __builtin_elementwise_fma(a, h[qq], du2 * Bp);
+      if (qq & 1) yb = __builtin_elementwise_fma(h[qq], Cp, yb);
+      else ya = __builtin_elementwise_fma(h[qq], Cp, ya);
+    }
+    const f2 ys = ya + yb;
+    const float y = (ys.x + ys.y) * gf;
+    bstore<T>(from_f32<T>(y), orr, live ? voff : kSeqDead, t * os);
+  };
+  // block bookkeeping around step j of the block starting at tg: prefetch the next block's
+  // A fragments at j == 0, the next quad at j % 4 == 0, the next block's dt after j == 14
+  uint2 afn[NKS];
+  auto around = [&](const int tg, const int j) {
+    if (j == 0) a_load(tg + kDtG, afn);
+    if ((j & 3) == 0 && j < 12) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);
+    if (j == 14) {
+      dt_block(afn);         // every read of this block's LDS rows has been issued
+      dqa[0] = dq_read(0);  // the next block's first quad, consumed from step 15 on
+    }
+  };
+
+  int t0 = 0;
+  // Main loop: whole 16-step blocks whose u / z refills (kPF ahead) stay in the sequence:
+  // no clamps; the refill byte offsets are two running SGPRs advanced by one scalar add per
+  // step (asm: left to itself the compiler precomputes all 32 of a block's offsets and
+  // spills them to VGPR lanes, which costs a v_readlane per load)
+  int su = kPF * us, sz = kPF * zs;
+  for (; t0 + kDtG + kPF <= L; t0 += kDtG) {
+#pragma unroll
+    for (int j = 0; j < kDtG; ++j) {
+      around(t0, j);
+      step(t0 + j, j, true, voff, su, voff, sz);
+      asm volatile("s_add_u32 %0, %0, %1" : "+s"(su) : "s"(us) : "scc");
+      asm volatile("s_add_u32 %0, %0, %1" : "+s"(sz) : "s"(zs) : "scc");
+    }
+  }
+  // Tail: clamped refills and live masks, same block structure.
+  for (; t0 < L; t0 += kDtG) {
+#pragma unroll
+    for (int j = 0; j < kDtG; ++j) {
+      around(t0, j);
+      const int t = t0 + j;
+      const int tn = min(t + kPF, tlast);
+      step(t, j, t < L, voff, tn * us, voff, tn * zs);
+    }
+  }
+  if (L > 0) {
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n)
+      if (p.hl)
+        store_dyn(p.hl, b * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
+                  ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * kLn2f);
+  }
+  for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
+}
+
 // ============================================================ chunked form (small batches)
 // The sequence is cut into segments of T steps; a workgroup holds kChW consecutive segments
 // of one 64-channel group (one wave per segment, lane = channel), so the chip fills even at
@@ -1324,6 +1575,32 @@ void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
   }
   if (dtype == VM_DTYPE_BF16) launch_seq<bf16_t>(p, w, s);
   else launch_seq<float>(p, w, s);
+}
+
+bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_rank) {
+  const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
+                   static_cast<const bf16_t*>(p.C) == static_cast<const bf16_t*>(p.B) + kMaxN;
+  const int nks = (dt_rank + 15) / 16;
+  const long long dl_span = static_cast<long long>(p.out_len) * q.dtl_sl * 2;
+  return dtype == VM_DTYPE_BF16 && seq_supported(p, dtype) && seq_sgpr_bc(p, 2) && bc1 &&
+         p.dstate == kMaxN && p.z && p.softplus && p.split == p.batch &&
+         p.dim % (64 * kSeqNW) == 0 && dt_rank >= 1 && dt_rank <= 64 && q.dtl && q.wdt &&
+         q.wdt_ld >= 16 * nks && q.wdt_ld % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(q.wdt) & 7) == 0 &&
+         (reinterpret_cast<uintptr_t>(q.dtl) & 7) == 0 && q.dtl_sl % 4 == 0 &&
+         q.dtl_sb % 4 == 0 && q.dtl_sl >= dt_rank && dl_span < (1ll << 31) &&
+         static_cast<long long>(p.seqlen) * q.dtl_sl * 2 < (1ll << 31);
+}
+
+void seq_dtp_launch(const ScanParams& p, const DtpArgs& q, int dt_rank, hipStream_t s) {
+  const int groups = p.dim / 64;
+  const dim3 grid(groups / kSeqNW, 1, p.batch);
+  switch ((dt_rank + 15) / 16) {
+    case 1: hipLaunchKernelGGL(scan_seq_dtp_kernel<1>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;
+    case 2: hipLaunchKernelGGL(scan_seq_dtp_kernel<2>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;
+    case 3: hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;
+    default: hipLaunchKernelGGL(scan_seq_dtp_kernel<4>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;
+  }
 }
 
 }  // namespace vm

@@ -271,6 +271,26 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
     _lib.check(rc, "vm_selective_scan_bidir_fwd")
 
 
+def scan_dtproj_raw(u, u_s, dtl, dtl_s, dt_rank, wdt_pad, A32, B, b_s, C, c_s, D32, z, z_s,
+                    bias32, h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen,
+                    dstate, stream):
+    """``vm_selective_scan_dtproj_fwd``: the single-pass token-major scan with dt_proj
+    folded in — delta = bf16(dt_low @ W_dt^T) per 16-step block on the matrix cores, then
+    softplus(delta + bias) as selective_scan_fn.  ``dtl`` = the x_dbl rows (dt_low = their
+    first ``dt_rank`` columns), ``dtl_s`` = (batch, row) element strides; ``wdt_pad`` = the
+    zero-padded (D, 32|64) bf16 W_dt.  bf16 only, z and softplus on."""
+    rc = _lib.load().vm_selective_scan_dtproj_fwd(
+        _p(u), u_s[0], u_s[1], u_s[2], _p(dtl), dtl_s[0], dtl_s[1], int(dt_rank),
+        _p(wdt_pad), wdt_pad.stride(0), _p(A32),
+        _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
+        _p(D32), _p(z), z_s[0], z_s[1], z_s[2], _p(bias32), 1,
+        _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
+        _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
+        _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate,
+        dtype_code(u.dtype), stream)
+    _lib.check(rc, "vm_selective_scan_dtproj_fwd")
+
+
 def conv_raw(x, x_s, w32, b32, cs_in, csi_s, cs_out, cso_s, out, o_s, out_len, batch, dim,
              seqlen, width, silu, dtype, stream):
     """x_s / o_s: (batch, channel, step) element strides (unit step or unit channel)."""

@@ -261,10 +261,24 @@ class Mamba(nn.Module):
             out += self.out_proj.bias.to(out.dtype)
         return out.view(Bsz, Lp, C)
 
-    def _tm_front(self, hn, seqlen, conv_state_in, conv_state_out, bufs=None):
+    def _dtp_ok(self, hn: Tensor, seqlen: int) -> bool:
+        """Fold dt_proj into the scan (vm_selective_scan_dtproj_fwd): bf16 fused conv_proj
+        path, 16 states, D % 128 == 0, and a single-pass scan at this batch (the segmented
+        small-batch forms read a dt row); "auto" only above the split-K batch (> 8), where
+        conv_proj's wide kernel would otherwise write dt rows the scan reads straight back."""
+        mode = options.get().scan_dt_proj
+        Bsz = hn.shape[0]
+        if mode == "off" or (mode == "auto" and Bsz <= 8):
+            return False
+        return (self._fused_conv_proj_ok(hn, seqlen) and self.d_state == 16
+                and self.d_inner % 128 == 0 and self.dt_rank <= 64
+                and K.scan_workspace_bytes(Bsz, self.d_inner, seqlen, self.d_state) == 0)
+
+    def _tm_front(self, hn, seqlen, conv_state_in, conv_state_out, bufs=None, want_dt=True):
         """in_proj -> conv + silu -> x_proj -> dt_proj of the token-major form: (xz, u,
         x_dbl, dt), each (B*Lp, channels).  ``bufs`` = preallocated (xz, u, x_dbl, dt) (the
-        refiner's paired buffers); otherwise they are allocated here."""
+        refiner's paired buffers); otherwise they are allocated here.  ``want_dt=False``
+        (fused conv_proj only) skips dt_proj: dt is None, the scan computes it."""
         Bsz, Lp, C = hn.shape
         Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
         n = Bsz * Lp
@@ -292,10 +306,11 @@ class Mamba(nn.Module):
             wx_pad, wdt_pad = self._padded_proj_weights()
             if x_dbl is None:
                 x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
-                dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+                dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device) if want_dt else None
             K.conv_proj_raw(xz, s_xz[::2], cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
-                            wx_pad, E, wdt_pad, R, u, s_u[::2], x_dbl, (Lp * E, E), dt,
-                            s_u[::2], Lp, Bsz, Dm, seqlen, W, stream)
+                            wx_pad, E, wdt_pad if want_dt else None, R, u, s_u[::2], x_dbl,
+                            (Lp * E, E), dt if want_dt else None, s_u[::2], Lp, Bsz, Dm, seqlen,
+                            W, stream)
         else:
             K.conv_raw(xz, s_xz, cw, cb, conv_state_in, csi_s, conv_state_out, cso_s,
                        u, s_u, Lp, Bsz, Dm, seqlen, W, True, dt_code, stream)
@@ -316,13 +331,21 @@ class Mamba(nn.Module):
         stream = torch.cuda.current_stream(hn.device).cuda_stream
         A, Dv, dbias, _, _ = self._fp32_params()
         s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
-        xz, u, x_dbl, dt = self._tm_front(hn, seqlen, conv_state_in, conv_state_out)
+        dtp = self._dtp_ok(hn, seqlen)
+        xz, u, x_dbl, dt = self._tm_front(hn, seqlen, conv_state_in, conv_state_out,
+                                          want_dt=not dtp)
         y = torch.empty_like(u)
-        K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
-                   xz[:, Dm:], s_xz, dbias, True,
-                   h0, (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0),
-                   h_last, (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0),
-                   y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+        h0_s = (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0)
+        hl_s = (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0)
+        if dtp:  # dt_proj inside the scan: no dt rows written or read
+            _, wdt_pad = self._padded_proj_weights()
+            K.scan_dtproj_raw(u, s_u, x_dbl, (Lp * E, E), R, wdt_pad, A, x_dbl[:, R:R + N],
+                              s_bc, x_dbl[:, R + N:], s_bc, Dv, xz[:, Dm:], s_xz, dbias,
+                              h0, h0_s, h_last, hl_s, y, s_u, Lp, Bsz, Dm, seqlen, N, stream)
+        else:
+            K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
+                       xz[:, Dm:], s_xz, dbias, True, h0, h0_s, h_last, hl_s,
+                       y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
         out = _linear(y, self.out_proj.weight, self.out_proj.bias)  # (n, C)
         return out.view(Bsz, Lp, C)
 

@@ -21,6 +21,10 @@ documented options object; tests and sweeps change them with :func:`override`.
                      workgroup per CU runs as one launch (blocks hand their aggregates on
                      through a zeroed sync buffer, vm_selective_scan_fwd ``sync``); False:
                      the two-launch form (identical results).
+    scan_dt_proj     "auto" (default): at chip-filling batches (> 8 clips, single-pass scan) the
+                     bf16 token-major mixer folds dt_proj into the scan
+                     (vm_selective_scan_dtproj_fwd) and conv_proj skips its dt rows; "on":
+                     whenever the single-pass scan runs (tests); "off": conv_proj writes dt.
     small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -49,6 +53,7 @@ class Options:
     scan_segments: int = 0
     fused_conv_proj: bool = True
     scan_one_launch: bool = True
+    scan_dt_proj: str = "auto"
     gemm_tuning: str = "on"
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
@@ -60,6 +65,8 @@ class Options:
             raise ValueError("scan_segments must be >= 0")
         if int(self.small_gemm_rows) < 0:
             raise ValueError("small_gemm_rows must be >= 0")
+        if self.scan_dt_proj not in ("auto", "on", "off"):
+            raise ValueError(f"scan_dt_proj must be auto / on / off, got {self.scan_dt_proj!r}")
         if self.gemm_tuning not in _TUNING:
             raise ValueError(f"gemm_tuning must be one of {_TUNING}, got {self.gemm_tuning!r}")
 
