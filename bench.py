@@ -362,10 +362,16 @@ def cpu_baseline(cfg, threads):
     dt = _oracle_clip_seconds(cfg)
     ti = CONFIGS["ti8"]
     dt_c1 = _oracle_clip_seconds(ti)
+    cal = _cpu_calibration()
+    key = {16: "m16", 8: "ti8"}.get(cfg["frames"]) if cfg["embed_dim"] in (576, 192) else None
+    ratio = (cal or {}).get("oracle_over_reference_s_per_clip", {}).get(key)
     return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
             "cores": threads, "kind": "port", "cpu_model": model,
             "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
-            "calibration": _cpu_calibration(),
+            "calibration": cal,
+            # the reference's own CPU path on these cores, scaled by the one-session
+            # oracle/reference time ratio of the calibration record (the port is faster)
+            "reference_rate_estimate": round(cfg["frames"] * 196 / dt * ratio, 2) if ratio else None,
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
                       f"median of 3 after 1 warm-up ({dt:.2f} s), oracle/videomamba_oracle.py",
             "c1": {"value": round(ti["frames"] * 196 / dt_c1, 2), "unit": "video-tokens/s",

@@ -15,6 +15,9 @@ import torch  # noqa: E402
 from bench import scan_roofline  # noqa: E402
 
 dev = torch.device("cuda", 0)
-for B in [int(b) for b in (sys.argv[2:] or ["1", "336"])]:
-    r = scan_roofline(B, 30, dev, "tm")
-    print(json.dumps({"variant": name, "B": B, "avg_us": r["avg_us"], "frac": r["frac"]}), flush=True)
+args = sys.argv[2:]
+dtp = "--dtp" in args
+for B in [int(b) for b in ([a for a in args if a != "--dtp"] or ["1", "336"])]:
+    r = scan_roofline(B, 30, dev, "tm", dtp=dtp)
+    print(json.dumps({"variant": name, "dtp": dtp, "B": B, "kernel": r["kernel"],
+                      "avg_us": r["avg_us"], "frac": r["frac"]}), flush=True)

@@ -549,7 +549,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     const bf16_t* wrow = q.wdt + static_cast<long long>(d) * q.wdt_ld;
     bf16_t* srow = &sW[wave][lane * KP];
 #pragma unroll
-    for (int i = 0; i < 2 * NKS; ++i) {
+    for (int i = 0; i < 4 * NKS; ++i) {  // 16 * NKS bf16 as 4-element (8-byte) pieces
       const uint2 v = *reinterpret_cast<const uint2*>(wrow + 4 * i);
       *reinterpret_cast<uint2*>(srow + 4 * i) = v;
     }
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
 
   // One step: t, slot j = t % 16 within the dt block; refill slot j % kPF at (vu, su)/(vz, sz).
   auto step = [&](const int t, const int j, const bool live, const int vu, const int su,
-                  const int vz, const int sz) {
+                  const int vz, const int sz, auto&& mid) {
     const int s = j & (kPF - 1);
     const float uu = raw_f32<T>(ru[s]);
     ru[s] = bload<T>(ur, vu, su);
@@ -671,6 +671,9 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B|C rows have landed
     bc_load(t + 1 < tlast ? t + 1 : tlast, bcw[(j + 1) & 1]);
     __builtin_amdgcn_sched_barrier(0);
+    // the block bookkeeping goes after that wait, so the next step's lgkmcnt(0) (a step
+    // later) is the first to wait for its LDS reads / writes
+    mid();
     // the next step's delta and gate a step early (as scan_seq_kernel); its dt sits in the
     // current quad, the next quad (j % 4 == 3), or the next block's first quad (j == 15)
     float dl = dl_nx;
@@ -680,7 +683,12 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     dl = live ? dl : 0.0f;
     const float du = dl * uu;
     const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
-    const f2 dl2 = {dl, dl}, du2 = {du, du};
+    const f2 dl2 = {dl, dl};
+    // du as a genuine register pair (one packed multiply): a {du, du} pair formed with
+    // op_sel leaves its unused half free for the allocator, which can make it the
+    // destination of an in-flight refill load — the packed read then waits for that load
+    // (a vmcnt(1) at the block head)
+    const f2 du2 = dl2 * f2{uu, uu};
     f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
 #pragma unroll
     for (int qq = 0; qq < kMaxN / 2; ++qq) {
@@ -697,8 +705,8 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     const float y = (ys.x + ys.y) * gf;
     bstore<T>(from_f32<T>(y), orr, live ? voff : kSeqDead, t * os);
   };
-  // block bookkeeping around step j of the block starting at tg: prefetch the next block's
-  // A fragments at j == 0, the next quad at j % 4 == 0, the next block's dt after j == 14
+  // block bookkeeping in step j of the block starting at tg: prefetch the next block's
+  // A fragments at j == 0, the next quad at j % 4 == 0, the next block's dt at j == 14
   uint2 afn[NKS];
   auto around = [&](const int tg, const int j) {
     if (j == 0) a_load(tg + kDtG, afn);
@@ -718,8 +726,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   for (; t0 + kDtG + kPF <= L; t0 += kDtG) {
 #pragma unroll
     for (int j = 0; j < kDtG; ++j) {
-      around(t0, j);
-      step(t0 + j, j, true, voff, su, voff, sz);
+      step(t0 + j, j, true, voff, su, voff, sz, [&]() { around(t0, j); });
       asm volatile("s_add_u32 %0, %0, %1" : "+s"(su) : "s"(us) : "scc");
       asm volatile("s_add_u32 %0, %0, %1" : "+s"(sz) : "s"(zs) : "scc");
     }
@@ -728,10 +735,9 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   for (; t0 < L; t0 += kDtG) {
 #pragma unroll
     for (int j = 0; j < kDtG; ++j) {
-      around(t0, j);
       const int t = t0 + j;
       const int tn = min(t + kPF, tlast);
-      step(t, j, t < L, voff, tn * us, voff, tn * zs);
+      step(t, j, t < L, voff, tn * us, voff, tn * zs, [&]() { around(t0, j); });
     }
   }
   if (L > 0) {

@@ -51,31 +51,43 @@ from .layers import round_up, warn_if_grad
 _SMALL_GEMM_K = (192, 384, 576, 768, 1152, 1536)  # vm_linear_fwd's unrolled K-step counts
 
 
-def _small_gemm_ok(x: Tensor, w: Tensor, b: Optional[Tensor], out: Optional[Tensor] = None) -> bool:
-    """One clip's token rows in bf16 with a narrow output (out_proj, N = C) take the HIP
-    small-M GEMM (vm_linear_fwd): 11.0 vs 13.4 us at B = 1 M-16f.  in_proj (N = 2D) stays on
-    the library GEMM, which is faster there (14.8 vs 16.8 us)."""
-    lim = options.get().small_gemm_rows
+def _small_gemm_ok(x: Tensor, w: Tensor, b: Optional[Tensor], out: Optional[Tensor] = None,
+                   clips: Optional[int] = None) -> bool:
+    """bf16 projections run on the HIP GEMM (vm_linear_fwd, each output row computed in the
+    same order whatever the row count) instead of the library GEMM when
+      * the mixer holds at most ``options.row_invariant_gemm_clips`` clips (streaming
+        batches): at every token count, so a chunked stream equals the one-pass forward bit
+        for bit — the library picks M-dependent kernels (C5, 16 x 64-frame chunks vs one
+        1,024-frame pass: 6.2e-4 relative on the last chunk with the library, 0.0 with this
+        GEMM; scripts/diag/c5_invariance.py); or
+      * one clip's rows with a narrow output (out_proj at B = 1: 11.0 vs 13.4 us)."""
+    o = options.get()
     ok16 = lambda t: t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(1) == 1  # noqa: E731
-    return (0 < x.shape[0] <= lim and b is None and x.dtype == torch.bfloat16
+    if not (x.shape[0] > 0 and b is None and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.is_cuda and x.shape[1] in _SMALL_GEMM_K
-            and w.shape[0] % 8 == 0 and w.shape[0] <= options.get().small_gemm_max_n and ok16(x)
-            and ok16(w) and (out is None or ok16(out)))
+            and w.shape[0] % 8 == 0 and ok16(x) and ok16(w) and (out is None or ok16(out))
+            and x.shape[0] * x.stride(0) * 2 < (1 << 31)):
+        return False
+    if clips is not None and 0 < clips <= o.row_invariant_gemm_clips:
+        return True
+    return x.shape[0] <= o.small_gemm_rows and w.shape[0] <= o.small_gemm_max_n
 
 
-def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
-    """A projection GEMM of the mixer: the HIP small-M GEMM for one clip's rows, else the
-    library GEMM with the shipped tuning results."""
-    if _small_gemm_ok(x, w, b):
+def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None,
+            clips: Optional[int] = None) -> Tensor:
+    """A projection GEMM of the mixer: the HIP GEMM for streaming-sized batches and one
+    clip's narrow projections, else the library GEMM with the shipped tuning results."""
+    if _small_gemm_ok(x, w, b, clips=clips):
         return K.linear(x, w)
     with tuned():
         return F.linear(x, w, b)
 
 
-def _linear_into(x: Tensor, w: Tensor, b: Optional[Tensor], out: Tensor) -> Tensor:
+def _linear_into(x: Tensor, w: Tensor, b: Optional[Tensor], out: Tensor,
+                 clips: Optional[int] = None) -> Tensor:
     """:func:`_linear` into a preallocated buffer with unit column stride (a half of the
     bidirectional refiner's paired buffers)."""
-    if _small_gemm_ok(x, w, b, out):
+    if _small_gemm_ok(x, w, b, out, clips=clips):
         return K.linear(x, w, out=out)
     with tuned():
         if b is None:
@@ -288,12 +300,13 @@ class Mamba(nn.Module):
         _, _, _, cw, cb = self._fp32_params()
         s_u, s_xz = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm)
         if bufs is None:
-            xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias)  # (n, 2D)
+            xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias,
+                         clips=Bsz)  # (n, 2D)
             u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
             x_dbl = dt = None
         else:
             xz, u, x_dbl, dt = bufs
-            _linear_into(hn.view(n, C), self.in_proj.weight, self.in_proj.bias, xz)
+            _linear_into(hn.view(n, C), self.in_proj.weight, self.in_proj.bias, xz, clips=Bsz)
         csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
@@ -346,7 +359,7 @@ class Mamba(nn.Module):
             K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                        xz[:, Dm:], s_xz, dbias, True, h0, h0_s, h_last, hl_s,
                        y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
-        out = _linear(y, self.out_proj.weight, self.out_proj.bias)  # (n, C)
+        out = _linear(y, self.out_proj.weight, self.out_proj.bias, clips=Bsz)  # (n, C)
         return out.view(Bsz, Lp, C)
 
     def _check_state(self, t: Tensor, last: int, what: str, batch: int) -> Tensor:

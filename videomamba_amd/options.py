@@ -25,6 +25,11 @@ documented options object; tests and sweeps change them with :func:`override`.
                      bf16 token-major mixer folds dt_proj into the scan
                      (vm_selective_scan_dtproj_fwd) and conv_proj skips its dt rows; "on":
                      whenever the single-pass scan runs (tests); "off": conv_proj writes dt.
+    row_invariant_gemm_clips
+                     mixers holding at most this many clips (default 8: streaming batches)
+                     run in_proj / out_proj on the HIP GEMM at every token count, whose rows
+                     do not depend on the row count — chunked streaming == the one-pass
+                     forward bit for bit; 0: only the small_gemm_* rule below.
     small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -55,6 +60,7 @@ class Options:
     scan_one_launch: bool = True
     scan_dt_proj: str = "auto"
     gemm_tuning: str = "on"
+    row_invariant_gemm_clips: int = 8
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
 

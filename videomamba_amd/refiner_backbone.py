@@ -187,8 +187,8 @@ class BiMambaRefinerBlock(nn.Module):
 
         # out_proj of each direction straight into the gate's concatenated input
         cat = torch.empty((n, 2 * C), dtype=hdt, device=dev)
-        _linear_into(half(y, 0), mf.out_proj.weight, mf.out_proj.bias, cat[:, :C])
-        _linear_into(half(y, 1), mb.out_proj.weight, mb.out_proj.bias, cat[:, C:])
+        _linear_into(half(y, 0), mf.out_proj.weight, mf.out_proj.bias, cat[:, :C], clips=B)
+        _linear_into(half(y, 1), mb.out_proj.weight, mb.out_proj.bias, cat[:, C:], clips=B)
         out_f, out_b = cat[:, :C], cat[:, C:]
         gate = self.fusion_gate(cat)
         out = self.out_proj(gate * out_f + (1.0 - gate) * out_b).view(B, Lp, C)
