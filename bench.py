@@ -11,7 +11,7 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
-Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 336 clips per rank by default, so
+Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 448 clips per rank by default, so
 the 1/2/4/8-GPU curve keeps every GPU at the batch where the scan holds its occupancy —
 weak scaling; --global-batch G instead splits G clips across ranks with
 sharding.shard_range — strong scaling; run under torchrun for the 8-GPU case), --config ti8
@@ -76,6 +76,8 @@ def _args():
     ap.add_argument("--p50-chunks", type=int, default=100)
     ap.add_argument("--scan-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-b1", action="store_true",
+                    help="skip the B=1 chunk latency and per-stage B=1 rooflines (batch sweeps)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle threads (0: the CPUs this process may run on, at most 16 — "
                          "a one-GPU box's share)")
@@ -86,7 +88,10 @@ def _args():
     a = ap.parse_args()
     a.batch_default = a.batch is None
     if a.batch is None:
-        a.batch = CONFIGS[a.config].get("batch", 336)
+        # 448 clips per GPU: the single-pass scan grid (9 workgroups per clip, 8 resident per
+        # CU) runs ~2 full rounds; at 336 (1.5 rounds) the dt_proj-in-scan kernel loses 15 %
+        # in the partial second round (profiles/r03c_batch_sweep.txt)
+        a.batch = CONFIGS[a.config].get("batch", 448)
     return a
 
 
@@ -527,20 +532,22 @@ def main():
                     lat.append((time.perf_counter() - t1) * 1e3)
             return statistics.median(lat)
 
-        p50_eager = chunk_lat(lambda: model(x1, ssm_state=st1, temporal_pos_offset=0))
-        p50_graph = chunk_lat(lambda: runner.run(x1, temporal_pos_offset=0))
+        p50_eager = p50_graph = None
+        if not args.no_b1:
+            p50_eager = chunk_lat(lambda: model(x1, ssm_state=st1, temporal_pos_offset=0))
+            p50_graph = chunk_lat(lambda: runner.run(x1, temporal_pos_offset=0))
         from videomamba_amd.mamba_simple import mixer_layout
         mx0 = model.layers[0].mixer
         hn0 = torch.empty((max(B, 1), 8, cfg["embed_dim"]), device=device, dtype=torch.bfloat16)
         roof = scan_roofline(max(B, 1), args.scan_reps, device,
                              mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device),
                              dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))
-        b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 else None
+        b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 and not args.no_b1 else None
 
     if rank == 0:
         line.update({
-            "chunk_p50_ms": round(p50_graph, 3),
-            "chunk_p50_eager_ms": round(p50_eager, 3),
+            "chunk_p50_ms": round(p50_graph, 3) if p50_graph is not None else None,
+            "chunk_p50_eager_ms": round(p50_eager, 3) if p50_eager is not None else None,
             "chunk_p50_batch": 1, "chunk_p50_mode": "hipGraph replay (StreamingChunkGraph)",
             "roofline": roof,
         })

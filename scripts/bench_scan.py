@@ -19,11 +19,13 @@ ap.add_argument("--batches", type=int, nargs="+", default=[1, 4, 8])
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--layout", default="tm", choices=["tm", "cm"])
 ap.add_argument("--segments", type=int, default=0, help="token-major segment count (0 = auto)")
+ap.add_argument("--dtp", action="store_true",
+                help="the dt_proj-in-scan kernel (vm_selective_scan_dtproj_fwd) the bench runs")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 with options.override(scan_segments=a.segments):
     for B in a.batches:
-        r = scan_roofline(B, a.reps, dev, a.layout)
+        r = scan_roofline(B, a.reps, dev, a.layout, dtp=a.dtp)
         r["segments"] = a.segments
         r["us_per_clip_layer"] = round(r["avg_us"] / B, 2)
         print(json.dumps(r), flush=True)

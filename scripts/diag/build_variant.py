@@ -54,9 +54,8 @@ VARIANTS = {
                    "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch && tok0 < 0)")],
     # dt_proj-in-scan kernel (scan_seq_dtp_kernel) pricing (results wrong): no dt block
     # (dtp_nodt), no per-quad LDS reads of dt (dtp_noquad)
-    "dtp_nodt": [("vm_scan_seq.hip", """    if (j == 14) {
-      dt_block(afn);""", """    if (j == 14) {
-      if (tg < 0) dt_block(afn);""")],
+    "dtp_nodt": [("vm_scan_seq.hip", """    if (j == 12) dt_store();""",
+                  """    if (j == 12 && tg < 0) dt_store();""")],
     "dtp_noquad": [("vm_scan_seq.hip", """    if ((j & 3) == 0 && j < 12) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);""",
                     """    if ((j & 3) == 0 && j < 12 && tg < 0) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);""")],
     # timing probe: every step reads the segment's first B/C row (L1/K$-resident), so the

@@ -7,8 +7,9 @@
 # profile.  PART=1: bench + its profile; PART=2: the rest (one gpurun call each).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-R=${ROUND:-r02}
-B=${BATCH:-336}
+R=${ROUND:-r03}
+B=${BATCH:-448}
+DTP=${DTP:---dtp}
 O=gpurun_out/$R
 mkdir -p $O
 if [ "${PART:-1}" = 1 ]; then
@@ -18,10 +19,10 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 echo part 1 done
 exit 0
 fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_scan -o scan -- python scripts/bench_scan.py --batches $B --reps 20 > $O/prof_scan.log 2>&1 || { echo scan prof failed; tail $O/prof_scan.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_scan -o scan -- python scripts/bench_scan.py --batches $B --reps 20 $DTP > $O/prof_scan.log 2>&1 || { echo scan prof failed; tail $O/prof_scan.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
   tag=$(echo $c | cut -d' ' -f1)
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$tag -o scan -- python scripts/bench_scan.py --batches $B --reps 3 > $O/pmc_$tag.log 2>&1 || { echo pmc $c failed; tail $O/pmc_$tag.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$tag -o scan -- python scripts/bench_scan.py --batches $B --reps 3 $DTP > $O/pmc_$tag.log 2>&1 || { echo pmc $c failed; tail $O/pmc_$tag.log; exit 1; }
 done
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/calib_$c -o calib -- ./tools/probes/scan_lab $B 2 3137 calib > $O/calib_$c.log 2>&1 || { echo calib $c failed; tail $O/calib_$c.log; exit 1; }

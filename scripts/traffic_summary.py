@@ -42,7 +42,7 @@ calib_read = 3.0 * batch * Lp * D * e
 calib_write = 1.0 * batch * Lp * D * e
 cf = per_dispatch("calib_FETCH_SIZE", "stream_kernel").get("FETCH_SIZE")
 cw = per_dispatch("calib_WRITE_SIZE", "stream_kernel").get("WRITE_SIZE")
-out = {"kernel": f"vm::{kname}<bf16> (token-major, B/C as scalar loads)",
+out = {"kernel": f"vm::{kname}" + ("" if "dtp" in kname else "<bf16>") + " (token-major, B/C as scalar loads)",
        "shape": f"B={batch} D={D} L={L} N={N} bf16, stateful",
        "fetch_size_bytes_raw": fetch, "write_size_bytes_raw": write,
        "algorithmic_bytes_per_launch": algo, "round": rnd}

@@ -86,21 +86,21 @@ def test_bench_control_flow_world2_weak_scaling():
     slowest rank's (rank 1 sleeps 4 ms per step), one JSON line from rank 0."""
     line = _bench_stub([])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["config"]["per_gpu_batch"] == 336 and line["config"]["global_batch"] == 672
+    assert line["config"]["per_gpu_batch"] == 448 and line["config"]["global_batch"] == 896
     assert line["ms_per_step"] >= 4.0  # the slower rank sets the step time
-    want = 672 * 16 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
+    want = 896 * 16 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
     assert abs(line["value"] - want) / want < 1e-3
     assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
 
 
-def test_bench_control_flow_world2_m32_default_is_weak_336_per_rank():
-    """C4 (--config m32) without --global-batch keeps 336 clips per rank (the batch where
+def test_bench_control_flow_world2_m32_default_is_weak_448_per_rank():
+    """C4 (--config m32) without --global-batch keeps 448 clips per rank (the batch where
     the scan holds its occupancy; 84 per GPU at N = 8 from a fixed 672 would have measured
-    the batch choice, not the sharding): weak scaling, global batch = world x 336, and the
+    the batch choice, not the sharding): weak scaling, global batch = world x 448, and the
     metric names the workload actually run."""
     line = _bench_stub(["--config", "m32"])
     assert line["scaling"] == "weak"
-    assert line["config"]["per_gpu_batch"] == 336 and line["config"]["global_batch"] == 672
+    assert line["config"]["per_gpu_batch"] == 448 and line["config"]["global_batch"] == 896
     assert line["metric"].endswith("VideoMamba-M 32f 224")
     assert _bench_stub(["--config", "ti8"])["metric"].endswith("VideoMamba-Ti 8f 224")
 

@@ -604,20 +604,29 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
       af[ks] = uint2{v[0], v[1]};
     }
   };
-  auto dt_block = [&](const uint2 (&af)[NKS]) {
+  // in stages, so no step waits on a dependent MFMA / LDS chain: the MFMAs of channel
+  // tiles [t0, t1) into dacc, later the bf16 pack + LDS store of all four tiles
+  dtp_f4 dacc[4];
+  auto dt_mfma = [&](const uint2 (&af)[NKS], const int t0, const int t1) {
 #pragma unroll
-    for (int tile = 0; tile < 4; ++tile) {
-      dtp_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int tile = t0; tile < t1; ++tile) {
+      dacc[tile] = dtp_f4{0.0f, 0.0f, 0.0f, 0.0f};
       const bf16_t* wb = &sW[wave][(16 * tile + (lane & 15)) * KP + 4 * (lane >> 4)];
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const uint2 bw = *reinterpret_cast<const uint2*>(wb + 16 * ks);
-        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(
-            __builtin_bit_cast(dtp_s4, af[ks]), __builtin_bit_cast(dtp_s4, bw), acc, 0, 0, 0);
+        dacc[tile] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(
+            __builtin_bit_cast(dtp_s4, af[ks]), __builtin_bit_cast(dtp_s4, bw), dacc[tile], 0,
+            0, 0);
       }
+    }
+  };
+  auto dt_store = [&]() {
+#pragma unroll
+    for (int tile = 0; tile < 4; ++tile) {
       // D[4 (lane>>4) + i][lane & 15] -> channel 16 tile + (lane & 15), steps 4 (lane>>4) + i
-      const uint32_t p01 = cvt_pk_bf16(acc[0], acc[1]);
-      const uint32_t p23 = cvt_pk_bf16(acc[2], acc[3]);
+      const uint32_t p01 = cvt_pk_bf16(dacc[tile][0], dacc[tile][1]);
+      const uint32_t p23 = cvt_pk_bf16(dacc[tile][2], dacc[tile][3]);
       *reinterpret_cast<uint2*>(&sD[wave][(16 * tile + (lane & 15)) * kDtRow + 2 * (lane >> 4)]) =
           uint2{p01, p23};
     }
@@ -644,7 +653,8 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   a_load(0, af);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();  // sW is written (each wave reads only its own rows; one barrier is cheap)
-  dt_block(af);
+  dt_mfma(af, 0, 4);
+  dt_store();
   uint2 dqa[4];  // the block's four quads (steps 4k .. 4k+3), each read a quad ahead
   dqa[0] = dq_read(0);
   dqa[1] = dqa[2] = dqa[3] = dqa[0];
@@ -706,15 +716,17 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     bstore<T>(from_f32<T>(y), orr, live ? voff : kSeqDead, t * os);
   };
   // block bookkeeping in step j of the block starting at tg: prefetch the next block's
-  // A fragments at j == 0, the next quad at j % 4 == 0, the next block's dt at j == 14
+  // A fragments at j == 0, the next quad at j % 4 == 0 (j < 12); the next block's dt: the
+  // MFMAs at j == 9 / 10, the pack + LDS store at j == 12 (after the last quad read of this
+  // block, j == 8), its first quad read at j == 14 (consumed from step 15 on)
   uint2 afn[NKS];
   auto around = [&](const int tg, const int j) {
     if (j == 0) a_load(tg + kDtG, afn);
     if ((j & 3) == 0 && j < 12) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);
-    if (j == 14) {
-      dt_block(afn);         // every read of this block's LDS rows has been issued
-      dqa[0] = dq_read(0);  // the next block's first quad, consumed from step 15 on
-    }
+    if (j == 9) dt_mfma(afn, 0, 2);
+    if (j == 10) dt_mfma(afn, 2, 4);
+    if (j == 12) dt_store();
+    if (j == 14) dqa[0] = dq_read(0);
   };
 
   int t0 = 0;
