@@ -29,6 +29,8 @@
  *                                 LayerNorm (videomamba.py:983-1062, :702-751 masked)
  *   vm_linear_fwd              <- the mixer's in_proj / out_proj nn.Linear at one clip's
  *                                 token count (mamba_simple.py:333-339, :445-446)
+ *   vm_linear_add_norm_fwd     <- out_proj + the next Block's fused add + RMSNorm
+ *                                 (mamba_simple.py:445-446, videomamba.py:141-166)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
  *                                 (videomamba.py:359-368, :806-815)
  *
@@ -343,6 +345,24 @@ int vm_pool_finish_fwd(const void* workspace, int batch, int groups, int group_r
 int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
                   const float* bias, void* out, long long ldo, int m, int n, int k, int dtype,
                   vm_stream_t stream);
+
+/*
+ * out_proj fused with the NEXT block's residual add + RMSNorm (mamba_simple.py:445-446, then
+ * videomamba.py:141-166 with fused_add_norm, rms_norm, residual_in_fp32):
+ *   h = bf16(x @ w^T);  residual += h (fp32, in place);  hn = bf16(rmsnorm(residual) * nw)
+ * with vm_add_norm_fwd's exact arithmetic (bit-identical to vm_linear_fwd + vm_add_norm_fwd).
+ * x (m, k), w (n, k), h (m, n), hn (m, n) bf16; residual (m, n) fp32; norm_weight (n) fp32.
+ * Each 16-row granule is normalised by the workgroup whose hand-off counter add comes last
+ * (agent-coherent h stores / loads, no spin, no co-residency assumption).  `counters`:
+ * vm_linear_add_norm_counter_bytes(m) zeroed bytes, left zeroed; one buffer must not serve
+ * two launches that can run at the same time.  n % 8 == 0, n <= 1024, k as vm_linear_fwd.
+ */
+long long vm_linear_add_norm_counter_bytes(int m);
+int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* w, long long ldw,
+                           void* h, long long ldo, float* residual, long long ldr,
+                           const float* norm_weight, float eps, void* hn, long long ldh,
+                           int m, int n, int k, void* counters, long long counter_bytes,
+                           vm_stream_t stream);
 
 /*
  * Tubelet patch embed + positional embeddings (Conv3d with kernel = stride = (kt,Ph,Pw);

@@ -58,6 +58,22 @@ VARIANTS = {
                   """    if (j == 12 && tg < 0) dt_store();""")],
     "dtp_noquad": [("vm_scan_seq.hip", """    if ((j & 3) == 0 && j < 12) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);""",
                     """    if ((j & 3) == 0 && j < 12 && tg < 0) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);""")],
+    # small-M GEMM with an unpadded 64-element LDS row and the 16-byte chunks XOR-swizzled
+    # by (row & 7) instead of the 72-element padded pitch
+    "lin_swz": [("vm_gemm.hip", "constexpr int kLinPitch = 72;  // bf16 per staged row: 64 + 8 pad (144 B)",
+                 "constexpr int kLinPitch = 64;  // bf16 per staged row, 16-B chunks XOR-swizzled"),
+                ("vm_gemm.hip", "      *reinterpret_cast<i32x4_t*>(&sA[(pc / KQ) * PITCH + (pc % KQ) * 8]) = a[i];",
+                 "      *reinterpret_cast<i32x4_t*>(&sA[(pc / KQ) * PITCH + (((pc % KQ) ^ ((pc / KQ) & 7)) * 8)]) = a[i];"),
+                ("vm_gemm.hip", "      *reinterpret_cast<i32x4_t*>(&sB[(pc / KQ) * PITCH + (pc % KQ) * 8]) = b[i];",
+                 "      *reinterpret_cast<i32x4_t*>(&sB[(pc / KQ) * PITCH + (((pc % KQ) ^ ((pc / KQ) & 7)) * 8)]) = b[i];"),
+                ("vm_gemm.hip", """        af[i] = *reinterpret_cast<const bf16x8_t*>(
+            &sA[(wm * WM + i * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);""",
+                 """        af[i] = *reinterpret_cast<const bf16x8_t*>(
+            &sA[(wm * WM + i * 16 + (lane & 15)) * PITCH + (((ks * 4 + (lane >> 4)) ^ (lane & 7)) * 8)]);"""),
+                ("vm_gemm.hip", """        bw[j] = *reinterpret_cast<const bf16x8_t*>(
+            &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);""",
+                 """        bw[j] = *reinterpret_cast<const bf16x8_t*>(
+            &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + (((ks * 4 + (lane >> 4)) ^ (lane & 7)) * 8)]);""")],
     # timing probe: every step reads the segment's first B/C row (L1/K$-resident), so the
     # chunk kernel's time without the per-step scalar-load latency shows (results wrong)
     "bc_fixed": [("vm_scan_seq.hip",

@@ -22,5 +22,8 @@ for tag, m, n, k in [("in_proj", 3144, 2304, 576), ("out_proj", 3144, 576, 1152)
     x = torch.randn(m, k, device=dev).to(torch.bfloat16)
     w = torch.randn(n, k, device=dev).to(torch.bfloat16)
     out[tag + "_hip_us"] = round(_event_us(lambda: K.linear(x, w), 50), 2)
+    ref = (x.float() @ w.float().t())
+    err = ((K.linear(x, w).float() - ref).abs().max() / ref.abs().max()).item()
+    out[tag + "_maxrel"] = float(f"{err:.2e}")
     out[tag + "_lib_us"] = round(_event_us(lambda: F.linear(x, w), 50), 2)
 print(json.dumps(out), flush=True)

@@ -791,6 +791,33 @@ def test_c3_m_16f_bf16_bench_kernels_match_oracle():
     torch.testing.assert_close(xv[:1].float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("bsz", [1, 3])
+def test_fused_out_proj_norm_is_bitwise_the_unfused_model(bsz):
+    """options.fuse_out_norm (out_proj + the next block's add + RMSNorm in one kernel,
+    vm_linear_add_norm_fwd) changes no bit of the model: VideoMamba-M 16x224^2 bf16 stateful
+    chunk at B = 1 and 3 (the streaming batches whose out_proj runs on the HIP GEMM), and the
+    hipGraph replay of the B = 1 chunk equals the eager call."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    model = _m_model(16, add_pool_norm=True)
+    model.pool_type = "cls+avg"
+    g = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.randn(bsz, 3, 16, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+    outs = {}
+    for fuse in (False, True):
+        st = model.allocate_state(bsz, dtype=torch.bfloat16, device=DEV)
+        with options.override(fuse_out_norm=fuse), torch.no_grad():
+            xv, xp, st = model(x, ssm_state=st, temporal_pos_offset=0)
+        outs[fuse] = (xv, xp, [s for _, s in st])
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+    assert all(torch.equal(a, b) for a, b in zip(outs[True][2], outs[False][2]))
+    if bsz == 1:
+        runner = StreamingChunkGraph(model, batch=1, frames=16)
+        with torch.no_grad():
+            gv, gp = runner.run(x, temporal_pos_offset=0)
+        assert torch.equal(gv, outs[True][0]) and torch.equal(gp, outs[True][1])
+
+
 def test_c5_long_video_chunk64_streaming_matches_full():
     """C5 at reduced chunk count: VideoMamba-M built with num_frames=1024 (so the temporal
     embedding is sliced, never interpolated: SURVEY F7), 4 x chunk64 streamed with a

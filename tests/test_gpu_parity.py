@@ -806,3 +806,32 @@ def test_b1_mixer_projections_run_on_the_hip_gemm():
             y_lib = m(x)
     rel = ((y_hip.float() - y_lib.float()).norm() / y_lib.float().norm()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("m,n,k", [(3144, 576, 1152), (100, 192, 384), (1, 576, 1152),
+                                   (6288, 576, 1152), (37, 384, 768), (12552, 576, 1152)])
+def test_linear_add_norm_bitwise_equals_linear_then_add_norm(m, n, k):
+    """vm_linear_add_norm_fwd (out_proj with the next block's residual add + RMSNorm run by
+    the last column tile of each 16-row granule) == vm_linear_fwd followed by
+    vm_add_norm_fwd, bit for bit (h, the updated fp32 residual, the normalised rows); the
+    hand-off counters come back zeroed, so a second launch on the same buffer is exact too."""
+    torch.manual_seed(m + n)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device=DEV)
+    nw = torch.rand(n, device=DEV) + 0.5
+    h_ref = K.linear(x, w)
+    res_ref = res0.clone()
+    hn_ref = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    K.add_norm_raw(h_ref, res_ref, nw, None, hn_ref, res_ref, m, n, 1e-5, True,
+                   torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):
+        res = res0.clone()
+        hn = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+        h = K.linear_add_norm(x, w, res, nw, 1e-5, hn)
+        torch.cuda.synchronize()
+        assert torch.equal(h, h_ref)
+        assert torch.equal(res, res_ref)
+        assert torch.equal(hn, hn_ref)
+    cnt = K.counter_buffer(x.device, torch.cuda.current_stream().cuda_stream, 0)
+    assert not cnt.any()

@@ -106,6 +106,12 @@ _SIGNATURES = {
          _P, _I, _LL, _I, _I,                     # cls, dtype, stride, mode, keep_temporal
          _P, _P, c_float, _P, _I, _I, _P], _I),   # LN w / b / eps, x_pool, dtype, cols
     "vm_linear_fwd": ([_P, _LL, _P, _LL, _P, _P, _LL, _I, _I, _I, _I, _P], _I),
+    "vm_linear_add_norm_fwd": (
+        [_P, _LL, _P, _LL,                        # x, ldx, w, ldw
+         _P, _LL, _P, _LL,                        # h (out), ldo, residual (fp32), ldr
+         _P, c_float, _P, _LL,                    # norm weight, eps, hn, ldh
+         _I, _I, _I, _P, _LL, _P], _I),           # m, n, k, counters, bytes, stream
+    "vm_linear_add_norm_counter_bytes": ([_I], _LL),
     "vm_patch_embed_fwd": (
         [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
 }

@@ -27,12 +27,39 @@ struct LinParams {
   int m, n, k;
 };
 
+// Fused residual add + RMSNorm of the NEXT block (videomamba.py:141-166 with
+// fused_add_norm / rms_norm / residual_in_fp32): after the GEMM, out (= h, the block's
+// output rounded to bf16) is complete for a 16-row granule once every column tile of the
+// grid has stored its part; the workgroup whose counter add comes last normalises the
+// granule:  res += h (fp32, in place);  hn = bf16(res * rsqrt(mean(res^2) + eps) * w).
+// Hand-off (MI355X_MICROARCH.md cross-workgroup table, row 1): every h store is sc1, each
+// storing wave waits vmcnt(0), a workgroup barrier, then ONE lane per granule adds to the
+// granule's counter (agent-scope atomic); the last adder's waves read h with sc1 loads after
+// a barrier.  The last adder also resets the counter, so the buffer is zero after a launch.
+struct NormTail {
+  float* res;         // (m, n) fp32, row stride ldr: read and updated in place
+  long long ldr;
+  const float* w;     // (n) fp32 norm weight
+  bf16_t* hn;         // (m, n) bf16 normalised output, row stride ldh
+  long long ldh;
+  float eps;
+  unsigned* cnt;      // ceil(m / 16) zeroed counters
+};
+constexpr int kNormGran = 16;  // rows per hand-off granule
+constexpr int kSC1 = 16;       // buffer cache-policy bit: sc1 (agent-coherent)
+
+__device__ __forceinline__ float lin_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 constexpr int kLinBN = 128;
 constexpr int kLinBK = 64;
 constexpr int kLinPitch = 72;  // bf16 per staged row: 64 + 8 pad (144 B)
 
-template <int BM, int NK>  // NK = k / 64 K-steps, fully unrolled (straight-line prefetch)
-__global__ __launch_bounds__(256) void linear_kernel(const LinParams p) {
+template <int BM, int NK, bool NORM = false>  // NK = k / 64 K-steps, fully unrolled
+__global__ __launch_bounds__(256) void linear_kernel(const LinParams p, const NormTail q) {
   constexpr int BN = kLinBN, BK = kLinBK, PITCH = kLinPitch;
   constexpr int WM = BM / 2, WN = BN / 2;  // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -167,13 +194,92 @@ __global__ __launch_bounds__(256) void linear_kernel(const LinParams p) {
     }
   __syncthreads();
   constexpr int kPieces = BM * BN / 8;
+  const auto hr = __builtin_amdgcn_make_buffer_rsrc(
+      p.out, 0, static_cast<int>((long long)p.m * p.ldo * 2), 0x00020000);
 #pragma unroll
   for (int i = 0; i < kPieces / 256; ++i) {
     const int pc = tid + 256 * i, row = pc / (BN / 8), cq = pc % (BN / 8);
     const int gm = m0 + row, gn = n0 + cq * 8;
-    if (gm < p.m && gn < p.n)
-      *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) =
-          *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+    if (gm < p.m && gn < p.n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+      if constexpr (NORM) {  // agent-coherent: another workgroup normalises these rows
+        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+        __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, hr,
+                                               (gm * static_cast<int>(p.ldo) + gn) * 2, 0, kSC1);
+      } else {
+        *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) = v;
+      }
+    }
+  }
+  if constexpr (NORM) {
+    // ---- hand-off: the last column tile of a 16-row granule normalises it ----
+    __shared__ int s_last[BM / kNormGran];
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's h stores are acknowledged
+    __syncthreads();
+    const int ntn = (p.n + BN - 1) / BN;
+    if (tid < BM / kNormGran) {
+      const int g = m0 / kNormGran + tid;
+      int last = 0;
+      if (g * kNormGran < p.m) {
+        const unsigned old =
+            __hip_atomic_fetch_add(&q.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == static_cast<unsigned>(ntn - 1);
+        if (last) __hip_atomic_store(&q.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_last[tid] = last;
+    }
+    __syncthreads();
+    // per row: vm_add_norm_fwd's RMS arithmetic and lane -> chunk map (lane*4 + 256*j), so
+    // the fused result is bit-identical to out_proj followed by vm_add_norm_fwd
+    constexpr int CPL = 4;  // n <= 1024
+#pragma unroll 1
+    for (int gi = 0; gi < BM / kNormGran; ++gi) {
+      if (!s_last[gi]) continue;
+#pragma unroll 1
+      for (int rr = 0; rr < kNormGran / 4; ++rr) {
+        const int gm = m0 + gi * kNormGran + wave * (kNormGran / 4) + rr;
+        if (gm >= p.m) break;
+        float v[CPL][4];
+        float* rrow = q.res + (long long)gm * q.ldr;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = lane * 4 + 256 * j;
+          if (c < p.n) {
+            const auto hv = __builtin_amdgcn_raw_buffer_load_b64(
+                hr, (gm * static_cast<int>(p.ldo) + c) * 2, 0, kSC1);
+            const float4 r = *reinterpret_cast<const float4*>(rrow + c);
+            v[j][0] = __uint_as_float(hv[0] << 16) + r.x;
+            v[j][1] = __uint_as_float(hv[0] & 0xffff0000u) + r.y;
+            v[j][2] = __uint_as_float(hv[1] << 16) + r.z;
+            v[j][3] = __uint_as_float(hv[1] & 0xffff0000u) + r.w;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[j][i] = 0.0f;
+          }
+        }
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
+        const float rstd = rsqrtf(lin_wave_sum(sq) / p.n + q.eps);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = lane * 4 + 256 * j;
+          if (c < p.n) {
+            const float4 w = *reinterpret_cast<const float4*>(q.w + c);
+            const float y0 = (v[j][0] - 0.0f) * rstd * w.x, y1 = (v[j][1] - 0.0f) * rstd * w.y;
+            const float y2 = (v[j][2] - 0.0f) * rstd * w.z, y3 = (v[j][3] - 0.0f) * rstd * w.w;
+            *reinterpret_cast<uint2*>(q.hn + (long long)gm * q.ldh + c) = uint2{
+                static_cast<uint32_t>(from_f32<bf16_t>(y0)) |
+                    (static_cast<uint32_t>(from_f32<bf16_t>(y1)) << 16),
+                static_cast<uint32_t>(from_f32<bf16_t>(y2)) |
+                    (static_cast<uint32_t>(from_f32<bf16_t>(y3)) << 16)};
+            *reinterpret_cast<float4*>(rrow + c) = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+          }
+        }
+      }
+    }
   }
 }
 
@@ -203,17 +309,18 @@ extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long l
   p.bias = bias; p.out = static_cast<bf16_t*>(out); p.ldo = ldo;
   p.m = m; p.n = n; p.k = k;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int nt = (n + kLinBN - 1) / kLinBN;
+  const NormTail nt{};
+  const int ntn = (n + kLinBN - 1) / kLinBN;
   // 128-row tiles when that still gives >= 1.5 workgroups per CU (256 CUs), else 64-row
-  const bool big = (long long)((m + 127) / 128) * nt >= 384;
+  const bool big = (long long)((m + 127) / 128) * ntn >= 384;
   const int bm = big ? 128 : 64;
-  const dim3 grid((m + bm - 1) / bm, nt);
+  const dim3 grid((m + bm - 1) / bm, ntn);
   const size_t lds = 2 * (bm + kLinBN) * kLinPitch * sizeof(bf16_t);
   switch (k / kLinBK) {
-#define VM_LIN(NKV)                                                                  \
-  case NKV:                                                                          \
-    if (big) hipLaunchKernelGGL((linear_kernel<128, NKV>), grid, dim3(256), lds, s, p); \
-    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p);    \
+#define VM_LIN(NKV)                                                                       \
+  case NKV:                                                                               \
+    if (big) hipLaunchKernelGGL((linear_kernel<128, NKV>), grid, dim3(256), lds, s, p, nt); \
+    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p, nt);    \
     break;
     VM_LIN(3) VM_LIN(6) VM_LIN(9) VM_LIN(12) VM_LIN(18) VM_LIN(24)
 #undef VM_LIN
@@ -222,4 +329,56 @@ extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long l
       return VM_E_INVALID;
   }
   return vmhost::launch_status("vm_linear_fwd");
+}
+
+extern "C" long long vm_linear_add_norm_counter_bytes(int m) {
+  return m <= 0 ? 0 : static_cast<long long>((m + kNormGran - 1) / kNormGran) * sizeof(unsigned);
+}
+
+extern "C" int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* w, long long ldw,
+                                      void* h, long long ldo, float* residual, long long ldr,
+                                      const float* norm_weight, float eps, void* hn, long long ldh,
+                                      int m, int n, int k, void* counters,
+                                      long long counter_bytes, vm_stream_t stream) {
+  if (!x || !w || !h || !residual || !norm_weight || !hn || !counters) {
+    vmhost::set_error("vm_linear_add_norm_fwd: null required pointer");
+    return VM_E_INVALID;
+  }
+  if (m < 0 || n < 4 || n > 1024 || n % 8 || k < kLinBK || k % kLinBK || ldx < k || ldw < k ||
+      ldo < n || ldr < n || ldh < n || ldx % 8 || ldw % 8 || ldo % 8 || ldr % 4 || ldh % 4 ||
+      !vmhost::aligned16(x) || !vmhost::aligned16(w) || !vmhost::aligned16(h) ||
+      !vmhost::aligned16(residual) || !vmhost::aligned16(norm_weight) || !vmhost::aligned16(hn) ||
+      (long long)m * ldx * 2 >= (1ll << 31) || (long long)n * ldw * 2 >= (1ll << 31) ||
+      (long long)m * ldo * 2 >= (1ll << 31) ||
+      counter_bytes < vm_linear_add_norm_counter_bytes(m)) {
+    vmhost::set_error("vm_linear_add_norm_fwd: bf16 x / w / h / hn, fp32 residual and weight; "
+                      "k a multiple of 64, n a multiple of 8 and <= 1024, 16-byte aligned "
+                      "rows under 2 GB, vm_linear_add_norm_counter_bytes(m) zeroed counters");
+    return VM_E_INVALID;
+  }
+  if (m == 0) return VM_OK;
+  LinParams p{};
+  p.x = static_cast<const bf16_t*>(x); p.ldx = ldx;
+  p.w = static_cast<const bf16_t*>(w); p.ldw = ldw;
+  p.bias = nullptr; p.out = static_cast<bf16_t*>(h); p.ldo = ldo;
+  p.m = m; p.n = n; p.k = k;
+  NormTail q{};
+  q.res = residual; q.ldr = ldr; q.w = norm_weight; q.hn = static_cast<bf16_t*>(hn); q.ldh = ldh;
+  q.eps = eps; q.cnt = static_cast<unsigned*>(counters);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid((m + 63) / 64, (n + kLinBN - 1) / kLinBN);
+  const size_t lds = 2 * (64 + kLinBN) * kLinPitch * sizeof(bf16_t);
+  switch (k / kLinBK) {
+#define VM_LIN(NKV)                                                                   \
+  case NKV:                                                                           \
+    hipLaunchKernelGGL((linear_kernel<64, NKV, true>), grid, dim3(256), lds, s, p, q); \
+    break;
+    VM_LIN(3) VM_LIN(6) VM_LIN(9) VM_LIN(12) VM_LIN(18) VM_LIN(24)
+#undef VM_LIN
+    default:
+      vmhost::set_error("vm_linear_add_norm_fwd: k = %d (supported: 192, 384, 576, 768, 1152, "
+                        "1536)", k);
+      return VM_E_INVALID;
+  }
+  return vmhost::launch_status("vm_linear_add_norm_fwd");
 }

@@ -94,6 +94,7 @@ class StreamingChunkGraph:
         self._tpos_offset = None  # temporal offset whose embedding slice static_tpos holds
         self._ws = None  # scan scratch owned by the captured graphs
         self._sync = None  # the one-launch scan's sync flags (zeroed; replays leave them zeroed)
+        self._cnt = None  # vm_linear_add_norm_fwd hand-off counters (zeroed, left zeroed)
 
     # ------------------------------------------------------------------ state
     @property
@@ -156,6 +157,10 @@ class StreamingChunkGraph:
         # the one-launch scan's sync flags: zeroed once, left zeroed by every replay
         if self._sync is None or self._sync.numel() < max(sync_need, 1):
             self._sync = torch.zeros(max(sync_need, 4096), dtype=torch.uint8, device=self.device)
+        Lp = (self.tt * gh * gw + 1 + 7) // 8 * 8
+        cnt_need = K.linear_add_norm_counter_bytes(self.batch * Lp)
+        if self._cnt is None or self._cnt.numel() < max(cnt_need, 1):
+            self._cnt = torch.zeros(max(cnt_need, 4096), dtype=torch.uint8, device=self.device)
         return self._ws
 
     def check(self) -> None:
@@ -172,13 +177,13 @@ class StreamingChunkGraph:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.no_grad(), torch.cuda.stream(side), K.scratch_override(ws), \
-                K.sync_override(self._sync):
+                K.sync_override(self._sync), K.counter_override(self._cnt):
             for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
                 self._body(has_cls)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws), \
-                K.sync_override(self._sync):
+                K.sync_override(self._sync), K.counter_override(self._cnt):
             outs = self._body(has_cls)
         self._pool = g.pool()
         self.load_state(saved)  # warm-up passes advanced the state: restore it

@@ -381,6 +381,67 @@ def linear(x: Tensor, w: Tensor, b32: Optional[Tensor] = None,
     return out
 
 
+_CNT = {}
+_CNT_OVERRIDE = [None]
+
+
+class counter_override:
+    """Within the block ``vm_linear_add_norm_fwd`` takes its hand-off counters from ``buf``
+    (a zero-filled uint8 device tensor owned by the caller, e.g. a captured graph) instead
+    of the per-stream buffer.  The kernel leaves the counters zeroed."""
+
+    def __init__(self, buf: Tensor):
+        self.buf = buf
+
+    def __enter__(self):
+        self.prev = _CNT_OVERRIDE[0]
+        _CNT_OVERRIDE[0] = self.buf
+        return self.buf
+
+    def __exit__(self, *exc):
+        _CNT_OVERRIDE[0] = self.prev
+        return False
+
+
+def counter_buffer(device: torch.device, stream: int, nbytes: int) -> Tensor:
+    ov = _CNT_OVERRIDE[0]
+    if ov is not None:
+        if ov.numel() < nbytes:
+            raise RuntimeError(f"counter_override buffer too small: {ov.numel()} < {nbytes}")
+        return ov
+    key = (device.type, device.index, stream)
+    buf = _CNT.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(nbytes, 4096), dtype=torch.uint8, device=device)
+        _CNT[key] = buf
+    return buf
+
+
+def linear_add_norm_counter_bytes(m: int) -> int:
+    return int(_lib.load().vm_linear_add_norm_counter_bytes(m))
+
+
+def linear_add_norm(x: Tensor, w: Tensor, residual: Tensor, norm_w32: Tensor, eps: float,
+                    hn: Tensor, h: Optional[Tensor] = None) -> Tensor:
+    """The mixer's out_proj fused with the next block's residual add + RMSNorm
+    (``vm_linear_add_norm_fwd``): h = bf16(x @ w^T); residual += h (fp32, in place);
+    hn = bf16(rmsnorm(residual) * norm_w) — bit-identical to ``linear`` followed by
+    ``vm_add_norm_fwd``.  x (m, k), w (n, k) bf16; residual (m, n) fp32; hn (m, n) bf16.
+    Returns h (the block output, a new (m, n) bf16 tensor unless given)."""
+    m, k = x.shape
+    n = w.shape[0]
+    if h is None:
+        h = torch.empty((m, n), dtype=x.dtype, device=x.device)
+    nbytes = linear_add_norm_counter_bytes(m)
+    cnt = counter_buffer(x.device, _stream(x), nbytes)
+    rc = _lib.load().vm_linear_add_norm_fwd(
+        _p(x), x.stride(0), _p(w), w.stride(0), _p(h), h.stride(0), _p(residual),
+        residual.stride(0), _p(norm_w32), float(eps), _p(hn), hn.stride(0), m, n, k, _p(cnt),
+        cnt.numel(), _stream(x))
+    _lib.check(rc, "vm_linear_add_norm_fwd")
+    return h
+
+
 POOL_MODES = {"avg": 0, "cls+avg": 1, "cls_cat_avg": 2, "cls": 3}
 
 

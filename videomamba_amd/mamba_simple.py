@@ -223,11 +223,14 @@ class Mamba(nn.Module):
     # ------------------------------------------------------------------ core
     def _forward_padded(self, hn: Tensor, seqlen: int, *, conv_state_in: Optional[Tensor] = None,
                         conv_state_out: Optional[Tensor] = None, h0: Optional[Tensor] = None,
-                        h_last: Optional[Tensor] = None) -> Tensor:
+                        h_last: Optional[Tensor] = None, next_norm=None) -> Tensor:
         """hn: (B, Lp, C) contiguous, rows >= seqlen zero.  Returns (B, Lp, C) with rows
-        >= seqlen zero.  States are read/written by the kernels (see module doc)."""
+        >= seqlen zero.  States are read/written by the kernels (see module doc).
+        ``next_norm`` (videomamba.NextNorm): fuse the next block's add + RMSNorm into
+        out_proj when it runs on the HIP GEMM (sets ``next_norm.done``)."""
         if mixer_layout(hn.shape[0], self.d_inner, hn.device) == "tm":
-            return self._forward_padded_tm(hn, seqlen, conv_state_in, conv_state_out, h0, h_last)
+            return self._forward_padded_tm(hn, seqlen, conv_state_in, conv_state_out, h0, h_last,
+                                           next_norm)
         Bsz, Lp, C = hn.shape
         Dm, N, R, W = self.d_inner, self.d_state, self.dt_rank, self.d_conv
         n = Bsz * Lp
@@ -335,7 +338,8 @@ class Mamba(nn.Module):
                 _linear_into(x_dbl[:, :R], self.dt_proj.weight, None, dt)
         return xz, u, x_dbl, dt
 
-    def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last):
+    def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last,
+                           next_norm=None):
         """Token-major form of :meth:`_forward_padded` (same math, same rounding points)."""
         Bsz, Lp, C = hn.shape
         Dm, N, R = self.d_inner, self.d_state, self.dt_rank
@@ -359,6 +363,13 @@ class Mamba(nn.Module):
             K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                        xz[:, Dm:], s_xz, dbias, True, h0, h0_s, h_last, hl_s,
                        y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+        if (next_norm is not None and next_norm.residual is not None
+                and _small_gemm_ok(y, self.out_proj.weight, self.out_proj.bias, clips=Bsz)):
+            # out_proj + the next block's residual add + RMSNorm in one kernel
+            out = K.linear_add_norm(y, self.out_proj.weight, next_norm.residual.view(-1, C),
+                                    next_norm.w32, next_norm.eps, next_norm.hn.view(-1, C))
+            next_norm.done = True
+            return out.view(Bsz, Lp, C)
         out = _linear(y, self.out_proj.weight, self.out_proj.bias, clips=Bsz)  # (n, C)
         return out.view(Bsz, Lp, C)
 
@@ -372,7 +383,8 @@ class Mamba(nn.Module):
 
     def forward_padded(self, hn: Tensor, seqlen: int, *, ssm_state: Optional[Tensor] = None,
                        state: Optional[Tuple[Tensor, Tensor]] = None,
-                       return_state: bool = False, conv_out: Optional[Tensor] = None):
+                       return_state: bool = False, conv_out: Optional[Tensor] = None,
+                       next_norm=None):
         """Model-internal entry on the padded layout (no inference_params).  Same state
         semantics as :meth:`forward`; ``conv_out`` (B, D, d_conv) receives the new conv
         state instead of a fresh tensor (the graph runner's batched state buffers)."""
@@ -397,7 +409,7 @@ class Mamba(nn.Module):
             h_last = ssm_state if ssm_state is not None else torch.empty(
                 (Bsz, self.d_inner, self.d_state), dtype=torch.float32, device=hn.device)
         out = self._forward_padded(hn, seqlen, conv_state_in=conv_state, conv_state_out=cs_out,
-                                   h0=ssm_state, h_last=h_last)
+                                   h0=ssm_state, h_last=h_last, next_norm=next_norm)
         if return_state:
             return out, (cs_out, h_last)
         return out

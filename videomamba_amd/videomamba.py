@@ -29,6 +29,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from . import kernels as K
+from . import options
 from .layers import DropPath, RMSNorm, round_up, to_2tuple, trunc_normal_, warn_if_grad
 from .mamba_simple import InferenceParamsLike, Mamba
 from .streaming import (STREAMING_CONTRACT_VERSION, ForwardReturnSemantics, StateShape,
@@ -61,6 +62,19 @@ def _infer_spatial_grid(token_count: int, reference_grid: Tuple[int, int]) -> Tu
 def _norm_kind(norm: nn.Module) -> bool:
     """True for RMSNorm, False for LayerNorm (the two norms fused_add_norm supports)."""
     return isinstance(norm, RMSNorm)
+
+
+# ----------------------------------------------------------------------------- Block
+class NextNorm:
+    """The next block's fused add + RMSNorm, offered to a mixer's out_proj
+    (vm_linear_add_norm_fwd): the norm's fp32 weight and eps, the residual stream (updated in
+    place), the buffer for the normalised rows, and whether the out_proj did it."""
+
+    def __init__(self, w32: Tensor, eps: float):
+        self.w32, self.eps = w32, eps
+        self.residual: Optional[Tensor] = None
+        self.hn: Optional[Tensor] = None
+        self.done = False
 
 
 # ----------------------------------------------------------------------------- Block
@@ -121,11 +135,22 @@ class Block(nn.Module):
         return hidden, residual
 
     def forward_padded(self, hidden: Tensor, residual: Optional[Tensor], seqlen: int,
-                       state=None, ssm_state=None, return_state: bool = False, conv_out=None):
-        """Model-internal: same as ``forward`` on the padded (B, Lp, C) buffers."""
-        hn, residual = self._add_norm(hidden, residual, inplace=True)
+                       state=None, ssm_state=None, return_state: bool = False, conv_out=None,
+                       pre: Optional["NextNorm"] = None, next_norm: Optional["NextNorm"] = None):
+        """Model-internal: same as ``forward`` on the padded (B, Lp, C) buffers.  ``pre``: the
+        previous block's out_proj already ran this block's add + norm (``pre.done``): use its
+        normalised rows and updated residual.  ``next_norm``: offer the NEXT block's norm to
+        this block's out_proj (vm_linear_add_norm_fwd)."""
+        if pre is not None and pre.done:
+            hn, residual = pre.hn, pre.residual
+        else:
+            hn, residual = self._add_norm(hidden, residual, inplace=True)
+        if next_norm is not None:
+            next_norm.residual = residual
+            next_norm.hn = torch.empty_like(hn)
         res = self.mixer.forward_padded(hn, seqlen, ssm_state=ssm_state, state=state,
-                                        return_state=return_state, conv_out=conv_out)
+                                        return_state=return_state, conv_out=conv_out,
+                                        next_norm=next_norm)
         if return_state:
             return res[0], residual, res[1]
         return res, residual, None
@@ -432,7 +457,13 @@ class PretrainVideoMamba(nn.Module):
         ``conv_out`` (depth, B, D, d_conv) receives the new conv states (graph runner)."""
         new_states = None
         tuple_out = False
+        fuse = self._fuse_out_norm_ok(h)
+        pending = None
         for idx, layer in enumerate(self.layers):
+            nxt = None
+            if fuse and idx + 1 < len(self.layers):
+                nn_ = self.layers[idx + 1].norm
+                nxt = NextNorm(K.f32_cached(nn_, nn_.weight, "w"), nn_.eps)
             layer_state = self._get_layer_state(ssm_state, idx)
             full = isinstance(layer_state, (list, tuple)) and len(layer_state) == 2
             if full and new_states is None:
@@ -444,12 +475,31 @@ class PretrainVideoMamba(nn.Module):
             if full:
                 h, residual, layer_state = layer.forward_padded(
                     h, residual, L, state=tuple(layer_state), return_state=True,
-                    conv_out=None if conv_out is None else conv_out[idx])
+                    conv_out=None if conv_out is None else conv_out[idx], pre=pending,
+                    next_norm=nxt)
             else:
-                h, residual, _ = layer.forward_padded(h, residual, L, ssm_state=layer_state)
+                h, residual, _ = layer.forward_padded(h, residual, L, ssm_state=layer_state,
+                                                      pre=pending, next_norm=nxt)
             if new_states is not None:
                 new_states[idx] = layer_state
+            pending = nxt
         return h, residual, new_states, tuple_out
+
+    def _fuse_out_norm_ok(self, h: Tensor) -> bool:
+        """Every block's add + norm after the first may run inside the previous block's
+        out_proj (vm_linear_add_norm_fwd) when the blocks use the fused RMSNorm with an fp32
+        residual on bf16 activations and no stochastic depth is active; each mixer then
+        decides per call (its out_proj must take the row-invariant HIP GEMM)."""
+        if not options.get().fuse_out_norm or h.dtype != torch.bfloat16:
+            return False
+        C = self.embed_dim
+        if C % 8 or C > 1024:
+            return False
+        for layer in self.layers:
+            if not (layer.fused_add_norm and layer.residual_in_fp32 and _norm_kind(layer.norm)
+                    and (isinstance(layer.drop_path, nn.Identity) or not layer.training)):
+                return False
+        return True
 
     def _final_norm_pool(self, h, residual, L, has_cls, visible, pool):
         """Final add + norm of the padded buffer straight into contiguous (B, L, C)
