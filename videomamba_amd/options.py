@@ -30,9 +30,12 @@ documented options object; tests and sweeps change them with :func:`override`.
                      run in_proj / out_proj on the HIP GEMM at every token count, whose rows
                      do not depend on the row count — chunked streaming == the one-pass
                      forward bit for bit; 0: only the small_gemm_* rule below.
-    fuse_out_norm    True (default): with bf16 fused RMSNorm blocks, a mixer whose out_proj
-                     runs on the HIP GEMM also runs the next block's residual add + RMSNorm
-                     (vm_linear_add_norm_fwd; bit-identical to the separate kernels).
+    fuse_out_norm    False (default): True makes a mixer whose out_proj runs on the HIP GEMM
+                     (bf16 fused RMSNorm blocks) also run the next block's residual add +
+                     RMSNorm (vm_linear_add_norm_fwd; bit-identical to the separate kernels).
+                     Measured slower at B = 1 (48 vs 10.9 + 6.9 us per layer: the granule's
+                     last workgroup reads the other tiles' rows back from beyond L2), so it
+                     is off by default.
     small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -64,7 +67,7 @@ class Options:
     scan_dt_proj: str = "auto"
     gemm_tuning: str = "on"
     row_invariant_gemm_clips: int = 8
-    fuse_out_norm: bool = True
+    fuse_out_norm: bool = False
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
 
