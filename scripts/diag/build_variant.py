@@ -74,6 +74,77 @@ VARIANTS = {
             &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);""",
                  """        bw[j] = *reinterpret_cast<const bf16x8_t*>(
             &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + (((ks * 4 + (lane >> 4)) ^ (lane & 7)) * 8)]);""")],
+    # small-M GEMM: the register-ring kernel instead of the LDS-DMA pipelined form
+    "ldma_old": [("vm_gemm.hip", "constexpr bool kLinearDma = true;", "constexpr bool kLinearDma = false;")],
+    # LDS-DMA GEMM tile / depth alternatives: 128x128 with three stage buffers (one
+    # workgroup per CU); narrow outputs on 128x64 tiles with three buffers
+    "ldma3": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
+               "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 3)")],
+    "ldma_o64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3)",
+                  "  else VM_LDMA_TILE(64, 64, 3)")],
+    "ldma_o2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3)",
+                 "  else VM_LDMA_TILE(64, 64, 2)")],
+    # one-launch chunked scan: the preceding blocks' flags polled one after another by
+    # thread 0 (the round-2 form) instead of in parallel by wave 0
+    "poll_serial": [("vm_scan_seq.hip", "        for (int j = lane; j < blk; j += 64)",
+                     "        for (int j = 0; lane == 0 && j < blk; ++j)")],
+    # fused small-batch conv_proj with full __syncthreads() (vmcnt(0) drains) at its barriers
+    "cp_sync": [("vm_conv_proj_sk.hip", """__device__ __forceinline__ void fu_lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();""", """__device__ __forceinline__ void fu_lds_barrier() {
+  __syncthreads();""")],
+    # phase timestamps of the fused small-batch conv_proj (s_memrealtime, 100 MHz) per
+    # workgroup into a device array read back by vm_dbg_read_stamps
+    # (scripts/diag/stamp_conv_proj.py); results unchanged
+    "cp_stamp": [
+        ("vm_conv_proj_sk.hip", "template <int NB>  // NB = e_pad / 16 x_proj column blocks",
+         "__device__ unsigned long long vm_dbg_stamps[4096 * 8];\n"
+         "#define VM_STAMP(K) __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0) vm_dbg_stamps[blockIdx.x * 8 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
+         "template <int NB>  // NB = e_pad / 16 x_proj column blocks"),
+        ("vm_conv_proj_sk.hip", "  const int ntok = q.ntok;\n\n  // ---- one round of loads ----",
+         "  const int ntok = q.ntok;\n  VM_STAMP(0)\n\n  // ---- one round of loads ----"),
+        ("vm_conv_proj_sk.hip", "  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----",
+         "  VM_STAMP(1)\n  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----"),
+        ("vm_conv_proj_sk.hip", "  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials",
+         "  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials\n  VM_STAMP(2)"),
+        ("vm_conv_proj_sk.hip", "  if (!do_dt) return;\n  fu_lds_barrier();\n  // ---- dt for channels",
+         "  VM_STAMP(3)\n  if (!do_dt) return;\n  fu_lds_barrier();\n  // ---- dt for channels"),
+        ("vm_conv_proj_sk.hip", "  fu_lds_barrier();\n  // 16 token rows x dim channels out, 16 B per lane-store",
+         "  fu_lds_barrier();\n  VM_STAMP(4)\n  // 16 token rows x dim channels out, 16 B per lane-store"),
+        ("vm_conv_proj_sk.hip", "          *reinterpret_cast<const uint4*>(&sDT[t * dtp + qd * 8]);\n  }\n}",
+         "          *reinterpret_cast<const uint4*>(&sDT[t * dtp + qd * 8]);\n  }\n  __builtin_amdgcn_s_waitcnt(0);\n  __syncthreads();\n  VM_STAMP(5)\n}"),
+        ("vm_conv_proj_sk.hip", "bool conv_proj_fused_ok(const ConvProjTmArgs& a) {",
+         "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
+         "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
+         "namespace vm {\nbool conv_proj_fused_ok(const ConvProjTmArgs& a) {"),
+    ],
+    # phase timestamps of the one-launch chunked scan (PASS 3) per workgroup: entry (0),
+    # start-up loads landed (1), PASS 1 steps done (2), aggregate published (3), preceding
+    # flags seen (4), entry state composed (5), PASS 2 done and drained (6)
+    # (scripts/diag/stamp_scan.py); results unchanged
+    "sc_stamp": [
+        ("vm_scan_seq.hip", "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>\n__global__ __launch_bounds__(64 * kChW)",
+         "__device__ unsigned long long vm_dbg_stamps[4096 * 8];\n"
+         "#define VM_STAMP(K) __builtin_amdgcn_sched_barrier(0); if (PASS == 3 && threadIdx.x == 0) vm_dbg_stamps[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
+         "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>\n__global__ __launch_bounds__(64 * kChW)"),
+        ("vm_scan_seq.hip", "  const int nch = min(64, p.dim - d0);  // live channels of this group\n",
+         "  const int nch = min(64, p.dim - d0);  // live channels of this group\n  VM_STAMP(0)\n"),
+        ("vm_scan_seq.hip", "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n",
+         "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n  VM_STAMP(1)\n"),
+        ("vm_scan_seq.hip", "  run_steps(BoolTag<false>{});\n#pragma unroll\n",
+         "  run_steps(BoolTag<false>{});\n  VM_STAMP(2)\n#pragma unroll\n"),
+        ("vm_scan_seq.hip", "    if (tid == 0) __hip_atomic_store(&fl[blk], 1u,",
+         "    VM_STAMP(3)\n    if (tid == 0) __hip_atomic_store(&fl[blk], 1u,"),
+        ("vm_scan_seq.hip", "    __syncthreads();  // every wave's reads below follow the flags wave 0 saw\n",
+         "    __syncthreads();  // every wave's reads below follow the flags wave 0 saw\n    VM_STAMP(4)\n"),
+        ("vm_scan_seq.hip", "    run_steps(BoolTag<true>{});\n    finish();\n  }\n}",
+         "    VM_STAMP(5)\n    run_steps(BoolTag<true>{});\n    finish();\n    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    VM_STAMP(6)\n  }\n}"),
+        ("vm_scan_seq.hip", "bool seq_supported(const ScanParams& p, int dtype) {",
+         "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
+         "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
+         "namespace vm {\nbool seq_supported(const ScanParams& p, int dtype) {"),
+    ],
     # timing probe: every step reads the segment's first B/C row (L1/K$-resident), so the
     # chunk kernel's time without the per-step scalar-load latency shows (results wrong)
     "bc_fixed": [("vm_scan_seq.hip",

@@ -634,6 +634,18 @@ constexpr int kFuMaxSpl = 9;   // splits (waves) per workgroup: dim <= 1152
 constexpr int kFuUPitch = 136; // bf16 pitch of a wave's [16 tok][128 ch] u tile
 constexpr int kFuXdPitch = 72; // bf16 pitch of the [16 tok][64] x_dbl[:R] operand
 
+// Workgroup barrier over LDS traffic only: __syncthreads() also waits vmcnt(0), which
+// drained the W_dt fragment loads (issued to land during the partial reduction) and every
+// u / x_dbl store at the first barrier after the x_proj MFMAs (timestamps,
+// scripts/diag/stamp_conv_proj.py: that phase took 8.9 us of the 20.9 us kernel at B = 1).
+// Register operands still get their own counted waits from the compiler at first use.
+__device__ __forceinline__ void fu_lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 template <int NB>  // NB = e_pad / 16 x_proj column blocks
 __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const SkTmParams q) {
   const ConvProjTmArgs& p = q.a;
@@ -815,7 +827,7 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
                                                          (lane >> 4) * 8)
                       : bf16x8{};
     }
-  __syncthreads();  // every wave's u tile is consumed: the area becomes the partials
+  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials
   const int ep = q.ep;
   float* myP = sP + wave * kFuTok * ep;
 #pragma unroll
@@ -830,7 +842,7 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
     const int t = i / (p.r_pad - p.r);
     sXD[t * kFuXdPitch + p.r + (i - t * (p.r_pad - p.r))] = bf16_t(0);
   }
-  __syncthreads();
+  fu_lds_barrier();
   // ---- x_dbl = bf16(sum of the partials in split order) ----
   for (int i = tid; i < kFuTok * p.e; i += blockDim.x) {
     const int t = i / p.e, e = i - t * p.e;
@@ -841,7 +853,7 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
     if (tok0 + t < ntok) p.xdbl[(long long)(tok0 + t) * p.xd_tl + e] = v;
   }
   if (!do_dt) return;
-  __syncthreads();
+  fu_lds_barrier();
   // ---- dt for channels c0 .. c0 + 127: tokens x 8 column tiles, K = r_pad ----
   f32x4 dacc[8];
 #pragma unroll
@@ -865,7 +877,7 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
         sDT[((lane >> 4) * 4 + rr) * dtp + ch] = from_f32<bf16_t>(dacc[i][rr]);
     }
   }
-  __syncthreads();
+  fu_lds_barrier();
   // 16 token rows x dim channels out, 16 B per lane-store
   const int q8 = p.dim >> 3;
   for (int i = tid; i < kFuTok * q8; i += blockDim.x) {

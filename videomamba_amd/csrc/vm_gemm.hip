@@ -283,6 +283,202 @@ __global__ __launch_bounds__(256) void linear_kernel(const LinParams p, const No
   }
 }
 
+// ---------------------------------------------------------------- LDS-DMA pipelined form
+// The same GEMM (same per-row K order: 64-wide steps, two 16x16x32 MFMAs per step in k
+// order, so every output row is bit-identical to linear_kernel's whatever the tile shape)
+// with the operand tiles staged global -> LDS by buffer_load ... lds (no VGPR round trip,
+// no ds_write pass) into NBUF stage buffers, NBUF - 1 steps in flight across the raw
+// s_barrier (counted vmcnt, never 0 in the loop; cdna_hip_programming.md §5 "Pipelining
+// across barriers").  linear_kernel's register ring keeps one step in flight and its
+// barrier drains vmcnt, so at B = 1 (M = 3144) each of its K steps waited out an L2 round
+// trip: in_proj (N = 2304, K = 576) ran 24.7 us against ~4 us of MFMA work.
+// LDS image per stage: [BM rows | BN rows] x 128 B (64 bf16 of K), 16-byte chunks
+// XOR-swizzled by (row / 2) & 7 so a 16-row fragment read touches every 16-byte slot of
+// the 256-byte bank row once; the swizzle is applied to the per-lane SOURCE address (the
+// DMA writes lane-linear).  Rows past m / n read as zero (buffer range) and are never
+// stored.  Workgroups are renumbered so each XCD owns a contiguous run of M tiles (their x
+// rows enter one L2 once; W is read by every XCD).
+constexpr int kDmaRow = 128;  // bytes per staged row
+
+__device__ __forceinline__ int dma_slot(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// one 16-byte-per-lane buffer load straight into LDS (wave-uniform LDS base + lane * 16)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voff, 0, 0, 0);
+}
+// s_waitcnt vmcnt(N) lgkmcnt(0) (expcnt left at its maximum)
+template <int N>
+__device__ __forceinline__ void dma_wait_vm_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
+}
+
+template <int BM, int BN, int NK, int NBUF>
+__global__ __launch_bounds__(256) void linear_dma_kernel(const LinParams p) {
+  constexpr int R = kDmaRow;
+  constexpr int STAGE = (BM + BN) * R;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int GA = BM * R / 4096, GB = BN * R / 4096;  // DMA instructions per wave per stage
+  constexpr int G = GA + GB;
+  static_assert(NBUF >= 2 && NBUF <= 4, "one to three stages in flight");
+  static_assert(GA * 4096 == BM * R && GB * 4096 == BN * R, "tile rows must fill whole DMA rounds");
+  constexpr int kOutPitch = BN + 8;
+  static_assert(BM * kOutPitch * 2 <= NBUF * STAGE, "output tile must fit the stage buffers");
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // bijective XCD-contiguous renumbering of the linear workgroup id (N tiles fastest)
+  const int ntn = gridDim.y;
+  const int nwg = gridDim.x * gridDim.y;
+  const int h = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xcd = h & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int l = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);
+  const int m0 = (l / ntn) * BM, n0 = (l % ntn) * BN;
+
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.x), 0, static_cast<int>((long long)p.m * p.ldx * 2), 0x00020000);
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.w), 0, static_cast<int>((long long)p.n * p.ldw * 2), 0x00020000);
+  // per-lane source byte offsets (at k = 0) of this wave's DMA instructions
+  int aoff[GA], boff[GB];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int o = (wave * GA + i) * 1024 + lane * 16;
+    const int row = o / R, chunk = dma_slot(row, (o % R) >> 4);
+    aoff[i] = ((m0 + row) * static_cast<int>(p.ldx)) * 2 + chunk * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int o = (wave * GB + i) * 1024 + lane * 16;
+    const int row = o / R, chunk = dma_slot(row, (o % R) >> 4);
+    boff[i] = ((n0 + row) * static_cast<int>(p.ldw)) * 2 + chunk * 16;
+  }
+  auto issue = [&](int kt, int buf) {
+    char* sa = dsm + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < GA; ++i)
+      dma16(xr, sa + (wave * GA + i) * 1024, aoff[i] + kt * R);
+    char* sb = sa + BM * R;
+#pragma unroll
+    for (int i = 0; i < GB; ++i)
+      dma16(wr, sb + (wave * GB + i) * 1024, boff[i] + kt * R);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* sA = dsm + buf * STAGE;
+    const char* sB = sA + BM * R;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[TM], bw[TN];
+      const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + row * R + dma_slot(row, chunk) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bw[j] = *reinterpret_cast<const bf16x8_t*>(sB + row * R + dma_slot(row, chunk) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < NK) issue(s, s);
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    // stage kt's DMA (this wave's share) has landed once at most the stages issued after
+    // it are outstanding; the barrier then covers every wave's share, and every wave is
+    // past its reads of the buffer the next issue overwrites (stage kt - 1's)
+    constexpr int kMaxAfter = NBUF - 2;
+    const int after = (kt + kMaxAfter < NK ? kMaxAfter : NK - 1 - kt);
+    // (lgkmcnt(0) too: this wave's fragment reads of the buffer the issue below refills
+    // have completed before it arrives; the signal fences keep the compiler from moving
+    // LDS accesses across the barrier)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (after >= 2) dma_wait_vm_lgkm0<2 * G>();
+    else if (after == 1) dma_wait_vm_lgkm0<G>();
+    else dma_wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (kt + NBUF - 1 < NK) issue(kt + NBUF - 1, (kt + NBUF - 1) % NBUF);
+    compute(kt % NBUF);
+  }
+
+  // epilogue: D[4(lane/16) + r][lane % 16] of every 16x16 tile -> LDS -> 16-B row stores
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();  // every wave is past its last fragment reads
+  bf16_t* sO = reinterpret_cast<bf16_t*>(dsm);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WN + j * 16 + (lane & 15);
+      const float b = p.bias && n0 + col < p.n ? p.bias[n0 + col] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        sO[row * kOutPitch + col] = from_f32<bf16_t>(acc[i][j][r] + b);
+      }
+    }
+  __syncthreads();
+  constexpr int kPieces = BM * BN / 8;
+#pragma unroll
+  for (int i = 0; i < (kPieces + 255) / 256; ++i) {
+    const int pc = tid + 256 * i;
+    if (kPieces % 256 != 0 && pc >= kPieces) break;
+    const int row = pc / (BN / 8), cq = pc % (BN / 8);
+    const int gm = m0 + row, gn = n0 + cq * 8;
+    if (gm < p.m && gn < p.n)
+      *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) =
+          *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+  }
+}
+
+// Tile choice for the pipelined form (row bits do not depend on it), measured at the B = 1
+// chunk shapes (scripts/diag/variant_linear.py): wide outputs (in_proj, N = 2 * d_inner)
+// on 128 x 128 tiles with two stage buffers (64 KB: two workgroups per CU; 14.1 us against
+// 17.6 for linear_kernel, three buffers 16.3); narrow ones (out_proj, N = d_model) on
+// 128 x 64 tiles with three buffers (72 KB; 9.1 against 11.3 us).
+#define VM_LDMA_TILE(BMV, BNV, NBV)                                                         \
+  {                                                                                         \
+    const dim3 grid((p.m + BMV - 1) / BMV, (p.n + BNV - 1) / BNV);                          \
+    const size_t lds = static_cast<size_t>(NBV) * (BMV + BNV) * kDmaRow;                    \
+    switch (p.k / kLinBK) {                                                                 \
+      VM_LDMA_K(BMV, BNV, NBV, 3) VM_LDMA_K(BMV, BNV, NBV, 6) VM_LDMA_K(BMV, BNV, NBV, 9)   \
+      VM_LDMA_K(BMV, BNV, NBV, 12) VM_LDMA_K(BMV, BNV, NBV, 18) VM_LDMA_K(BMV, BNV, NBV, 24) \
+      default: break;                                                                       \
+    }                                                                                       \
+  }
+#define VM_LDMA_K(BMV, BNV, NBV, NKV)                                                        \
+  case NKV:                                                                                  \
+    hipLaunchKernelGGL((linear_dma_kernel<BMV, BNV, NKV, NBV>), grid, dim3(256), lds, s, p); \
+    break;
+static void linear_dma_launch(const LinParams& p, hipStream_t s) {
+  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)
+  else VM_LDMA_TILE(128, 64, 3)
+}
+#undef VM_LDMA_K
+#undef VM_LDMA_TILE
+constexpr bool kLinearDma = true;  // vm_linear_fwd runs the pipelined form
+
 }  // namespace vm
 
 using namespace vm;
@@ -309,6 +505,10 @@ extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long l
   p.bias = bias; p.out = static_cast<bf16_t*>(out); p.ldo = ldo;
   p.m = m; p.n = n; p.k = k;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (kLinearDma) {
+    linear_dma_launch(p, s);
+    return vmhost::launch_status("vm_linear_fwd");
+  }
   const NormTail nt{};
   const int ntn = (n + kLinBN - 1) / kLinBN;
   // 128-row tiles when that still gives >= 1.5 workgroups per CU (256 CUs), else 64-row

@@ -1,20 +1,28 @@
 // Token-major selective scan for gfx950: one lane per channel, sequential in time.
 //
 // Same math as vm_scan.hip (_selective_scan_ref, models/videomamba/mamba_simple.py:30-106)
-// on the token-major layout the mixer uses for large batches: u / delta / z / out rows are
-// (batch, step, channel) with channel stride 1, so one wave reads one 128-byte line per
-// operand per step.  A lane owns one channel and keeps its 16 states in registers; per
-// (step, state) the work is the irreducible  a = exp2(delta*A*log2e),  h = a*h + (delta*u)*B,
-// y += h*C  — 4 VALU + 1 transcendental, no cross-lane scan and no re-sweep.  B_t / C_t
-// (shared by every channel of a batch row) are staged per 32-step block in LDS as fp32 and
-// read back as uniform-address (broadcast) ds_read_b128; u / delta / z are prefetched 8
-// steps ahead in registers.
-//
-// Parallelism is batch x channel-groups.  When that is too small to fill the chip (small
-// batch, e.g. the B=1 streaming-chunk latency case) the sequence is cut into S segments:
-//   pass 1 (MODE 1): each segment from a zero state -> end state and sum(delta);
-//   carry          : per (b, d, n) the entry state of every segment, sequentially over S;
-//   pass 2 (MODE 2): each segment from its entry state, emitting y (and h_last).
+// on the token-major layout the mixer uses: u / delta / z / out rows are (batch, step,
+// channel) with channel stride 1, so one wave reads one 128-byte line per operand per step.
+// A lane owns one channel and keeps its 16 states in registers as 8 packed fp32 pairs; per
+// (step, state) the work is the irreducible  a = exp2(delta*A),  h = a*h + (delta*u)*B,
+// y += h*C  (delta and the states in log2 units) — 4 VALU + 1 transcendental, no
+// cross-lane scan and no re-sweep.  B_t / C_t (shared by every channel of a batch row) are
+// one wave-uniform scalar load per step (both rows of the mixer's x_dbl in one
+// s_load_dwordx16), used directly as SGPR operands; u / delta / z are buffer loads
+// prefetched 8 steps ahead.  The kernels of this file:
+//   scan_seq_kernel (MODE 0)   single pass per (batch row, 128 channels), chip-filling batches;
+//   scan_seq_dtp_kernel        the same with dt_proj folded in (dt from the x_dbl rows on
+//                              MFMA, no delta stream) — the bench's kernel at B > 8;
+//   scan_chunk_kernel          small batches (e.g. the B = 1 streaming chunk): the sequence
+//                              cut into segments of T steps, 8 segments per workgroup;
+//                              PASS 1 (zero entry state -> end state and delta sum, composed
+//                              per workgroup into a block aggregate), PASS 2 (entry state
+//                              from h0 and the preceding blocks' aggregates, then the steps
+//                              again emitting y), either as two launches or as ONE launch
+//                              whose blocks hand their aggregates on through a sync buffer
+//                              (PASS 3 below);
+//   scan_seq_kernel MODE 1 / 2 + scan_seq_carry_kernel: the summary / carry / final form for
+//                              operands the scalar-load path cannot take (LDS-staged B / C).
 
 #include <stdlib.h>
 
@@ -691,7 +699,6 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     const float gf = g_nx;
     g_nx = gate_of(rz[(s + 1) & (kPF - 1)]);
     dl = live ? dl : 0.0f;
-    const float du = dl * uu;
     const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
     const f2 dl2 = {dl, dl};
     // du as a genuine register pair (one packed multiply): a {du, du} pair formed with
@@ -1211,20 +1218,31 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     // (per-XCD, non-coherent) L2 line, so no L2 write-back or invalidate is needed for them
     // to be seen.  Ordering: the publisher's s_waitcnt vmcnt(0) completes (acknowledges) its
     // aggregate stores before s_barrier lets thread 0 store the flag; the reader issues its
-    // aggregate loads only after thread 0's flag load has returned 1 (control dependency)
-    // and the following s_barrier.  An agent-scope release / acquire fence pair would add a
+    // aggregate loads only after wave 0's flag loads have all returned 1 (control
+    // dependency) and the following s_barrier.  An agent-scope release / acquire fence pair would add a
     // buffer_wbl2 / buffer_inv per workgroup for data that never sits in L2: measured
     // 45 -> 134 us at B = 1 with them.
-    if (tid == 0) {
+    // Wave 0 polls the preceding blocks' flags in parallel (lane j: blocks j, j + 64, ...):
+    // each poll is a round trip to the coherence point, and polled one block after another
+    // by one thread they cost the last block of a B = 1 row ~13 sequential round trips.
+    if (wave == 0) {
       bool timed_out = false;
-      for (int j = 0; j < blk; ++j) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(&fl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-               ++spins < (1u << 22))
-          __builtin_amdgcn_s_sleep(2);
-        if (spins >= (1u << 22)) timed_out = true;
+      unsigned spins = 0;
+      for (;;) {
+        bool seen = true;
+        for (int j = lane; j < blk; j += 64)
+          seen = seen && __hip_atomic_load(&fl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (__all(seen)) break;
+        if (++spins >= (1u << 22)) {
+          timed_out = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      s_fail = timed_out ? 1 : 0;
+      if (tid == 0) s_fail = timed_out ? 1 : 0;
+    }
+    if (tid == 0) {
+      const bool timed_out = s_fail != 0;
       if (timed_out) __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the last block past its wait resets the flags for the next launch
       if (__hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -1234,7 +1252,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         __hip_atomic_store(dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    __syncthreads();  // every wave's reads below follow the flags thread 0 saw
+    __syncthreads();  // every wave's reads below follow the flags wave 0 saw
     // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
     H0 *= kLog2e;  // log2 units
     H1 *= kLog2e;
