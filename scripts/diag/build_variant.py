@@ -98,12 +98,12 @@ VARIANTS = {
     # workgroup into a device array read back by vm_dbg_read_stamps
     # (scripts/diag/stamp_conv_proj.py); results unchanged
     "cp_stamp": [
-        ("vm_conv_proj_sk.hip", "template <int NB>  // NB = e_pad / 16 x_proj column blocks",
+        ("vm_conv_proj_sk.hip", "template <int NB, bool CS32>  // NB = e_pad / 16 x_proj column blocks; CS32: fp32 conv state in",
          "__device__ unsigned long long vm_dbg_stamps[4096 * 8];\n"
          "#define VM_STAMP(K) __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0) vm_dbg_stamps[blockIdx.x * 8 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
-         "template <int NB>  // NB = e_pad / 16 x_proj column blocks"),
-        ("vm_conv_proj_sk.hip", "  const int ntok = q.ntok;\n\n  // ---- one round of loads ----",
-         "  const int ntok = q.ntok;\n  VM_STAMP(0)\n\n  // ---- one round of loads ----"),
+         "template <int NB, bool CS32>  // NB = e_pad / 16 x_proj column blocks; CS32: fp32 conv state in"),
+        ("vm_conv_proj_sk.hip", "  const int ntok = q.ntok;\n\n  // Every global load and store",
+         "  const int ntok = q.ntok;\n  VM_STAMP(0)\n\n  // Every global load and store"),
         ("vm_conv_proj_sk.hip", "  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----",
          "  VM_STAMP(1)\n  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----"),
         ("vm_conv_proj_sk.hip", "  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials",
@@ -144,6 +144,31 @@ VARIANTS = {
          "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
          "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
          "namespace vm {\nbool seq_supported(const ScanParams& p, int dtype) {"),
+    ],
+    # per-wave phase timestamps of the fused small-batch conv_proj (lane 0 of every wave):
+    # entry (0), conv done (1), W_x 2-3 issued (2), u LDS tile written (3), x_proj MFMAs
+    # retired (4), u rows stored (5), W_dt issued (6), barrier passed (7)
+    # (scripts/diag/stamp_conv_proj.py --waves); results unchanged
+    "cp_stampw": [
+        ("vm_conv_proj_sk.hip", "template <int NB, bool CS32>  // NB = e_pad / 16 x_proj column blocks; CS32: fp32 conv state in",
+         "__device__ unsigned long long vm_dbg_stamps[2048 * 16 * 8];\n"
+         "#define VM_STAMP(K) __builtin_amdgcn_sched_barrier(0); if ((threadIdx.x & 63) == 0) vm_dbg_stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
+         "template <int NB, bool CS32>  // NB = e_pad / 16 x_proj column blocks; CS32: fp32 conv state in"),
+        ("vm_conv_proj_sk.hip", "  const int ntok = q.ntok;\n\n  // Every global load and store",
+         "  const int ntok = q.ntok;\n  VM_STAMP(0)\n\n  // Every global load and store"),
+        ("vm_conv_proj_sk.hip", "  wx_load(2);\n  wx_load(3);\n", "  VM_STAMP(1)\n  wx_load(2);\n  wx_load(3);\n  VM_STAMP(2)\n"),
+        ("vm_conv_proj_sk.hip", "  __builtin_amdgcn_wave_barrier();\n  // ---- x_proj partial",
+         "  VM_STAMP(3)\n  __builtin_amdgcn_wave_barrier();\n  // ---- x_proj partial"),
+        ("vm_conv_proj_sk.hip", "  // u rows leave from the LDS tile as 16-byte pieces",
+         "  { float sink = 0.0f;\n#pragma unroll\n    for (int j = 0; j < NB; ++j) sink += acc[j][0];\n    asm volatile(\"\" :: \"v\"(sink)); }\n  VM_STAMP(4)\n  // u rows leave from the LDS tile as 16-byte pieces"),
+        ("vm_conv_proj_sk.hip", "  // W_dt fragments for this wave's dt channels (128 per wave",
+         "  VM_STAMP(5)\n  // W_dt fragments for this wave's dt channels (128 per wave"),
+        ("vm_conv_proj_sk.hip", "  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials",
+         "  VM_STAMP(6)\n  fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials\n  VM_STAMP(7)"),
+        ("vm_conv_proj_sk.hip", "bool conv_proj_fused_ok(const ConvProjTmArgs& a) {",
+         "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
+         "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
+         "namespace vm {\nbool conv_proj_fused_ok(const ConvProjTmArgs& a) {"),
     ],
     # timing probe: every step reads the segment's first B/C row (L1/K$-resident), so the
     # chunk kernel's time without the per-step scalar-load latency shows (results wrong)

@@ -11,7 +11,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import videomamba_amd._lib as L  # noqa: E402
-L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", "cp_stamp", "libvideomamba_hip.so")
+WAVES = "--waves" in sys.argv  # cp_stampw: per-wave stamps [wg][16][8]
+L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", "cp_stampw" if WAVES else "cp_stamp",
+                          "libvideomamba_hip.so")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from bench import _event_us  # noqa: E402
@@ -48,6 +50,21 @@ us = _event_us(run, 50)
 lib = L.load()
 lib.vm_dbg_read_stamps.argtypes = [ctypes.c_void_p]
 res = []
+if WAVES:
+    run()
+    torch.cuda.synchronize()
+    nwg = (Lp + 15) // 16
+    buf = np.zeros(2048 * 16 * 8, dtype=np.uint64)
+    assert lib.vm_dbg_read_stamps(buf.ctypes.data) == 0
+    st = buf.reshape(2048, 16, 8)[:nwg, :9, :].astype(np.int64)
+    rel = (st - st[:, :, 0].min()) * 10e-3
+    d = rel[:, :, 1:] - rel[:, :, :-1]  # [wg][wave][7] phase durations
+    print(json.dumps({"event_us_avg": round(us, 2),
+                      "phase_median_us": [round(float(np.median(d[:, :, k])), 2) for k in range(7)],
+                      "phase_p90_us": [round(float(np.percentile(d[:, :, k], 90)), 2) for k in range(7)],
+                      "wave_skew_at_barrier_us": round(float(np.median(rel[:, :, 6].max(1) - rel[:, :, 6].min(1))), 2),
+                      "wave_start_skew_us": round(float(np.median(rel[:, :, 0].max(1) - rel[:, :, 0].min(1))), 2)}))
+    sys.exit(0)
 for rep in range(5):
     run()
     torch.cuda.synchronize()

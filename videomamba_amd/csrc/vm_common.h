@@ -26,6 +26,16 @@ template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+// One 16-byte-per-lane buffer load straight into LDS: the DMA writes lane l's 16 bytes at
+// (wave-uniform LDS base) + 16 l, so the LDS image is lane-linear and any layout is made by
+// choosing each lane's source offset.  Out-of-range offsets read as zero.  Kept in a device
+// function: written inline in a kernel-template lambda, clang dropped the kernels' host
+// stubs (undefined symbols at load time).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voff, 0, 0, 0);
+}
+
 // Round-trip through the storage type (models the reference's "->e" rounding points).
 template <typename T> __device__ __forceinline__ float round_to(float v) {
   return to_f32(from_f32<T>(v));

@@ -633,6 +633,7 @@ constexpr int kFuTok = 16;     // token rows per workgroup
 constexpr int kFuMaxSpl = 9;   // splits (waves) per workgroup: dim <= 1152
 constexpr int kFuUPitch = 136; // bf16 pitch of a wave's [16 tok][128 ch] u tile
 constexpr int kFuXdPitch = 72; // bf16 pitch of the [16 tok][64] x_dbl[:R] operand
+constexpr int kFuXRows = 20;   // x rows staged per wave (tok0 - 3 .. tok0 + 16)
 
 // Workgroup barrier over LDS traffic only: __syncthreads() also waits vmcnt(0), which
 // drained the W_dt fragment loads (issued to land during the partial reduction) and every
@@ -646,7 +647,7 @@ __device__ __forceinline__ void fu_lds_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-template <int NB>  // NB = e_pad / 16 x_proj column blocks
+template <int NB, bool CS32>  // NB = e_pad / 16 x_proj column blocks; CS32: fp32 conv state in
 __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const SkTmParams q) {
   const ConvProjTmArgs& p = q.a;
   // LDS: per-wave u tiles, then (aliased) the split partials [split][tok][ep], then
@@ -673,16 +674,77 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
   const int c = c0 + 2 * (cact ? lane : 0);
   const int ntok = q.ntok;
 
+  // Every global load and store of the tile is a buffer access whose out-of-range offset
+  // (rows outside [0, ntok), idle lanes, padding k-steps) reads 0 / stores nothing, so none
+  // sits behind a branch: a per-element "load or zero" select made hipcc branch around each
+  // access and wait vmcnt(0) after it — 16 dependent round trips for the W_dt fragments,
+  // most of the 8.9 us between the conv and the x_proj partials at B = 1
+  // (scripts/diag/stamp_conv_proj.py).
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.x), 0, static_cast<int>((long long)ntok * p.x_tl * 2), 0x00020000);
+  const auto wxr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.wx), 0, static_cast<int>((long long)p.e_pad * p.dim * 2), 0x00020000);
+  const auto wdr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.wdt), 0,
+      p.wdt ? static_cast<int>((long long)p.dim * p.r_pad * 2) : 0, 0x00020000);
+  const auto ur = __builtin_amdgcn_make_buffer_rsrc(
+      p.u, 0, static_cast<int>((long long)ntok * p.u_tl * 2), 0x00020000);
+  constexpr int kOut = 0x7ffffff0;  // an offset past every range above
+  // the offset select stays a select: seen through, hipcc splits the access into a load
+  // per arm of a divergent branch and waits vmcnt(0) at the join
+  auto opaque = [](int off) {
+    asm volatile("" : "+v"(off));
+    return off;
+  };
   // ---- one round of loads ----
-  // x rows tok0 - 3 .. tok0 + 15 of channels c, c + 1 (zero outside [0, ntok))
-  uint32_t xw[kFuTok + 3];
+  // the (at most one: out_len >= 24) sequence starting in tok0 - 2 .. tok0 + 15, whose
+  // first 3 steps may lie in this tile: its old conv-state taps for steps -1, -2, -3
+  // (state columns W - 1, W - 2, W - 3)
+  const int bs = (tok0 - 2 + p.out_len - 1) / p.out_len;  // tok0 - 2 + out_len - 1 >= 0
+  const int ts = bs * p.out_len;
+  const bool has_start = ts < tok0 + kFuTok && bs < p.batch;
+  // Loaded first and unconditionally as 16-bit buffer pieces (offsets out of range where
+  // unused): no load sits in a branch whose join makes hipcc drain vmcnt, and the counted
+  // waits for them never cover the W_x round issued later.
+  float csl[3], csh[3];
+  {
+    constexpr int es = CS32 ? 4 : 2;
+    const long long span = p.csi ? ((long long)(p.batch - 1) * p.csi_sb +
+                                    (long long)(p.dim - 1) * p.csi_sd + W) * es
+                                 : 0;
+    const auto csr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.csi), 0,
+                                                       static_cast<int>(span), 0x00020000);
+    auto tap = [&](long long idx, bool ok) {
+      const int off = opaque(ok ? static_cast<int>(idx * es) : kOut);
+      if constexpr (CS32)
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csr, off, 0, 0));
+      else
+        return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(csr, off, 0, 0)) << 16);
+    };
 #pragma unroll
-  for (int r = 0; r < kFuTok + 3; ++r) {
-    const int tok = tok0 - 3 + r;
-    xw[r] = (tok >= 0 && tok < ntok && cact)
-                ? *reinterpret_cast<const uint32_t*>(p.x + (long long)tok * p.x_tl + c)
-                : 0u;
+    for (int m = 0; m < 3; ++m) {
+      const int col = W - 1 - m;
+      const bool ok = has_start && p.csi && col >= 0;
+      const long long base = (long long)bs * p.csi_sb + (long long)c * p.csi_sd + col;
+      csl[m] = tap(base, ok);
+      csh[m] = tap(base + p.csi_sd, ok);
+    }
   }
+
+  __builtin_amdgcn_sched_barrier(0);
+  // x rows tok0 - 3 .. tok0 + 16 of this split's 128 channels go to the wave's own LDS
+  // slice by buffer_load ... lds, 4 rows x 256 B per instruction (5 instead of 19 per-lane
+  // 4-byte loads: with 9 waves per CU issuing ~70 memory instructions each, their issue
+  // backed up; per-wave stamps, scripts/diag/stamp_conv_proj.py --waves).  Rows outside
+  // [0, ntok) read as zero or hold stale bytes: their taps are replaced (sequence starts
+  // take the conv state) or their outputs dropped (tokens past ntok).
+  char* sXw = fsm + kArea + kFuTok * kFuXdPitch * 2 + wave * (kFuXRows * 256);
+#pragma unroll
+  for (int i = 0; i < kFuXRows / 4; ++i) {
+    const int row = 4 * i + (lane >> 4);
+    dma16(xr, sXw + i * 1024, ((tok0 - 3 + row) * static_cast<int>(p.x_tl) + c0) * 2 + (lane & 15) * 16);
+  }
+  __builtin_amdgcn_sched_barrier(0);
   // W_x fragments of this split: column block j, k-step ks (rows e, 8 channels per lane);
   // k-steps 0-1 with the first round, 2-3 once the x rows are consumed (register budget)
   bf16x8 wv[4][NB];
@@ -690,39 +752,41 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int kc = ks * 32 + (lane >> 4) * 8;
-      wv[ks][j] = kc < nch ? *reinterpret_cast<const bf16x8*>(
-                                 p.wx + (long long)(j * 16 + (lane & 15)) * p.dim + c0 + kc)
-                           : bf16x8{};
+      wv[ks][j] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                      wxr, opaque(kc < nch ? ((j * 16 + (lane & 15)) * p.dim + c0 + kc) * 2 : kOut),
+                      0, 0));
     }
   };
-  wx_load(0);
-  wx_load(1);
+  // conv taps and bias: unconditional loads (clamped index), zeroed by a select
   float wl[4], wh[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    wl[k] = k >= 4 - W ? p.cw[c * W + k - (4 - W)] : 0.0f;
-    wh[k] = k >= 4 - W ? p.cw[(c + 1) * W + k - (4 - W)] : 0.0f;
+    const int kk = k - (4 - W) > 0 ? k - (4 - W) : 0;
+    const float vl = p.cw[c * W + kk], vh = p.cw[(c + 1) * W + kk];
+    wl[k] = k >= 4 - W ? vl : 0.0f;
+    wh[k] = k >= 4 - W ? vh : 0.0f;
   }
-  const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
-  // the (at most one: out_len >= 24) sequence starting in tok0 - 2 .. tok0 + 15, whose
-  // first 3 steps may lie in this tile: its old conv-state taps for steps -1, -2, -3
-  // (state columns W - 1, W - 2, W - 3)
-  const int bs = (tok0 - 2 + p.out_len - 1) / p.out_len;  // tok0 - 2 + out_len - 1 >= 0
-  const int ts = bs * p.out_len;
-  const bool has_start = ts < tok0 + kFuTok && bs < p.batch;
-  float csl[3] = {0.f, 0.f, 0.f}, csh[3] = {0.f, 0.f, 0.f};
-  if (has_start && p.csi) {
+  const float* cbp = p.cb ? p.cb : p.cw;
+  const float bl0 = cbp[c], bh0 = cbp[c + 1];
+  const float bl = p.cb ? bl0 : 0.0f, bh = p.cb ? bh0 : 0.0f;
+  __builtin_amdgcn_sched_barrier(0);
+  wx_load(0);
+  wx_load(1);
+  __builtin_amdgcn_sched_barrier(0);
+  // the x rows (and the taps) have landed once only the 2 * NB W_x loads are in flight;
+  // each wave reads only the rows its own DMA wrote
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if constexpr (2 * NB == 2) __builtin_amdgcn_s_waitcnt(0x0F72);
+  else if constexpr (2 * NB == 4) __builtin_amdgcn_s_waitcnt(0x0F74);
+  else if constexpr (2 * NB == 6) __builtin_amdgcn_s_waitcnt(0x0F76);
+  else if constexpr (2 * NB == 8) __builtin_amdgcn_s_waitcnt(0x0F78);
+  else __builtin_amdgcn_s_waitcnt(0x0F7A);  // vmcnt(10)
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  uint32_t xw[kFuTok + 3];
 #pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int col = W - 1 - m;
-      if (col >= 0) {
-        const long long base = (long long)bs * p.csi_sb + (long long)c * p.csi_sd + col;
-        csl[m] = load_dyn(p.csi, base, p.csi_dtype);
-        csh[m] = load_dyn(p.csi, base + p.csi_sd, p.csi_dtype);
-      }
-    }
-  }
-
+  for (int r = 0; r < kFuTok + 3; ++r)
+    xw[r] = cact ? *reinterpret_cast<const uint32_t*>(sXw + r * 256 + 4 * lane) : 0u;
   // ---- conv + SiLU: channels c, c + 1, tokens tok0 .. tok0 + 15 ----
   auto pack = [&](float al, float ah, bool live) -> uint32_t {
     const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
@@ -763,43 +827,13 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
     }
     upk[i] = pack(al, ah, st < p.seqlen && tok0 + i < ntok && cact);
   }
-  // ---- new conv state of a sequence ending in this tile: its last W raw inputs ----
-  if (p.cso && cact) {
-    const int be1 = min(p.batch - 1, (tok0 + kFuTok - 1) / p.out_len);
-    for (int be = b0; be <= be1; ++be) {  // the tile's (at most two) sequences
-      const int tl = be * p.out_len + p.seqlen - 1;
-      if (tl < tok0 || tl >= tok0 + kFuTok) continue;
-      for (int s2 = 0; s2 < W; ++s2) {
-        const int te = p.seqlen - W + s2;
-        float vl = 0.0f, vh = 0.0f;
-        if (te >= 0) {
-          const int r = be * p.out_len + te - (tok0 - 3);  // 0 .. kFuTok + 2
-          uint32_t v = 0u;
-#pragma unroll
-          for (int rr = 0; rr < kFuTok + 3; ++rr) v = rr == r ? xw[rr] : v;
-          vl = __uint_as_float(v << 16);
-          vh = __uint_as_float(v & 0xffff0000u);
-        } else if (p.csi) {
-          const long long base = (long long)be * p.csi_sb + (long long)c * p.csi_sd + W + te;
-          vl = load_dyn(p.csi, base, p.csi_dtype);
-          vh = load_dyn(p.csi, base + p.csi_sd, p.csi_dtype);
-        }
-        const long long ob = (long long)be * p.cso_sb + (long long)c * p.cso_sd + s2;
-        store_dyn(p.cso, ob, p.cso_dtype, vl);
-        store_dyn(p.cso, ob + p.cso_sd, p.cso_dtype, vh);
-      }
-    }
-  }
   wx_load(2);
   wx_load(3);
   // ---- u: global rows and this wave's LDS tile ----
   bf16_t* myU = sU + wave * kFuTok * kFuUPitch;
 #pragma unroll
-  for (int i = 0; i < kFuTok; ++i) {
+  for (int i = 0; i < kFuTok; ++i)
     *reinterpret_cast<uint32_t*>(&myU[i * kFuUPitch + 2 * lane]) = upk[i];
-    if (cact && tok0 + i < ntok)
-      *reinterpret_cast<uint32_t*>(p.u + (long long)(tok0 + i) * p.u_tl + c) = upk[i];
-  }
   __builtin_amdgcn_wave_barrier();
   // ---- x_proj partial of this split: tokens x e_pad columns, K = 128 ----
   f32x4 acc[NB];
@@ -813,6 +847,18 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
     for (int j = 0; j < NB; ++j)
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wv[ks][j], acc[j], 0, 0, 0);
   }
+  // u rows leave from the LDS tile as 16-byte pieces (4 stores per lane instead of 16)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int id = k * 64 + lane, row = id >> 4, ch = (id & 15) * 8;
+    typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+    const v4i v = *reinterpret_cast<const v4i*>(&myU[row * kFuUPitch + ch]);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        v, ur,
+        opaque(ch < nch && tok0 + row < ntok ? ((tok0 + row) * static_cast<int>(p.u_tl) + c0 + ch) * 2
+                                             : kOut),
+        0, 0);
+  }
   // W_dt fragments for this wave's dt channels (128 per wave, 8 column tiles x 2 k-steps),
   // in flight during the reduction
   const bool do_dt = p.wdt != nullptr;
@@ -822,10 +868,11 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = min(c0 + i * 16 + (lane & 15), p.dim - 1);
-      bw[i][ks] = do_dt && ks * 32 < p.r_pad
-                      ? *reinterpret_cast<const bf16x8*>(p.wdt + (long long)ch * p.r_pad + ks * 32 +
-                                                         (lane >> 4) * 8)
-                      : bf16x8{};
+      bw[i][ks] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                      wdr, opaque(ks * 32 < p.r_pad ? (ch * p.r_pad + ks * 32 + (lane >> 4) * 8) * 2
+                                                  : kOut),
+                      0, 0));
     }
   fu_lds_barrier();  // every wave's u tile is consumed: the area becomes the partials
   const int ep = q.ep;
@@ -852,7 +899,39 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
     if (e < p.r) sXD[t * kFuXdPitch + e] = v;
     if (tok0 + t < ntok) p.xdbl[(long long)(tok0 + t) * p.xd_tl + e] = v;
   }
-  if (!do_dt) return;
+  // ---- new conv state of a sequence ending in this tile: its last W raw inputs (from the
+  // staged x rows), written last: after the conv, the branch's join made hipcc wait
+  // vmcnt(0) there, serialising the two W_x load rounds ----
+  auto write_conv_state = [&]() {
+    if (p.cso && cact) {
+      const int be1 = min(p.batch - 1, (tok0 + kFuTok - 1) / p.out_len);
+      for (int be = b0; be <= be1; ++be) {  // the tile's (at most two) sequences
+        const int tl = be * p.out_len + p.seqlen - 1;
+        if (tl < tok0 || tl >= tok0 + kFuTok) continue;
+        for (int s2 = 0; s2 < W; ++s2) {
+          const int te = p.seqlen - W + s2;
+          float vl = 0.0f, vh = 0.0f;
+          if (te >= 0) {
+            const int r = be * p.out_len + te - (tok0 - 3);  // 0 .. kFuTok + 2
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(sXw + r * 256 + 4 * lane);
+            vl = __uint_as_float(v << 16);
+            vh = __uint_as_float(v & 0xffff0000u);
+          } else if (p.csi) {
+            const long long base = (long long)be * p.csi_sb + (long long)c * p.csi_sd + W + te;
+            vl = load_dyn(p.csi, base, p.csi_dtype);
+            vh = load_dyn(p.csi, base + p.csi_sd, p.csi_dtype);
+          }
+          const long long ob = (long long)be * p.cso_sb + (long long)c * p.cso_sd + s2;
+          store_dyn(p.cso, ob, p.cso_dtype, vl);
+          store_dyn(p.cso, ob + p.cso_sd, p.cso_dtype, vh);
+        }
+      }
+    }
+  };
+  if (!do_dt) {
+    write_conv_state();
+    return;
+  }
   fu_lds_barrier();
   // ---- dt for channels c0 .. c0 + 127: tokens x 8 column tiles, K = r_pad ----
   f32x4 dacc[8];
@@ -886,13 +965,17 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
       *reinterpret_cast<uint4*>(p.dt + (long long)(tok0 + t) * p.dt_tl + qd * 8) =
           *reinterpret_cast<const uint4*>(&sDT[t * dtp + qd * 8]);
   }
+  write_conv_state();
 }
 
 bool conv_proj_fused_ok(const ConvProjTmArgs& a) {
   // e_pad <= 80 (R + 2N <= 80, every VideoMamba size up to d_model 768): wider x_proj
-  // outputs exceed the register budget of the 576-thread workgroup
+  // outputs exceed the register budget of the 576-thread workgroup; buffer byte offsets
+  // (x and u rows) must fit 31 bits
+  const long long ntok = static_cast<long long>(a.batch) * a.out_len;
   return a.dim <= kFuMaxSpl * kSkCh && a.out_len >= 24 && a.e_pad <= 80 &&
-         (a.e + 3) / 4 * 4 <= kSkMaxEp && (a.wdt == nullptr || a.r_pad <= 64);
+         (a.e + 3) / 4 * 4 <= kSkMaxEp && (a.wdt == nullptr || a.r_pad <= 64) &&
+         (ntok + 3) * a.x_tl * 2 < (1ll << 31) && (ntok + 3) * a.u_tl * 2 < (1ll << 31);
 }
 
 void conv_proj_fused_launch(const ConvProjTmArgs& a, hipStream_t s) {
@@ -906,12 +989,16 @@ void conv_proj_fused_launch(const ConvProjTmArgs& a, hipStream_t s) {
   constexpr int kUBytes = kFuMaxSpl * kFuTok * kFuUPitch * 2;
   constexpr int kPBytes = kFuMaxSpl * kFuTok * kSkMaxEp * 4;
   const size_t lds = static_cast<size_t>(kUBytes > kPBytes ? kUBytes : kPBytes) +
-                     kFuTok * kFuXdPitch * 2;
+                     kFuTok * kFuXdPitch * 2 + kFuMaxSpl * kFuXRows * 256;
   static_assert(kFuTok * (kFuMaxSpl * kSkCh + 8) * 2 <= kPBytes, "dt tile exceeds the area");
   const dim3 grid(tiles), block(64 * q.nsplit);
+  const bool cs32 = a.csi != nullptr && a.csi_dtype != VM_DTYPE_BF16;
   switch (a.e_pad / 16) {
-#define VM_FU_CASE(NBV) \
-    case NBV: hipLaunchKernelGGL(conv_proj_fused_kernel<NBV>, grid, block, lds, s, q); break;
+#define VM_FU_CASE(NBV)                                                                    \
+    case NBV:                                                                              \
+      if (cs32) hipLaunchKernelGGL((conv_proj_fused_kernel<NBV, true>), grid, block, lds, s, q); \
+      else hipLaunchKernelGGL((conv_proj_fused_kernel<NBV, false>), grid, block, lds, s, q);   \
+      break;
     VM_FU_CASE(1) VM_FU_CASE(2) VM_FU_CASE(3) VM_FU_CASE(4) VM_FU_CASE(5)
 #undef VM_FU_CASE
   }

@@ -301,11 +301,6 @@ __global__ __launch_bounds__(256) void linear_kernel(const LinParams p, const No
 constexpr int kDmaRow = 128;  // bytes per staged row
 
 __device__ __forceinline__ int dma_slot(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-// one 16-byte-per-lane buffer load straight into LDS (wave-uniform LDS base + lane * 16)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                           voff, 0, 0, 0);
-}
 // s_waitcnt vmcnt(N) lgkmcnt(0) (expcnt left at its maximum)
 template <int N>
 __device__ __forceinline__ void dma_wait_vm_lgkm0() {
