@@ -45,8 +45,9 @@
  *   - Return 0 on success, a negative VM_E* code otherwise; vm_last_error() gives the
  *     message.  Nothing is thrown across the ABI.
  *   - Outputs are deterministic (bitwise repeatable).  The only atomics are the one-launch
- *     segmented scan's block hand-off flags (agent-scope, in the caller's sync buffer; see
- *     vm_selective_scan_sync_bytes) — they order work, never accumulate values.
+ *     segmented scan's block hand-off granules and launch counter (agent-scope, in the
+ *     caller's sync buffer; see vm_selective_scan_sync_bytes) — they carry and order values,
+ *     never accumulate them.
  */
 #ifndef VIDEOMAMBA_HIP_H
 #define VIDEOMAMBA_HIP_H
@@ -55,7 +56,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 8
+#define VM_ABI_VERSION 9
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -170,8 +171,11 @@ long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen, int 
 
 /* Sync-buffer bytes for the one-launch segmented form (0 when the single pass runs).
  * `sync` (ABI v7, both scan entry points; NULL = the two-launch segmented form) must be
- * zero-filled before its first use; every launch leaves its flags zero again.  One sync
- * buffer must not serve two launches that can run at the same time (e.g. on two streams).
+ * zero-filled before its first use and then left alone: every launch leaves it valid for the
+ * next (ABI v9: word 1 is an epoch each launch advances, and blocks hand their aggregates on
+ * as {tag = epoch, value} granules, so stale granules of any earlier launch — of any shape —
+ * never match; tags wrap after 2^32 - 1 launches on one buffer).  One sync buffer must not
+ * serve two launches that can run at the same time (e.g. on two streams).
  * The one-launch form runs when the buffer is large enough and the segmented grid fits one
  * workgroup per CU of the stream's device (blocks then wait on earlier, resident blocks'
  * published aggregates); results are identical to the two-launch form.

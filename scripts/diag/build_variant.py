@@ -120,8 +120,9 @@ VARIANTS = {
          "namespace vm {\nbool conv_proj_fused_ok(const ConvProjTmArgs& a) {"),
     ],
     # phase timestamps of the one-launch chunked scan (PASS 3) per workgroup: entry (0),
-    # start-up loads landed (1), PASS 1 steps done (2), aggregate published (3), preceding
-    # flags seen (4), entry state composed (5), PASS 2 done and drained (6)
+    # start-up loads landed (1), PASS 1 steps done (2), segments composed and aggregate
+    # granules stored (3), PASS 2 prefetch issued (4), preceding granules seen and entry
+    # state composed (5), PASS 2 done and drained (6)
     # (scripts/diag/stamp_scan.py); results unchanged
     "sc_stamp": [
         ("vm_scan_seq.hip", "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>\n__global__ __launch_bounds__(64 * kChW)",
@@ -134,10 +135,10 @@ VARIANTS = {
          "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n  VM_STAMP(1)\n"),
         ("vm_scan_seq.hip", "  run_steps(BoolTag<false>{});\n#pragma unroll\n",
          "  run_steps(BoolTag<false>{});\n  VM_STAMP(2)\n#pragma unroll\n"),
-        ("vm_scan_seq.hip", "    if (tid == 0) __hip_atomic_store(&fl[blk], 1u,",
-         "    VM_STAMP(3)\n    if (tid == 0) __hip_atomic_store(&fl[blk], 1u,"),
-        ("vm_scan_seq.hip", "    __syncthreads();  // every wave's reads below follow the flags wave 0 saw\n",
-         "    __syncthreads();  // every wave's reads below follow the flags wave 0 saw\n    VM_STAMP(4)\n"),
+        ("vm_scan_seq.hip", "    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)",
+         "    VM_STAMP(3)\n    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)"),
+        ("vm_scan_seq.hip", "    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----\n    // Wave w",
+         "    VM_STAMP(4)\n    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----\n    // Wave w"),
         ("vm_scan_seq.hip", "    run_steps(BoolTag<true>{});\n    finish();\n  }\n}",
          "    VM_STAMP(5)\n    run_steps(BoolTag<true>{});\n    finish();\n    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    VM_STAMP(6)\n  }\n}"),
         ("vm_scan_seq.hip", "bool seq_supported(const ScanParams& p, int dtype) {",

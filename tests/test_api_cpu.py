@@ -288,9 +288,10 @@ def test_scan_workspace_query_without_gpu():
     chunked = 2 * (9 * 64 * 17) * 4
     legacy = 2 * 4 * 64 * (2 * 16 + 1) * 4
     assert one == 0 and four == max(chunked, legacy)
-    # the one-launch form's sync buffer: a 16-byte header (the sticky error word), then
-    # (nblk + 1) counters per (row, 64-channel group)
-    assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 16 + 2 * 1 * (1 + 1) * 4
+    # the one-launch form's sync buffer: a 16-byte header (error word, epoch, start count),
+    # then a {tag, value} granule per (row, 64-channel group, block, 16 states + delta sum,
+    # channel)
+    assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 16 + 2 * 1 * 1 * 17 * 64 * 8
     assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
     assert lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0) > 0
 
@@ -298,12 +299,13 @@ def test_scan_workspace_query_without_gpu():
 def test_scan_segment_cost_model_choices_without_gpu():
     """The measured segment cost model (vm_scan_seq.hip::choose_segments, fitted to
     profiles/r02_scan_segments_sweep.jsonl) as seen through the sync-buffer query:
-    (nblk + 1) flags per (row, 64-channel group) at M-16f (D = 1152, 18 groups).  B = 1:
+    nblk blocks of {tag, value} granules per (row, 64-channel group) at M-16f (D = 1152, 18
+    groups).  B = 1:
     S = 112 -> 14 blocks of 8 segments (252 workgroups, one per CU); B = 2 .. 8: S = 56 ->
     7 blocks (the round-1 wave-target rule chose 2-3x slower counts there); B >= 72 (1,280+
     waves): single pass, no segments."""
     lib = _lib.load()
-    nblk = lambda B, L: (lib.vm_selective_scan_sync_bytes(B, 1152, L, 16, 0) - 16) // (B * 18 * 4) - 1  # noqa: E731
+    nblk = lambda B, L: (lib.vm_selective_scan_sync_bytes(B, 1152, L, 16, 0) - 16) // (B * 18 * 17 * 64 * 8)  # noqa: E731
     assert nblk(1, 3137) == 14 and nblk(1, 12545) == 14
     assert nblk(2, 3137) == nblk(4, 3137) == nblk(8, 3137) == 7
     assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
@@ -342,7 +344,7 @@ def test_scan_sync_error_word_is_reported_on_the_host():
     buf.view(torch.int32)[0] = 1  # what a timed-out block stores
     assert K.scan_sync_status(buf) == 1
     buf.view(torch.int32)[0] = 0
-    buf[16:] = 7  # flags / counters do not count as errors
+    buf[4:] = 7  # epoch, start count and granules do not count as errors
     assert K.scan_sync_status(buf) == 0
     assert lib.vm_selective_scan_sync_status(buf.data_ptr(), 8) == -1
     assert b"sync header" in lib.vm_last_error()

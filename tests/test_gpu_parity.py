@@ -351,10 +351,11 @@ def test_scan_dtproj_matches_oracle(Bz, D, L, R):
                                               (1, 40, 3137, 0), (3, 64, 1000, 24),
                                               (1, 192, 12545, 0)])
 def test_scan_one_launch_matches_two_launch_bitwise(Bz, D, L, segments, dt):
-    """The segmented token-major scan as ONE launch (blocks publish their aggregates and
-    wait on the earlier blocks' flags in a zeroed sync buffer) against the two-launch form:
-    bit-identical y and h_last, over repeated launches on the same sync buffer (every
-    launch must leave it zeroed for the next), with the flags checked zero afterwards."""
+    """The segmented token-major scan as ONE launch (blocks publish their aggregates as
+    epoch-tagged granules in a zero-initialised sync buffer and poll the earlier blocks'
+    granules) against the two-launch form: bit-identical y and h_last, over repeated
+    launches on the same sync buffer (each leaves it valid for the next: epoch = launches
+    so far, start count 0, no error)."""
     N, R = 16, 8
     E = R + 2 * N
     Lp = (L + 7) // 8 * 8
@@ -385,11 +386,14 @@ def test_scan_one_launch_matches_two_launch_bitwise(Bz, D, L, segments, dt):
         return y, h
 
     y2, h2 = run(False)
-    for _ in range(3):
+    for k in range(3):
         y1, h1 = run(True)
         torch.cuda.synchronize()
         assert torch.equal(y1, y2) and torch.equal(h1, h2)
-        assert not sync.any()
+        # header after the launch (ABI v9): no timed-out hand-off, the epoch advanced to
+        # this launch's tag, the start count back at 0 for the next launch
+        head = sync[:16].view(torch.int32).cpu().tolist()
+        assert head[0] == 0 and head[1] == k + 1 and head[2] == 0, head
     ref_y, _ = orc.selective_scan(u.float(), delta.float(), A, Bm.float(), Cm.float(), Dv,
                                   z.float(), bias, True, init, True)
     _close(y1.view(Bz, Lp, D)[:, :L].transpose(1, 2), ref_y, 1e-4 if dt == torch.float32 else 2e-2)

@@ -63,7 +63,8 @@ void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
                 size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s);
 // Bytes of the zeroed sync buffer the one-launch chunked form needs (0: single pass).
 // Word 0 is the sticky error word (non-zero after a launch whose block handoff timed out;
-// vm_selective_scan_sync_status), words 1..kSyncHeaderWords-1 pad, then flags / counters.
+// vm_selective_scan_sync_status), word 1 the epoch, word 2 the launch's start count, word 3
+// pad, then the {tag, value} hand-off granules.
 constexpr int kSyncHeaderWords = 4;
 size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus = 0);
 // Paired scans need the scalar-B/C kernels and, when segmented, the chunked form.

@@ -795,9 +795,11 @@ struct ChunkWork {
   float* aggS;  // [B][nblk][D]               block delta' sums
   int T;        // steps per segment
   int nblk;     // blocks per sequence
-  unsigned* flags;  // one-launch form: [B][groups][nblk] block-published flags (0 between launches)
-  unsigned* done;   // one-launch form: [B][groups] count of blocks past their wait
-  unsigned* err;    // one-launch form: sticky error word (word 0 of the sync buffer)
+  // one-launch form (PASS 3), all in the caller's zero-initialised sync buffer:
+  unsigned* err;     // word 0: sticky error word
+  unsigned* epoch;   // word 1: the tag of the last launch that used the buffer
+  unsigned* done;    // word 2: blocks of the current launch that have read the epoch
+  unsigned long long* gran;  // [B][groups][nblk][kMaxN + 1][64] {tag, value} granules
 };
 
 template <bool V> struct BoolTag { static constexpr bool value = V; };
@@ -812,7 +814,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   __shared__ float sH[kChW][kMaxN][64];
   __shared__ float sS[kChW][64];
   __shared__ float sA[kMaxN][64];
-  __shared__ int s_fail;  // one-launch form: this block's wait timed out
+  __shared__ unsigned s_tag;  // one-launch form: this launch's hand-off tag
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -959,6 +961,24 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // one wait for every start-up load (parameters, entry operands, prologue): left pending
   // they would merge into the step loop's header waits
   __builtin_amdgcn_s_waitcnt(0);
+  if constexpr (PASS == 3) {
+    // This launch's hand-off tag: the buffer's epoch + 1 (never 0, the zeroed buffer's
+    // value).  Every block reads the epoch before adding itself to `done`; the block that
+    // completes the count (so every block has read it) resets the count and advances the
+    // epoch for the next launch.  Tags only grow over a buffer's launches, so granules left
+    // by an earlier launch — of any shape — never match (until 2^32 - 1 launches wrap).
+    if (tid == 0) {
+      const unsigned ep = __hip_atomic_load(w.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned tag = ep + 1u == 0u ? 1u : ep + 1u;
+      s_tag = tag;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the read completes before the count
+      const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+      if (__hip_atomic_fetch_add(w.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
+        __hip_atomic_store(w.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   // A transposed into LDS: sA[n][c] (zero for n >= N and for channels past dim)
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -1137,7 +1157,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     sH[wave][2 * q + 1][lane] = h[q].y;
   }
   sS[wave][lane] = sdel;
-  __syncthreads();
+  // LDS-only barrier: the step loop's last refill loads (for steps past the segment) are
+  // still in flight and need not land before the composition
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   // compose the block's segments for states n0, n0 + 1: entry offsets E_j, delta prefixes
   // P_j and the block aggregate (PASS 1: all to the workspace; one-launch form: E_j back into
   // sH[j] in place, the aggregate to the workspace for the blocks after this one)
@@ -1160,34 +1185,38 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     E1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), E1, Hj1);
     P += Sj;
   }
-  if (active) {
-    float* ah = &w.aggH[(rowA + blk * D + d) * kMaxN + n0];
-    if constexpr (PASS == 3) {  // agent-coherent stores: no L2 write-back needed to publish
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(ah),
-                         static_cast<unsigned long long>(__float_as_uint(E0)) |
-                             (static_cast<unsigned long long>(__float_as_uint(E1)) << 32),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (wave == 0)
-        __hip_atomic_store(reinterpret_cast<unsigned*>(&w.aggS[rowA + blk * D + d]),
-                           __float_as_uint(P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      *reinterpret_cast<f2*>(ah) = f2{E0, E1};
+  if constexpr (PASS != 3) {
+    if (active) {
+      *reinterpret_cast<f2*>(&w.aggH[(rowA + blk * D + d) * kMaxN + n0]) = f2{E0, E1};
       if (wave == 0) w.aggS[rowA + blk * D + d] = P;
     }
   }
   if constexpr (PASS == 3) {
-    // ---- publish this block's aggregate, then wait for the blocks before it ----
-    unsigned* fl = w.flags + (static_cast<long long>(b) * gridDim.x + gx) * w.nblk;
-    unsigned* dn = w.done + static_cast<long long>(b) * gridDim.x + gx;
-    // Publication without cache maintenance: the aggregates went out as agent-coherent
-    // stores (straight to the coherence point) and the barrier waits until every wave's
-    // stores are acknowledged, so thread 0's agent-coherent flag store follows them there;
-    // readers use agent-coherent loads for the flags and the aggregates.  (Agent-scope
-    // release / acquire fences — an L2 write-back and an L2 invalidate per workgroup — cost
-    // ~10 us at B = 1; the invalidates evicted the other blocks' operands.)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();  // also: every wave's E_j is in sH
-    if (tid == 0) __hip_atomic_store(&fl[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- publish this block's aggregate: the data is the flag ----
+    // Every value goes out as one aligned 8-byte {tag, value} granule by an agent-scope
+    // atomic store (an sc1 store to the coherence point); a reader polls the granules it
+    // needs until every tag is this launch's.  No drain, no separate flag, no second load
+    // round (cdna_hip_programming.md Guideline 16, R2): the round-2 form (aggregate stores,
+    // vmcnt(0), barrier, flag store, flag polls, then aggregate loads) spent ~11 us of the
+    // B = 1 scan between PASS 1 and PASS 2 (scripts/diag/stamp_scan.py).
+    // Granule layout [row][group][block][state 0..15 | delta sum][channel lane].
+    const unsigned tag = s_tag;
+    const unsigned long long tg = static_cast<unsigned long long>(tag) << 32;
+    unsigned long long* gb =
+        w.gran + ((static_cast<long long>(b) * gridDim.x + gx) * w.nblk) * ((kMaxN + 1) * 64);
+    unsigned long long* gmine = gb + static_cast<long long>(blk) * ((kMaxN + 1) * 64);
+    __hip_atomic_store(gmine + n0 * 64 + lane, tg | __float_as_uint(E0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gmine + (n0 + 1) * 64 + lane, tg | __float_as_uint(E1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0)
+      __hip_atomic_store(gmine + kMaxN * 64 + lane, tg | __float_as_uint(P), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     // this segment's entry offsets (composed by the 8 waves) into registers
     f2 Ew[kMaxN / 2];
 #pragma unroll
@@ -1204,88 +1233,51 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // Blocks are dispatched in order and the host launches this form only when the whole
-    // grid is co-resident, so every block waited on is running or done.  The spin is
-    // bounded anyway so a broken assumption can never hang the GPU: a block whose wait runs
-    // out sets the sticky error word (word 0 of the sync buffer, read on the host with
-    // vm_selective_scan_sync_status) and poisons its entry state with NaN, so every output
-    // and h_last it writes is NaN — never a plausible wrong value.
-    //
-    // Memory ordering (no fences; gfx942 / gfx950 memory model, LLVM AMDGPUUsage "Memory
-    // Model GFX942"): every cross-workgroup value — aggregates, flags, the done counter —
-    // is written and read ONLY with agent-scope atomics, which the backend emits as
-    // sc1 global stores / loads that go to the agent's coherence point instead of a
-    // (per-XCD, non-coherent) L2 line, so no L2 write-back or invalidate is needed for them
-    // to be seen.  Ordering: the publisher's s_waitcnt vmcnt(0) completes (acknowledges) its
-    // aggregate stores before s_barrier lets thread 0 store the flag; the reader issues its
-    // aggregate loads only after wave 0's flag loads have all returned 1 (control
-    // dependency) and the following s_barrier.  An agent-scope release / acquire fence pair would add a
-    // buffer_wbl2 / buffer_inv per workgroup for data that never sits in L2: measured
-    // 45 -> 134 us at B = 1 with them.
-    // Wave 0 polls the preceding blocks' flags in parallel (lane j: blocks j, j + 64, ...):
-    // each poll is a round trip to the coherence point, and polled one block after another
-    // by one thread they cost the last block of a B = 1 row ~13 sequential round trips.
-    if (wave == 0) {
-      bool timed_out = false;
+    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
+    // Wave w needs only its own states n0, n0 + 1 (and the delta sums) of each preceding
+    // block: 3 granules per block and lane, polled 8 blocks at a time.  Blocks are
+    // dispatched in order and the host launches this form only when the whole grid is
+    // co-resident, so every block waited on is running or done; the poll is bounded anyway
+    // so a broken assumption can never hang the GPU: a wave whose poll runs out sets the
+    // sticky error word and poisons its states with NaN, so every output and h_last of the
+    // block is NaN — never a plausible wrong value.
+    H0 *= kLog2e;  // log2 units
+    H1 *= kLog2e;
+    for (int r0 = 0; r0 < blk; r0 += kChW) {
+      const int nj = min(kChW, blk - r0);
+      unsigned long long g0[kChW], g1[kChW], gs[kChW];
       unsigned spins = 0;
       for (;;) {
-        bool seen = true;
-        for (int j = lane; j < blk; j += 64)
-          seen = seen && __hip_atomic_load(&fl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        if (__all(seen)) break;
-        if (++spins >= (1u << 22)) {
-          timed_out = true;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < kChW; ++j) {
+          const unsigned long long* gj =
+              gb + static_cast<long long>(r0 + (j < nj ? j : 0)) * ((kMaxN + 1) * 64);
+          g0[j] = __hip_atomic_load(gj + n0 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          g1[j] = __hip_atomic_load(gj + (n0 + 1) * 64 + lane, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+          gs[j] = __hip_atomic_load(gj + kMaxN * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int j = 0; j < kChW; ++j)
+          ok = ok && static_cast<unsigned>(g0[j] >> 32) == tag &&
+               static_cast<unsigned>(g1[j] >> 32) == tag && static_cast<unsigned>(gs[j] >> 32) == tag;
+        if (__all(ok)) break;
+        if (++spins >= (1u << 20)) {
+          if (lane == 0) __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          H0 = __builtin_nanf("");
+          H1 = __builtin_nanf("");
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      if (tid == 0) s_fail = timed_out ? 1 : 0;
-    }
-    if (tid == 0) {
-      const bool timed_out = s_fail != 0;
-      if (timed_out) __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // the last block past its wait resets the flags for the next launch
-      if (__hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          static_cast<unsigned>(w.nblk - 1)) {
-        for (int j = 0; j < w.nblk; ++j)
-          __hip_atomic_store(&fl[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();  // every wave's reads below follow the flags wave 0 saw
-    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
-    H0 *= kLog2e;  // log2 units
-    H1 *= kLog2e;
-    if (s_fail) {  // a timed-out wait: make every output of this block NaN
-      H0 = __builtin_nanf("");
-      H1 = __builtin_nanf("");
-    }
-    const int ci = tid >> 3;
-    for (int r0 = 0; r0 < blk; r0 += kChW) {
-      if (r0 > 0) __syncthreads();  // every wave is done reading the previous group
 #pragma unroll
       for (int j = 0; j < kChW; ++j) {
-        unsigned long long v = 0ull;
-        if (r0 + j < blk && ci < nch)
-          v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(
-                                    &w.aggH[(rowA + (r0 + j) * D + d0) * kMaxN + 2 * tid]),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sH[j][2 * (tid & 7)][ci] = __uint_as_float(static_cast<unsigned>(v));
-        sH[j][2 * (tid & 7) + 1][ci] = __uint_as_float(static_cast<unsigned>(v >> 32));
-      }
-      const int jj = r0 + (tid >> 6);
-      sS[tid >> 6][lane] =
-          jj < blk && lane < nch
-              ? __uint_as_float(__hip_atomic_load(
-                    reinterpret_cast<unsigned*>(&w.aggS[rowA + jj * D + d0 + lane]),
-                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-              : 0.0f;
-      __syncthreads();
-      const int nj = min(kChW, blk - r0);
-      for (int j = 0; j < nj; ++j) {
-        const float Sj = sS[j][lane];
-        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, sH[j][n0][lane]);
-        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, sH[j][n0 + 1][lane]);
+        if (j < nj) {  // (static register indices: a runtime bound would spill the arrays)
+          const float Sj = __uint_as_float(static_cast<unsigned>(gs[j]));
+          H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, __uint_as_float(static_cast<unsigned>(g0[j])));
+          H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, __uint_as_float(static_cast<unsigned>(g1[j])));
+        }
       }
     }
     __syncthreads();  // sH[0] is rewritten with the block entry
@@ -1516,7 +1508,7 @@ bool seq_supported(const ScanParams& p, int dtype) {
 template <typename T, bool SP, bool HZ, bool BC1, bool PAIR>
 static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
-  if (w.flags) {  // one launch: blocks hand their aggregates on through the sync flags
+  if (w.gran) {  // one launch: blocks hand their aggregates on through the sync buffer
     hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
                        p, w);
     return;
@@ -1549,10 +1541,11 @@ static void launch_chunk(const ScanParams& p, const ChunkWork& w, hipStream_t s)
 #undef VM_CH
 }
 
-// One-launch chunked form: the sticky error word (word 0; words 1-3 pad to 16 bytes), then
-// sync flags per (row, channel group, block) plus a counter per (row, channel group).  Used
-// when the caller passes a zeroed sync buffer this large and the whole grid fits one
-// workgroup per CU (so every block it waits on is resident).
+// One-launch chunked form: the sticky error word (word 0), the epoch (word 1: the tag of the
+// last launch that used the buffer) and the launch's start count (word 2), word 3 pad, then
+// one 8-byte {tag, value} granule per (row, channel group, block, state | delta sum,
+// channel).  Used when the caller passes a zeroed sync buffer this large and the whole grid
+// fits one workgroup per CU (so every block it waits on is resident).
 size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus) {
   const int S = segments_for(batch, dim, seqlen, segments, cus);
   if (S <= 1) return 0;
@@ -1560,7 +1553,7 @@ size_t seq_sync_bytes(int batch, int dim, int seqlen, int segments, int cus) {
   chunk_geometry(seqlen, S, &T, &nblk);
   const size_t groups = (dim + 63) / 64;
   return kSyncHeaderWords * sizeof(unsigned) +
-         static_cast<size_t>(batch) * groups * (nblk + 1) * sizeof(unsigned);
+         static_cast<size_t>(batch) * groups * nblk * (kMaxN + 1) * 64 * sizeof(unsigned long long);
 }
 
 bool seq_pair_supported(const ScanParams& p, int dtype, int segments, size_t workspace_bytes) {
@@ -1584,8 +1577,9 @@ void seq_launch(const ScanParams& p, int dtype, int segments, void* workspace,
     if (sync && sync_bytes >= seq_sync_bytes(p.batch, p.dim, p.seqlen, segments, cus) &&
         grid <= dev_cus) {
       w.err = static_cast<unsigned*>(sync);
-      w.flags = w.err + kSyncHeaderWords;
-      w.done = w.flags + static_cast<size_t>(p.batch) * ((p.dim + 63) / 64) * w.nblk;
+      w.epoch = w.err + 1;
+      w.done = w.err + 2;
+      w.gran = reinterpret_cast<unsigned long long*>(w.err + kSyncHeaderWords);
     }
     const size_t nb = static_cast<size_t>(p.batch) * w.nblk;
     w.segE = static_cast<float*>(workspace);

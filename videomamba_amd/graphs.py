@@ -93,7 +93,7 @@ class StreamingChunkGraph:
         self._plist = None
         self._tpos_offset = None  # temporal offset whose embedding slice static_tpos holds
         self._ws = None  # scan scratch owned by the captured graphs
-        self._sync = None  # the one-launch scan's sync flags (zeroed; replays leave them zeroed)
+        self._sync = None  # the one-launch scan's sync buffer (zeroed once; replays keep it valid)
         self._cnt = None  # vm_linear_add_norm_fwd hand-off counters (zeroed, left zeroed)
 
     # ------------------------------------------------------------------ state
@@ -148,13 +148,13 @@ class StreamingChunkGraph:
     def _workspace(self) -> Tensor:
         """Kernel scratch (segmented scan, conv_proj partials, pooling sums) sized for the
         largest consumer of either chunk kind; allocated once per capture set, owned by this
-        runner (with the one-launch scan's sync flags)."""
+        runner (with the one-launch scan's sync buffer)."""
         m = self.model
         gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
         need, sync_need = chunk_workspace_bytes(m, self.batch, self.tt, gh, gw)
         if self._ws is None or self._ws.numel() < max(need, 1):
             self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
-        # the one-launch scan's sync flags: zeroed once, left zeroed by every replay
+        # the one-launch scan's sync buffer: zeroed once, left valid for the next by every replay
         if self._sync is None or self._sync.numel() < max(sync_need, 1):
             self._sync = torch.zeros(max(sync_need, 4096), dtype=torch.uint8, device=self.device)
         Lp = (self.tt * gh * gw + 1 + 7) // 8 * 8

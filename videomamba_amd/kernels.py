@@ -166,9 +166,10 @@ class sync_override:
 
 
 def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
-    """The one-launch scan's sync buffer: zero-filled when allocated, left zeroed by every
-    launch, one per (device, stream) so no two concurrent launches share it; grown (a new
-    zeroed buffer) when a shape needs more."""
+    """The one-launch scan's sync buffer: zero-filled when allocated, left valid for the next
+    launch by every launch (epoch-tagged hand-off granules, ABI v9), one per (device, stream)
+    so no two concurrent launches share it; grown (a new zeroed buffer) when a shape needs
+    more."""
     if nbytes <= 0:
         return None
     ov = _SYNC_OVERRIDE[0]
@@ -182,7 +183,7 @@ def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tens
     return buf
 
 
-SYNC_HEADER_BYTES = 16  # the sync buffer's sticky error word + padding (ABI v8)
+SYNC_HEADER_BYTES = 16  # error word, epoch, start count, pad (ABI v9)
 
 
 def scan_sync_status(buf: Tensor) -> int:
