@@ -235,7 +235,8 @@ def b1_kernel_rooflines(device, reps=50):
     launch stream, against its algorithmic bytes (HBM-bound kernels) or flops (GEMMs).
     Stages: add+RMSNorm (x bf16 + residual fp32 in, residual fp32 + normed bf16 out),
     in_proj GEMM, fused conv+x_proj+dt_proj (+ conv state out), the scan (scan_roofline at
-    B=1: the segmented chunk form), out_proj GEMM."""
+    B=1: the segmented chunk form), out_proj GEMM — each the kernel the mixer runs for a
+    one-clip chunk (the projections on the row-invariant HIP GEMM, clips=1)."""
     from videomamba_amd import kernels as K
     from videomamba_amd.layers import round_up
     from videomamba_amd.mamba_simple import Mamba, _linear
@@ -277,7 +278,8 @@ def b1_kernel_rooflines(device, reps=50):
     with torch.no_grad():
         hbm("add_norm", _event_us(lambda: K.add_norm_raw(x, res, w32, None, hn, res, Lp, C, 1e-5,
                                                          True, stream), reps), 12 * Lp * C)
-        mfma("in_proj", _event_us(lambda: _linear(hn, mx.in_proj.weight), reps),
+        hn.normal_()
+        mfma("in_proj", _event_us(lambda: _linear(hn, mx.in_proj.weight, clips=1), reps),
              2 * Lp * C * 2 * Dm)
         hbm("conv_proj", _event_us(lambda: K.conv_proj_raw(
             xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs_in, (cs_in.stride(0), cs_in.stride(1)),
@@ -287,7 +289,7 @@ def b1_kernel_rooflines(device, reps=50):
         sc = scan_roofline(1, reps, device, "tm")
         out["scan"] = {k: sc[k] for k in ("avg_us", "bound", "achieved", "peak", "unit", "frac")}
         out["scan"]["us"] = out["scan"].pop("avg_us")
-        mfma("out_proj", _event_us(lambda: _linear(y, mx.out_proj.weight), reps),
+        mfma("out_proj", _event_us(lambda: _linear(y, mx.out_proj.weight, clips=1), reps),
              2 * Lp * Dm * C)
     out["layer_us_sum"] = round(sum(v["us"] for v in out.values()), 2)
     out["shape"] = f"VideoMamba-M layer, B=1, L={L} (padded {Lp}), bf16, stages launched alone"
