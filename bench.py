@@ -375,6 +375,8 @@ def cpu_baseline(cfg, threads):
     return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
             "cores": threads, "kind": "port", "cpu_model": model,
             "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+            "threads_policy": "min(16, affinity): a one-GPU box's CPU share; os.cpu_count() "
+                              "(BASELINE.md's recipe) counts the whole shared host",
             "calibration": cal,
             # the reference's own CPU path on these cores, scaled by the one-session
             # oracle/reference time ratio of the calibration record (the port is faster)

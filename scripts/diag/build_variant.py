@@ -84,6 +84,13 @@ VARIANTS = {
                   "  else VM_LDMA_TILE(64, 64, 3)")],
     "ldma_o2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3)",
                  "  else VM_LDMA_TILE(64, 64, 2)")],
+    # LDS-DMA GEMM tile alternatives for in_proj (N >= 1024) and out_proj at B = 1
+    "ldma_i128x64": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
+                      "  if (p.n >= 1024) VM_LDMA_TILE(128, 64, 3)")],
+    "ldma_i64x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
+                      "  if (p.n >= 1024) VM_LDMA_TILE(64, 128, 3)")],
+    "ldma_o64n4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3)",
+                    "  else VM_LDMA_TILE(64, 64, 4)")],
     # one-launch chunked scan: the preceding blocks' flags polled one after another by
     # thread 0 (the round-2 form) instead of in parallel by wave 0
     "poll_serial": [("vm_scan_seq.hip", "        for (int j = lane; j < blk; j += 64)",

@@ -11,6 +11,10 @@ name = sys.argv[1]
 if name != "product":
     import videomamba_amd._lib as L
     L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", name, "libvideomamba_hip.so")
+    abi = [a for a in sys.argv[2:] if a.startswith("--abi=")]
+    if abi:  # an older build (same entry points) for a same-box A/B
+        L.ABI_VERSION = int(abi[0].split("=")[1])
+        sys.argv = [a for a in sys.argv if not a.startswith("--abi=")]
 import torch  # noqa: E402
 from bench import scan_roofline  # noqa: E402
 

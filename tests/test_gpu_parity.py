@@ -14,6 +14,7 @@ import torch.nn.functional as F
 
 from conftest import load_golden
 from oracle import videomamba_oracle as orc
+from videomamba_amd import _lib
 from videomamba_amd import kernels as K
 from videomamba_amd import options
 
@@ -485,6 +486,40 @@ def test_add_norm_matches_oracle(cols, is_rms, xdt, rdt):
     assert y.dtype == xdt and r.dtype == rr.dtype
     _close(y, ry, 1e-5 if xdt == torch.float32 else 1e-2)
     _close(r, rr, 1e-6)
+
+
+@pytest.mark.parametrize("rows,cols", [(3144, 576), (37, 192), (5, 1000), (9, 1024), (3, 8)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_add_rms_bf16_fast_path_matches_generic_form(rows, cols, with_res):
+    """vm_add_norm_fwd's branch-free bf16 / fp32-residual RMSNorm kernel (add_rms_bf16_kernel:
+    the block's add+norm) against the same call routed to the dtype-generic vector kernel
+    (residual_out requested in bf16 selects it; everything else identical): the fp32
+    residual sums, hence the statistics, are the same, so the bf16 outputs must agree
+    bitwise; and against the oracle at the bf16 tolerance."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device=DEV, generator=g).to(torch.bfloat16)
+    res = torch.randn(rows, cols, device=DEV, generator=g) if with_res else None
+    w = torch.randn(cols, device=DEV, generator=g)
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = {}
+    for ro_dt in (torch.float32, torch.bfloat16):
+        y = torch.empty(rows, cols, device=DEV, dtype=torch.bfloat16)
+        ro = torch.empty(rows, cols, device=DEV, dtype=ro_dt)
+        rc = lib.vm_add_norm_fwd(x.data_ptr(), K.dtype_code(x.dtype),
+                                 res.data_ptr() if res is not None else None,
+                                 K.dtype_code(torch.float32), w.data_ptr(), None, y.data_ptr(),
+                                 K.dtype_code(y.dtype), ro.data_ptr(), K.dtype_code(ro_dt),
+                                 rows, cols, 1e-5, 1, stream)
+        assert rc == 0, lib.vm_last_error()
+        outs[ro_dt] = (y, ro)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[torch.float32][0], outs[torch.bfloat16][0])
+    assert torch.equal(outs[torch.float32][1].to(torch.bfloat16), outs[torch.bfloat16][1])
+    ry, rr = orc.add_norm(x.cpu(), None if res is None else res.cpu(), w.cpu(), None, 1e-5,
+                          True, True, True)
+    _close(outs[torch.float32][0], ry, 1e-2)
+    _close(outs[torch.float32][1], rr, 1e-6)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])

@@ -42,6 +42,88 @@ __device__ __forceinline__ void store4_dyn(void* p, long long i, int dtype, cons
   }
 }
 
+// The block's common case — bf16 x / out, fp32 residual in / out, RMSNorm, no bias — with
+// every access a branch-free buffer access over the wave's own row (chunks past `cols` get
+// an out-of-range offset: they read 0 and store nothing) and every load of the row issued
+// before the first use.  The dtype-generic form below puts each access behind the dtype
+// and column-range branches, and hipcc waits vmcnt(0) at their joins: a chain of dependent
+// round trips per row that set the B = 1 chunk's add+norm at ~7 us.  Same arithmetic in
+// the same order as add_norm_vec_kernel (bit-identical outputs).
+constexpr int kNormOut = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  void* ub = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, 0, bytes, 0x00020000);
+}
+template <int CPL, bool RES, bool RO>
+__global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int lane = threadIdx.x & 63;
+  const long long base = row * p.cols;
+  const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, p.cols * 2);
+  const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, p.cols * 4);
+  const auto wr = norm_row_rsrc(p.w, p.cols * 4);
+  const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, p.cols * 2);
+  const auto ror = norm_row_rsrc(RO ? static_cast<float*>(p.res_out) + base : p.w, p.cols * 4);
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float v4f;
+  auto off = [&](int j, int es) {
+    int o = lane * 4 + 256 * j < p.cols ? (lane * 4 + 256 * j) * es : kNormOut;
+    asm volatile("" : "+v"(o));  // a select, not a branch around the access
+    return o;
+  };
+  uint32_t xq[CPL][2];
+  v4f rq[CPL], wq[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
+    xq[j][0] = q[0];
+    xq[j][1] = q[1];
+    if constexpr (RES) rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+    wq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(wr, off(j, 4), 0, 0));
+  __builtin_amdgcn_sched_barrier(0);  // all of the row's loads in flight before any use
+  float v[CPL][4];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    v[j][0] = __uint_as_float(xq[j][0] << 16); v[j][1] = __uint_as_float(xq[j][0] & 0xffff0000u);
+    v[j][2] = __uint_as_float(xq[j][1] << 16); v[j][3] = __uint_as_float(xq[j][1] & 0xffff0000u);
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[j][i] += rq[j][i];
+    }
+  }
+  float sq = 0.0f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
+  const float rstd = rsqrtf(wave_sum(sq) / p.cols + p.eps);
+  const float mean = 0.0f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    float y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = (v[j][i] - mean) * rstd * wq[j][i];
+    typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
+    const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
+                                     (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
+                    static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
+                                     (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
+    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);
+    if constexpr (RO) {
+      typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+      const v4i r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
+                      static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
+      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);
+    }
+  }
+}
+
 // Vectorised form for cols % 4 == 0 and 16-byte aligned rows: lane owns 4-element
 // chunks lane*4 + 256*j (8-byte bf16 / 16-byte fp32 accesses).
 template <int CPL>  // chunks per lane (cols <= 256 * CPL)
@@ -518,6 +600,26 @@ extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual,
   const bool vec = cols % 4 == 0 && vmhost::aligned16(x) && vmhost::aligned16(out) &&
                    vmhost::aligned16(weight) && (!residual || vmhost::aligned16(residual)) &&
                    (!residual_out || vmhost::aligned16(residual_out));
+  if (vec && is_rms && !bias && x_dtype == VM_DTYPE_BF16 && out_dtype == VM_DTYPE_BF16 &&
+      (!residual || res_dtype == VM_DTYPE_F32) && (!residual_out || res_out_dtype == VM_DTYPE_F32) &&
+      cols <= 256 * 4) {
+    const int cpl = (cols + 255) / 256;
+#define VM_RMS_BF16(CPLV)                                                                   \
+  if (residual && residual_out)                                                             \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, true>), grid, dim3(256), 0, s, p);   \
+  else if (residual)                                                                        \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, false>), grid, dim3(256), 0, s, p);  \
+  else if (residual_out)                                                                    \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, false, true>), grid, dim3(256), 0, s, p);  \
+  else                                                                                      \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, false, false>), grid, dim3(256), 0, s, p);
+    if (cpl <= 1) { VM_RMS_BF16(1) }
+    else if (cpl <= 2) { VM_RMS_BF16(2) }
+    else if (cpl <= 3) { VM_RMS_BF16(3) }
+    else { VM_RMS_BF16(4) }
+#undef VM_RMS_BF16
+    return vmhost::launch_status("vm_add_norm_fwd");
+  }
   if (vec) {
     const int cpl = (cols + 255) / 256;
     if (cpl <= 1) hipLaunchKernelGGL(add_norm_vec_kernel<1>, grid, dim3(256), 0, s, p);
