@@ -12,6 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 # name -> [(file, old, new)]
 VARIANTS = {
+    # the sources as they stand when built (a same-box baseline for a change under test)
+    "base": [],
     # scans without the one-step-early gate factor (kSeqGateAhead)
     "sc_nogate": [("vm_scan_seq.hip", "constexpr bool kSeqGateAhead = true;", "constexpr bool kSeqGateAhead = false;")],
     # single-pass scan without the one-step-early delta (kSeqDeltaAhead)

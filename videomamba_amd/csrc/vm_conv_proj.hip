@@ -33,6 +33,7 @@ namespace vm {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 struct ConvProjParams {
   const bf16_t* xz; const float* cw; const float* cb;
@@ -101,7 +102,10 @@ __device__ __forceinline__ void dt_phase_half(const ConvProjParams& p, const bf1
 // 1 W_x staging loads, 2 x_proj MFMAs, 4 u stores, 8 conv window loads, 16 loop barriers.
 // SPD: the dt epilogue emits softplus(dt + bias) (see the header)
 template <bool DT, int NB, int EXP = 0, bool SPD = false>  // DT: also run dt_proj here; NB = e_pad / 16 blocks
-__global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) {
+// 3 waves per SIMD = the 3 workgroups per CU the LDS budget allows (unbounded, hipcc spends
+// ~176 registers on the in-flight prefetch and runs 2)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void conv_proj_kernel(const ConvProjParams p) {
   // sU: W_x chunk (<= 128 rows x kCPPad) / x_dbl tile (64 x 2*kCPPad); with DT also the
   // per-wave dt staging (4 x 64 x kCPPad)
   constexpr int kSU = 2 * kCPTok * kCPPad;  // with DT the dt staging is 4 waves x 32 rows
@@ -131,49 +135,129 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
   const int rr = rva ? rowa : p.rows - 1;
   const int b = rr / p.lp;
   const int ta = rr - b * p.lp;  // step of the first row; window rows ta-3 .. ta+1
-  const bf16_t* xrow = p.xz + b * p.xz_sb;
-  auto load_win = [&](int c, uint4 (&w)[5]) {
+  // Every load of the sweep is unconditional, so none sits behind a branch whose join makes
+  // hipcc drain vmcnt: window rows outside [0, seqlen) read a clamped (valid) row and are
+  // zeroed at use, W_x padding pieces re-read its last row into LDS rows nothing reads.
+  // Round 2's per-row "load or zero" select and runtime-bound W_x staging loop compiled to
+  // a load + vmcnt(0) round trip per piece, exposing the window prefetch and three W_x
+  // latencies in every chunk.  Both are buffer loads: a per-lane 32-bit offset fixed for
+  // the sweep plus the chunk's channel offset in a scalar register.
+  // x window rows: the workgroup's 64 rows touch sequences b0 and b0 + 1 at most (out_len
+  // is even and a row pair never straddles one); the host checks the offsets fit 31 bits
+  const int b0 = row0 / p.lp;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.xz + (long long)b0 * p.xz_sb), 0,
+                                                    0x7fffffff, 0x00020000);
+  int woff[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int te = ta - 3 + j;
-      w[j] = (te >= 0 && te < p.seqlen)
-                 ? *reinterpret_cast<const uint4*>(xrow + te * p.xz_sl + c)
-                 : make_uint4(0, 0, 0, 0);
-    }
+  for (int j = 0; j < 5; ++j) {
+    const int te = min(max(ta - 3 + j, 0), p.seqlen - 1);
+    woff[j] = static_cast<int>(((long long)(b - b0) * p.xz_sb + (long long)te * p.xz_sl + cg * 8) * 2);
+  }
+  auto load_win = [&](int c0, uint4 (&w)[5]) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      w[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, woff[j], c0 * 2, 0));
   };
+  unsigned win_ok = 0;  // bit j: window row ta - 3 + j lies in [0, seqlen)
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    if (ta - 3 + j >= 0 && ta - 3 + j < p.seqlen) win_ok |= 1u << j;
+  // conv state (B, D, W) of fp32 or bf16 through one buffer resource (its size is checked
+  // on the host to fit 31-bit offsets)
+  const bool cs_bf16 = p.csi_dtype == VM_DTYPE_BF16;
+  const auto csr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.csi), 0,
+      p.csi ? static_cast<int>(((long long)(p.batch - 1) * p.csi_sb + (long long)(D - 1) * p.csi_sd + p.width) *
+                               (cs_bf16 ? 2 : 4))
+            : 0,
+      0x00020000);
+  auto cs_off = [](bool ok, int off) {
+    off = ok ? off : 0x7ffffff0;  // past the range: the load reads 0
+    asm volatile("" : "+v"(off));  // keep it a select (seen through, hipcc branches per load)
+    return off;
+  };
+  // W_x chunk [e_pad][64] as 16-B pieces, loaded one chunk ahead into registers and
+  // written to LDS after the previous chunk's MFMAs
+  constexpr int kWxIt = (NB * 128 + 255) / 256;
+  uint4 wreg[kWxIt];
+  const auto wxr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.wx), 0,
+                                                     NB * 16 * D * 2, 0x00020000);
+  int xoff[kWxIt];
+#pragma unroll
+  for (int i = 0; i < kWxIt; ++i) {
+    const int idx = tid + 256 * i;
+    xoff[i] = (min(idx >> 3, NB * 16 - 1) * D + (idx & 7) * 8) * 2;
+  }
+  auto load_wx = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < kWxIt; ++i)
+      wreg[i] = (EXP & 1) ? make_uint4(i, c0, 0, 0)
+                          : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wxr, xoff[i], c0 * 2, 0));
+  };
+
+  // u rows of this workgroup (the range ends at the last valid row): the stores need no
+  // branch, so the counted wait for the window prefetch at the end of a chunk can leave
+  // them in flight
+  const auto ur = __builtin_amdgcn_make_buffer_rsrc(
+      p.u + (long long)row0 * p.u_sl, 0, static_cast<int>(min(kCPTok, p.rows - row0) * p.u_sl * 2),
+      0x00020000);
+  const int u_row = static_cast<int>(p.u_sl * 2);
+  const int uoff = (2 * tg * static_cast<int>(p.u_sl) + cg * 8) * 2;
 
   f32x4 acc[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 cur[5], nxt[5];
-  load_win(cg * 8, cur);
+  uint4 wa[5], wb[5];
+  load_wx(0);
+  load_win(0, wa);
   __syncthreads();  // sW ready
-  for (int c0 = 0; c0 < D; c0 += kCPCh) {
+  // one 64-channel chunk; cur holds its window rows, nxt receives the next chunk's
+  auto chunk = [&](int c0, uint4 (&cur)[5], uint4 (&nxt)[5]) {
     const int c = c0 + cg * 8;
-    if (!(EXP & 8) && c0 + kCPCh < D) load_win(c + kCPCh, nxt);  // prefetch the next window
-    // ---- stage W_x[:, c0:c0+64] ----
-    for (int idx = tid; idx < p.e_pad * 8; idx += 256) {
-      const int n = idx >> 3, q = idx & 7;
-      *reinterpret_cast<uint4*>(&sB[n * kCPPad + q * 8]) =
-          (EXP & 1) ? make_uint4(n, q, 0, 0)
-                    : *reinterpret_cast<const uint4*>(p.wx + (long long)n * D + c0 + q * 8);
+    // ---- stage W_x[:, c0:c0+64] (rows < 128 <= kSU / kCPPad) ----
+#pragma unroll
+    for (int i = 0; i < kWxIt; ++i) {
+      const int idx = tid + 256 * i;
+      *reinterpret_cast<uint4*>(&sB[(idx >> 3) * kCPPad + (idx & 7) * 8]) = wreg[i];
+    }
+    // prefetch the next chunk (the last chunk re-reads its own: cache hits, no branch)
+    const int cn = min(c0 + kCPCh, D - kCPCh);
+    load_wx(cn);
+    if (!(EXP & 8)) load_win(cn, nxt);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {  // zero rows outside the sequence (a mask, not a branch)
+      const uint32_t m = 0u - ((win_ok >> j) & 1u);
+      cur[j].x &= m; cur[j].y &= m; cur[j].z &= m; cur[j].w &= m;
     }
     // ---- conv + silu, one channel pair (one packed word of each window row) at a time ----
     if (ta < 3 && p.csi) {  // window reaches before the sequence start: conv state
-      // a row's 8 state loads are issued together, then packed
+      // rows te < 0 of the window are zero here; the state taps are OR-ed in, each a buffer
+      // load whose offset is out of range (reads 0) where the row needs none: no branch
+      // inside this (rare) one, a row's 8 loads issued together
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int te = ta - 3 + j;
         const int sj = p.width + te;
-        if (te < 0 && sj >= 0) {
-          const long long base = b * p.csi_sb + (long long)c * p.csi_sd + sj;
+        const bool ok = te < 0 && sj >= 0;
+        const int base = b * (int)p.csi_sb + c * (int)p.csi_sd + sj;
+        uint32_t pk[4];
+        if (cs_bf16) {
+          uint32_t h[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            h[k] = __builtin_amdgcn_raw_buffer_load_b16(csr, cs_off(ok, (base + k * (int)p.csi_sd) * 2), 0, 0);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pk[k] = h[2 * k] | (h[2 * k + 1] << 16);
+        } else {
           float sv[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) sv[k] = load_dyn(p.csi, base + k * p.csi_sd, p.csi_dtype);
-          cur[j] = make_uint4(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]), pack2(sv[4], sv[5]),
-                              pack2(sv[6], sv[7]));
+          for (int k = 0; k < 8; ++k)
+            sv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csr, cs_off(ok, (base + k * (int)p.csi_sd) * 4), 0, 0));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pk[k] = pack2(sv[2 * k], sv[2 * k + 1]);
         }
+        cur[j].x |= pk[0]; cur[j].y |= pk[1]; cur[j].z |= pk[2]; cur[j].w |= pk[3];
       }
     }
     const bool la = rva && ta < p.seqlen, lb = rvb && ta + 1 < p.seqlen;
@@ -200,8 +284,10 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
     }
     const uint4 qa = make_uint4(pa[0], pa[1], pa[2], pa[3]);
     const uint4 qb = make_uint4(pb[0], pb[1], pb[2], pb[3]);
-    if (!(EXP & 4) && rva) *reinterpret_cast<uint4*>(p.u + (long long)rowa * p.u_sl + c) = qa;
-    if (!(EXP & 4) && rvb) *reinterpret_cast<uint4*>(p.u + (long long)(rowa + 1) * p.u_sl + c) = qb;
+    if (!(EXP & 4)) {  // unconditional: rows past the end fall outside ur's range
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, qa), ur, uoff + c0 * 2, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, qb), ur, uoff + c0 * 2 + u_row, 0, 0);
+    }
     *reinterpret_cast<uint4*>(&sA[(2 * tg) * kCPPad + cg * 8]) = qa;
     *reinterpret_cast<uint4*>(&sA[(2 * tg + 1) * kCPPad + cg * 8]) = qb;
     if (!(EXP & 16)) __syncthreads();
@@ -218,8 +304,13 @@ __global__ __launch_bounds__(256) void conv_proj_kernel(const ConvProjParams p) 
       }
     }
     if (!(EXP & 16)) __syncthreads();
+  };
+  // (a two-chunk trip with the window buffers swapping roles saves the copy below but needs
+  // ~220 registers: 2 waves per SIMD instead of 3)
+  for (int c0 = 0; c0 < D; c0 += kCPCh) {
+    chunk(c0, wa, wb);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) cur[j] = nxt[j];
+    for (int j = 0; j < 5; ++j) wa[j] = wb[j];
   }
 
   // ---- x_dbl: bf16 tile [64][e_pad] in sU (stride kCPPad*2), x_dbl[:, :R] -> sA ----
@@ -431,6 +522,16 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);
     else conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
     return vmhost::launch_status("vm_conv_proj_fwd");
+  }
+  // the wide kernel's buffer offsets: x rows of two adjacent sequences, the conv state
+  constexpr long long kOff31 = 0x7fffff00LL;
+  const int cs_es = cs_in && cs_in_dtype == VM_DTYPE_BF16 ? 2 : 4;
+  if ((xz_sb + (long long)seqlen * xz_sl + dim) * 2 > kOff31 ||
+      (cs_in && ((long long)(batch - 1) * csi_sb + (long long)(dim - 1) * csi_sd + width) * cs_es > kOff31) ||
+      (long long)kCPTok * u_sl * 2 > kOff31) {
+    vmhost::set_error("vm_conv_proj_fwd: batch > %d needs a sequence of xz under 1 GiB "
+                      "(31-bit buffer offsets)", kSkMaxBatch);
+    return VM_E_INVALID;
   }
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, p); };
   switch (e_pad / 16) {  // x_proj output blocks
