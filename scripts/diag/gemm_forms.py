@@ -1,4 +1,4 @@
-"""Library GEMM forms for the B = 448 projections (in_proj M x 576 -> 2304, out_proj
+"""GEMM forms for the B = 448 projections (in_proj M x 576 -> 2304, out_proj
 M x 1152 -> 576, M = 448 * 3144): torch.mm against w.t() (the product), against a
 pre-transposed weight, the transposed product (w @ x^T), rocBLAS instead of hipBLASLt.
     python scripts/diag/gemm_forms.py"""
@@ -9,6 +9,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 from bench import _event_us  # noqa: E402
+from videomamba_amd import kernels as VK  # noqa: E402
+from videomamba_amd.gemm_tuning import tuned  # noqa: E402
 
 dev = torch.device("cuda", 0)
 M = 448 * 3144
@@ -35,6 +37,17 @@ for name, K, N in (("in_proj", 576, 2304), ("out_proj", 1152, 576)):
             res[f"{lib}:{fname}_us"] = round(us, 1)
             res[f"{lib}:{fname}_tflops"] = round(flop / us / 1e6, 1)
     torch.backends.cuda.preferred_blas_library("cublaslt")
+    with tuned():
+        us = _event_us(lambda: torch.mm(x, w.t(), out=out), 10)
+    res["tuned_mm_us"] = round(us, 1)
+    # the HIP LDS-DMA GEMM (vm_gemm.hip) over row slabs that keep its 31-bit offsets
+    slab = (1 << 30) // (K * 2) // 128 * 128
+    def hip():
+        for r0 in range(0, M, slab):
+            VK.linear(x[r0:r0 + slab], w, out=out[r0:r0 + slab])
+    us = _event_us(hip, 10)
+    res["hip_dma_us"] = round(us, 1)
+    res["hip_dma_tflops"] = round(flop / us / 1e6, 1)
     # halves of M (two launches): does a smaller M pick another tile?
     h = M // 2
     us = _event_us(lambda: (torch.mm(x[:h], w.t(), out=out[:h]), torch.mm(x[h:], w.t(), out=out[h:])), 10)
