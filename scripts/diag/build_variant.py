@@ -89,6 +89,10 @@ VARIANTS = {
     # LDS-DMA GEMM tile alternatives for in_proj (N >= 1024) and out_proj at B = 1
     "ldma_i128x64": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
                       "  if (p.n >= 1024) VM_LDMA_TILE(128, 64, 3)")],
+    "ldma_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
+                       "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2)")],
+    "ldma_i128x256": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
+                       "  if (p.n >= 1024) VM_LDMA_TILE(128, 256, 2)")],
     "ldma_i64x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)",
                       "  if (p.n >= 1024) VM_LDMA_TILE(64, 128, 3)")],
     "ldma_o64n4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3)",

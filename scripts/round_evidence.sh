@@ -29,6 +29,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -k 10 600 python scripts/bench_long_video.py > $O/long_video.json 2> $O/long_video.err || { echo long video failed; tail $O/long_video.err; exit 1; }
 cat $O/long_video.json
+timeout -k 10 300 python bench.py --config ti8 --full-sequence --batch 512 --no-b1 --no-cpu-baseline > $O/c2_ti8.json 2> $O/c2.err || { echo c2 failed; tail $O/c2.err; exit 1; }
+timeout -k 10 300 python bench.py --config m32 --no-b1 --no-cpu-baseline > $O/m32.json 2> $O/m32.err || { echo m32 failed; tail $O/m32.err; exit 1; }
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_b1_graph -o run -- python -u scripts/diag/b1_chunk_graph.py 20 > $O/prof_b1_graph.log 2>&1 || { echo b1 prof failed; tail $O/prof_b1_graph.log; exit 1; }
 grep "graph replays" $O/prof_b1_graph.log
 echo evidence done
