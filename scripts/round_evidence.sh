@@ -3,8 +3,8 @@
 # command, kernel stats of the scan microbench alone at the bench shape (the roofline
 # kernel), FETCH_SIZE / WRITE_SIZE / SQ counter passes on that microbench, the same
 # FETCH/WRITE passes on a calibration kernel with the scan's access pattern and a known byte
-# count (tools/probes/scan_lab calib), the C5 long-video run and the B=1 graph-replay chunk
-# profile.  PART=1: bench + its profile; PART=2: the rest (one gpurun call each).
+# count (tools/probes/scan_lab calib), the C5 long-video run, the C2 (Ti-8f full sequence)
+# and M-32f bench lines and the B=1 graph-replay chunk profile.  PART=1: bench + its profile; PART=2: the rest (one gpurun call each).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r03}
