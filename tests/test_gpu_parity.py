@@ -719,6 +719,49 @@ def test_conv_proj_split_k_conv_state_out():
         assert torch.equal(got[1], want), L
 
 
+@pytest.mark.parametrize("width", [2, 3, 4])
+@pytest.mark.parametrize("state_dtype", [torch.float32, torch.bfloat16, None])
+def test_conv_proj_wide_kernel_widths_states_short_sequences(width, state_dtype):
+    """The wide conv_proj kernel (batch > 8; unconditional buffer loads of clamped window
+    rows zeroed by mask, conv-state taps OR-ed in from range-checked loads, u rows as
+    range-checked buffer stores) against the oracle's causal conv for every batch row:
+    conv widths 2-4 (state taps that do not exist for a narrow kernel), fp32 / bf16 / no
+    conv state, sequences shorter than the kernel, shorter than a workgroup's 64 rows (one
+    workgroup spans many sequences) and not aligned to it; x_dbl within one bf16 rounding
+    of the fp32 projection of the kernel's own u; padding rows zero."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(width * 7 + (0 if state_dtype is None else state_dtype.itemsize))
+    m = Mamba(d_model=96, d_state=16, d_conv=width, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    Dm, E, R, W = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    _, _, _, cw, cb = m._fp32_params()
+    wx_pad, _ = m._padded_proj_weights()
+    st = torch.cuda.current_stream().cuda_stream
+    bsz = 11
+    for L in (2, 3, 37, 101):
+        Lp = (L + 7) // 8 * 8
+        n = bsz * Lp
+        xz3 = torch.randn(bsz, Lp, 2 * Dm, device=DEV).to(torch.bfloat16)
+        xz3[:, L:] = 0
+        xz = xz3.reshape(n, 2 * Dm)
+        cs = None if state_dtype is None else torch.randn(bsz, Dm, W, device=DEV).to(state_dtype)
+        u = torch.full((n, Dm), float("nan"), device=DEV, dtype=torch.bfloat16)
+        xd = torch.full((n, E), float("nan"), device=DEV, dtype=torch.bfloat16)
+        K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs,
+                        (Dm * W, W) if cs is not None else (0, 0), None, (0, 0), wx_pad, E,
+                        None, R, u, (Lp * Dm, Dm), xd, (Lp * E, E), None, None, Lp, bsz, Dm,
+                        L, W, st)
+        torch.cuda.synchronize()
+        u3 = u.view(bsz, Lp, Dm)
+        assert not u3[:, L:].float().abs().any(), L  # padding rows: zeros, written
+        ref_u, _ = orc.causal_conv1d(xz3[:, :L, :Dm].transpose(1, 2).cpu(), cw.cpu(), cb.cpu(),
+                                     True, None if cs is None else cs.cpu())
+        got = u3[:, :L].transpose(1, 2).float().cpu()
+        tol = ref_u.abs() * 2.0 ** -7 + 1e-5  # one bf16 rounding of the fp32 conv
+        assert ((got - ref_u).abs() <= tol).all(), (L, (got - ref_u).abs().max())
+        want_xd = F.linear(u.float(), m.x_proj.weight.float())
+        assert ((xd.float() - want_xd).abs() <= want_xd.abs() * 2.0 ** -7 + 1e-3).all(), L
+
+
 @pytest.mark.parametrize("d_model", [576, 96])
 def test_conv_proj_split_k_matches_wide_kernel(d_model):
     """vm_conv_proj_fwd runs the split-K form (fixed 128-channel splits of the x_proj

@@ -142,8 +142,9 @@ void conv_proj_kernel(const ConvProjParams p) {
   // a load + vmcnt(0) round trip per piece, exposing the window prefetch and three W_x
   // latencies in every chunk.  Both are buffer loads: a per-lane 32-bit offset fixed for
   // the sweep plus the chunk's channel offset in a scalar register.
-  // x window rows: the workgroup's 64 rows touch sequences b0 and b0 + 1 at most (out_len
-  // is even and a row pair never straddles one); the host checks the offsets fit 31 bits
+  // x window rows: the workgroup's 64 rows touch sequences b0 .. b0 + 63 / out_len + 1
+  // (a row pair never straddles two: out_len is even); the host checks the offsets fit
+  // 31 bits
   const int b0 = row0 / p.lp;
   const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.xz + (long long)b0 * p.xz_sb), 0,
                                                     0x7fffffff, 0x00020000);
@@ -523,10 +524,11 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     else conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
     return vmhost::launch_status("vm_conv_proj_fwd");
   }
-  // the wide kernel's buffer offsets: x rows of two adjacent sequences, the conv state
+  // the wide kernel's buffer offsets: x rows of the sequences one workgroup's 64 rows
+  // touch, the conv state
   constexpr long long kOff31 = 0x7fffff00LL;
   const int cs_es = cs_in && cs_in_dtype == VM_DTYPE_BF16 ? 2 : 4;
-  if ((xz_sb + (long long)seqlen * xz_sl + dim) * 2 > kOff31 ||
+  if (((long long)(kCPTok / out_len + 1) * xz_sb + (long long)seqlen * xz_sl + dim) * 2 > kOff31 ||
       (cs_in && ((long long)(batch - 1) * csi_sb + (long long)(dim - 1) * csi_sd + width) * cs_es > kOff31) ||
       (long long)kCPTok * u_sl * 2 > kOff31) {
     vmhost::set_error("vm_conv_proj_fwd: batch > %d needs a sequence of xz under 1 GiB "
