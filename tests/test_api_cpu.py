@@ -372,3 +372,26 @@ def test_graph_workspace_covers_first_and_continuation_chunks(embed_dim, depth, 
                        > K.scan_workspace_bytes(B, mx.d_inner, L, mx.d_state))
     if (embed_dim, frames) == (192, 16):
         assert short_wins > 0  # the case the first-chunk-only sizing missed
+
+
+def test_conv_proj_wide_offset_limit_is_rejected_on_the_host():
+    """The wide conv_proj kernel (batch > 8) addresses x rows, the conv state and u rows
+    through buffer resources with 31-bit offsets; vm_conv_proj_fwd rejects shapes past them
+    before any HIP call (pointers here are never dereferenced): a 300k-token sequence of
+    xz at D = 1152 is past the limit."""
+    lib = _lib.load()
+    D, E, Ep, R = 1152, 68, 80, 36
+    fake = lambda i: ctypes.c_void_p((i + 1) << 20)  # noqa: E731  16-byte aligned, unused
+
+    def call(L, batch):
+        Lp = L
+        return lib.vm_conv_proj_fwd(
+            fake(0), Lp * 2 * D, 2 * D, fake(1), fake(2),
+            None, 0, 0, 0, None, 0, 0, 0,
+            fake(3), E, Ep, None, R, 0,
+            fake(4), Lp * D, D, fake(5), Lp * E, E, None, 0, 0,
+            None, 0, Lp, batch, D, L, 4, _lib.VM_DTYPE_BF16, None, 0, None)
+
+    assert call(300_000, 9) == -1
+    assert b"31-bit" in lib.vm_last_error()
+    assert call(300_000, 0) == 0  # empty batch: nothing to launch, nothing to check
