@@ -40,4 +40,10 @@ for B in [int(b) for b in (sys.argv[2:] or ["1"])]:
         (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, wdt_pad, R, u, (Lp * Dm, Dm), xd,
         (Lp * E, E), dt, (Lp * Dm, Dm), Lp, B, Dm, L, W, st), 50)
     out[f"B{B}_us"] = round(us, 2)
+    # without dt rows (the dt_proj-in-scan mixer's call, the bench's above 8 clips)
+    us = _event_us(lambda: K.conv_proj_raw(
+        xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs_in, (cs_in.stride(0), cs_in.stride(1)), cs_out,
+        (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, None, R, u, (Lp * Dm, Dm), xd,
+        (Lp * E, E), None, None, Lp, B, Dm, L, W, st), 50)
+    out[f"B{B}_nodt_us"] = round(us, 2)
 print(json.dumps(out), flush=True)
