@@ -235,7 +235,10 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
  * dt == NULL skips dt_proj (conv + x_proj only; wdt_pad may then be NULL too).
  * batch <= 8 runs a split-K form (fixed 128-channel splits of the x_proj reduction, so
  * every token's bits are independent of the sequence length) that needs `workspace` of
- * vm_conv_proj_workspace_bytes() bytes; larger batches need none (NULL, 0).
+ * vm_conv_proj_workspace_bytes() bytes; larger batches need none (NULL, 0), and address
+ * x rows, u rows and the conv state through 31-bit buffer offsets: VM_E_INVALID when the xz
+ * rows of the sequences one 64-row tile touches span 2 GiB (about 460k tokens at dim 1152)
+ * or the conv state does.
  * dt_softplus != 0: `dt` receives the scan's activated step instead,
  *   delta = softplus(float(bf16(dt)) + dt_bias[d])  (dt_bias nullable = 0), rounded to bf16
  *   — selective_scan_fn's delta_bias / delta_softplus prologue (mamba_simple.py:30-106),
