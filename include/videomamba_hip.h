@@ -237,7 +237,7 @@ int vm_causal_conv1d_fwd(const void* x, long long x_sb, long long x_sd, long lon
  * every token's bits are independent of the sequence length) that needs `workspace` of
  * vm_conv_proj_workspace_bytes() bytes; larger batches need none (NULL, 0), and address
  * x rows, u rows and the conv state through 31-bit buffer offsets: VM_E_INVALID when the xz
- * rows of the sequences one 64-row tile touches span 2 GiB (about 460k tokens at dim 1152)
+ * rows of the sequences one 64-row tile touches span 2 GiB (about 230k tokens at dim 1152)
  * or the conv state does.
  * dt_softplus != 0: `dt` receives the scan's activated step instead,
  *   delta = softplus(float(bf16(dt)) + dt_bias[d])  (dt_bias nullable = 0), rounded to bf16
