@@ -79,8 +79,8 @@ def _args():
     ap.add_argument("--no-b1", action="store_true",
                     help="skip the B=1 chunk latency and per-stage B=1 rooflines (batch sweeps)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="oracle threads (0: the CPUs this process may run on, at most 16 — "
-                         "a one-GPU box's share)")
+                    help="oracle threads (0: os.cpu_count(), SURVEY 8(d); the rate at a one-GPU "
+                         "box's share, min(16, affinity) threads, is reported beside it)")
     ap.add_argument("--scan-dt-proj", default="auto", choices=("auto", "on", "off"),
                     help="options.scan_dt_proj: dt_proj inside the scan at chip-filling batches")
     ap.add_argument("--full-sequence", action="store_true",
@@ -358,34 +358,51 @@ def _cpu_info():
 
 
 def cpu_baseline(cfg, threads):
-    """the oracle (the CPU restatement pinned to the reference) on the host
-    cores, median of 3 after 1 warm-up, fp32 B=1: the bench clip, and C1 (Ti 8x224^2).
-    ``threads`` 0 = the CPUs this process may run on, capped at 16 (a one-GPU box's share of
-    the host: os.cpu_count() there counts the whole machine, shared with other jobs)."""
+    """the CPU path on the host cores, fp32 B=1, one clip of the bench
+    config and of C1 (Ti 8x224^2).  The code timed is the oracle (the CPU restatement
+    pinned to the reference); it runs at 0.42x the reference's own time on M-16f
+    (profiles/r03_cpu_calibration.json, one session, same threads), so the headline
+    ``value`` is the reference's rate on these cores estimated from it (the measured
+    oracle rate divided by that calibration ratio); the oracle's own rate is ``port_value``.
+    ``threads`` 0 = os.cpu_count(); the rate at a one-GPU box's share of the
+    host (min(16, affinity) threads) is kept beside it.  Median of 2 after 1 warm-up per
+    thread count: a bounded sample (~10-30 s of CPU work) so the bench stays within minutes."""
     model, affinity = _cpu_info()
     if threads <= 0:
-        threads = max(1, min(16, affinity or 1))
-    torch.set_num_threads(threads)
-    dt = _oracle_clip_seconds(cfg)
+        threads = os.cpu_count() or 1
+    share = max(1, min(16, affinity or 1))
     ti = CONFIGS["ti8"]
-    dt_c1 = _oracle_clip_seconds(ti)
+    torch.set_num_threads(threads)
+    dt = _oracle_clip_seconds(cfg, runs=2)
+    dt_c1 = _oracle_clip_seconds(ti, runs=2)
+    dt_share = None
+    if share != threads:
+        torch.set_num_threads(share)
+        dt_share = _oracle_clip_seconds(cfg, runs=1)
     cal = _cpu_calibration()
     key = {16: "m16", 8: "ti8"}.get(cfg["frames"]) if cfg["embed_dim"] in (576, 192) else None
-    ratio = (cal or {}).get("oracle_over_reference_s_per_clip", {}).get(key)
-    return {"value": round(cfg["frames"] * 196 / dt, 2), "unit": "video-tokens/s",
-            "cores": threads, "kind": "port", "cpu_model": model,
-            "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
-            "threads_policy": "min(16, affinity): a one-GPU box's CPU share; os.cpu_count() "
-                              "(BASELINE.md's recipe) counts the whole shared host",
+    ratios = (cal or {}).get("oracle_over_reference_s_per_clip", {})
+    ratio, ratio_c1 = ratios.get(key), ratios.get("ti8")
+    port = cfg["frames"] * 196 / dt
+    port_c1 = ti["frames"] * 196 / dt_c1
+    return {"value": round(port * ratio, 2) if ratio else round(port, 2),
+            "unit": "video-tokens/s", "cores": threads, "kind": "port",
+            "value_basis": ("reference CPU path's rate on these cores, estimated: the timed "
+                            "oracle's rate x its one-session time ratio to the reference "
+                            f"({ratio})" if ratio else "the timed oracle's rate (no calibration)"),
+            "port_value": round(port, 2),
+            "cpu_model": model, "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+            "share_threads": share,
+            "port_value_share_threads": (round(cfg["frames"] * 196 / dt_share, 2)
+                                         if dt_share else round(port, 2)),
             "calibration": cal,
-            # the reference's own CPU path on these cores, scaled by the one-session
-            # oracle/reference time ratio of the calibration record (the port is faster)
-            "reference_rate_estimate": round(cfg["frames"] * 196 / dt * ratio, 2) if ratio else None,
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
-                      f"median of 3 after 1 warm-up ({dt:.2f} s), oracle/videomamba_oracle.py",
-            "c1": {"value": round(ti["frames"] * 196 / dt_c1, 2), "unit": "video-tokens/s",
+                      f"median of 2 after 1 warm-up ({dt:.2f} s at {threads} threads), "
+                      "oracle/videomamba_oracle.py",
+            "c1": {"value": round(port_c1 * ratio_c1, 2) if ratio_c1 else round(port_c1, 2),
+                   "port_value": round(port_c1, 2), "unit": "video-tokens/s",
                    "sample": f"C1: 1 clip {ti['name']} {ti['frames']}x224^2 fp32 B=1, median "
-                             f"of 3 after 1 warm-up ({dt_c1:.2f} s)"}}
+                             f"of 2 after 1 warm-up ({dt_c1:.2f} s)"}}
 
 
 def _timed_steps(step, steps, warmup, world, device, sync):
@@ -538,11 +555,20 @@ def main():
 
         p50_eager = p50_graph = None
         if not args.no_b1:
-            p50_eager = chunk_lat(lambda: model(x1, ssm_state=st1, temporal_pos_offset=0))
-            p50_graph = chunk_lat(lambda: runner.run(x1, temporal_pos_offset=0))
+            outs = []
+            p50_eager = chunk_lat(lambda: outs.append(
+                model(x1, ssm_state=st1, temporal_pos_offset=0)[1]))
+            p50_graph = chunk_lat(lambda: outs.append(runner.run(x1, temporal_pos_offset=0)[1]))
+            # the B=1 legs run the one-launch chunked scan: a timed-out block hand-off there
+            # poisons its outputs with NaN, so no latency is reported unless none happened
+            runner.check()
+            K.check_scan_sync()
+            assert all(bool(torch.isfinite(o.float()).all()) for o in outs[-3:] + outs[:3]), \
+                "non-finite B=1 chunk output"
         from videomamba_amd.mamba_simple import mixer_layout
         mx0 = model.layers[0].mixer
-        hn0 = torch.empty((max(B, 1), 8, cfg["embed_dim"]), device=device, dtype=torch.bfloat16)
+        hn0 = torch.empty((1, 1, cfg["embed_dim"]), device=device,
+                          dtype=torch.bfloat16).expand(max(B, 1), 3144, cfg["embed_dim"])
         roof = scan_roofline(max(B, 1), args.scan_reps, device,
                              mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device),
                              dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))

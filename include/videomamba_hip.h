@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 9
+#define VM_ABI_VERSION 10
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -148,7 +148,8 @@ int vm_selective_scan_bidir_fwd(
  *   w_dt:   (dim, w_dt_ld) bf16 with columns >= dt_rank zero, w_dt_ld >= 16*ceil(r/16);
  * everything else as vm_selective_scan_fwd.  Single pass only (no segments, no
  * workspace): bf16, token-major, 16 states with C directly after B in the x_dbl row (the
- * mixer's layout), z present, delta_softplus = 1, dim % 128 == 0, dt_rank <= 64.  Each
+ * mixer's layout), z present, delta_softplus = 1, dim % 128 == 0, dt_rank <= 64 and a
+ * multiple of 4 (ABI v10: x_dbl columns >= dt_rank are never read as dt_low).  Each
  * token's dt is computed from its own row in a fixed order (sequence-length independent).
  */
 int vm_selective_scan_dtproj_fwd(
@@ -258,6 +259,15 @@ int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
 
 /* Scratch bytes vm_conv_proj_fwd needs for this shape (0 above the split-K batch). */
 long long vm_conv_proj_workspace_bytes(int batch, int out_len, int dim, int e);
+
+/* ABI v10: 1 when vm_conv_proj_fwd accepts this shape's buffer extents (the small-batch forms
+ * always do; the wide form needs its 31-bit buffer offsets to cover the operands, see above),
+ * 0 when it would return VM_E_INVALID for them — a caller then takes the unfused conv +
+ * projection path instead.  Pure host code. */
+int vm_conv_proj_fits(int batch, int out_len, int seqlen, int dim, int e, int r_pad,
+                      int dt_softplus, long long xz_sb, long long xz_sl, int has_conv_state_in,
+                      int cs_in_dtype, long long csi_sb, long long csi_sd, int width,
+                      long long u_sl);
 
 /*
  * Channel-major mixer middle (bf16, small batches; the (D, B*L) layout of

@@ -395,3 +395,50 @@ def test_conv_proj_wide_offset_limit_is_rejected_on_the_host():
     assert call(300_000, 9) == -1
     assert b"31-bit" in lib.vm_last_error()
     assert call(300_000, 0) == 0  # empty batch: nothing to launch, nothing to check
+
+
+def test_conv_proj_fits_query_routes_long_sequences_to_the_unfused_path():
+    """the wide conv_proj form's 31-bit offsets reject ~230k-token sequences at
+    batch > 8; vm_conv_proj_fits reports that on the host and the mixer's fused-path test
+    mirrors it, so such a forward takes the unfused conv + projection path instead of
+    raising.  Small batches (split-K / fused forms, 64-bit addressing) always fit."""
+    from videomamba_amd import kernels as K
+    from videomamba_amd.mamba_simple import Mamba
+    D, E = 1152, 68
+    fits = lambda B, L: K.conv_proj_fits(B, L, L, D, E, 64, (L * 2 * D, 2 * D), D, None, 4)  # noqa: E731
+    assert fits(9, 3144) and fits(448, 3144) and fits(8, 300_000)
+    assert not fits(9, 300_000)
+    mx = Mamba(d_model=576).to(torch.bfloat16)
+    shape_only = lambda B, L: torch.empty(1, 1, 576, dtype=torch.bfloat16).expand(B, L, 576)  # noqa: E731
+    assert mx._fused_conv_proj_ok(shape_only(9, 3144), 3137)
+    assert not mx._fused_conv_proj_ok(shape_only(9, 300_000), 300_000)
+    assert not mx._dtp_ok(shape_only(9, 300_000), 300_000)
+    assert mx._fused_conv_proj_ok(shape_only(8, 300_000), 300_000)
+
+
+def test_linear_rejects_unsupported_k_before_launch():
+    """vm_linear_fwd validates k against the unrolled K-step counts it is built
+    for and returns VM_E_INVALID (no launch, nothing written) for any other multiple of 64."""
+    lib = _lib.load()
+    fake = lambda i: ctypes.c_void_p((i + 1) << 20)  # noqa: E731  never dereferenced
+    for k in (64, 256, 1024):
+        rc = lib.vm_linear_fwd(fake(0), k, fake(1), k, None, fake(2), 64, 128, 64, k,
+                               _lib.VM_DTYPE_BF16, None)
+        assert rc == -1 and b"k = " in lib.vm_last_error(), k
+
+
+def test_sync_rearm_clears_only_the_error_word():
+    """re-arming a sync buffer after a reported timeout zeroes word 0 (the error
+    word) only; the epoch (word 1) keeps growing so stale granules of earlier launches never
+    carry a later launch's tag."""
+    from videomamba_amd import kernels as K
+    buf = torch.zeros(64, dtype=torch.uint8)
+    words = buf.view(torch.int32)
+    words[0], words[1], words[2] = 1, 41, 3
+    with pytest.raises(RuntimeError):
+        K._SYNC[("cpu", None, 0)] = buf
+        try:
+            K.check_scan_sync()
+        finally:
+            del K._SYNC[("cpu", None, 0)]
+    assert words[0] == 0 and words[1] == 41 and words[2] == 3

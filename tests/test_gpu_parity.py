@@ -332,6 +332,24 @@ def test_scan_dtproj_bitwise_equals_dt_rows_then_scan(Bz, D, L, R):
     assert not y1[:, L:].float().abs().any()
 
 
+@pytest.mark.parametrize("R", [12, 36])
+def test_scan_dtproj_never_reads_b_columns_as_dt(R):
+    """with dt_rank not a multiple of 16 the last dt_low MFMA block spans x_dbl
+    columns >= dt_rank, which hold B.  The reference's dt never reads them; the kernel gives
+    those k-lanes an out-of-range (zero) load.  An infinite B value at one step must then
+    leave every other state's dt finite: bit-identical (NaN payloads included) to the scan
+    reading precomputed dt rows."""
+    Bz, D, L = 1, 256, 120
+    c = _dtproj_case(Bz, D, L, R, 5 + R, exact=True)
+    N, Lp = c["N"], c["Lp"]
+    c["XD"].view(Bz, Lp, -1)[0, 50, R] = float("inf")  # B[state 0] of step 50
+    y1, h1 = _run_dtproj(c, Bz, D, L, R, True)
+    y0, h0 = _run_dtproj(c, Bz, D, L, R, False)
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16))
+    assert torch.equal(h1.view(torch.int32), h0.view(torch.int32))
+    assert torch.isfinite(h1[:, :, 1:]).all()  # only state 0 saw the infinite B
+
+
 @pytest.mark.parametrize("Bz,D,L,R", [(2, 256, 301, 36), (1, 1152, 777, 36)])
 def test_scan_dtproj_matches_oracle(Bz, D, L, R):
     """Real-valued dt_low / W_dt: the fused dt_proj + scan against the oracle's scan of

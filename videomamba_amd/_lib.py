@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _P = c_void_p
 _LL = c_longlong
@@ -82,6 +82,9 @@ _SIGNATURES = {
          _I, _I, _I, _I, _I, _I,                  # out_len, batch, dim, seqlen, width, dtype
          _P, _LL, _P], _I),                       # workspace, bytes, stream
     "vm_conv_proj_workspace_bytes": ([_I, _I, _I, _I], _LL),
+    "vm_conv_proj_fits": (
+        [_I, _I, _I, _I, _I, _I, _I,              # batch, out_len, seqlen, dim, e, r_pad, softplus
+         _LL, _LL, _I, _I, _LL, _LL, _I, _LL], _I),  # xz strides, conv state in, width, u_sl
     "vm_conv_proj_cm_fwd": (
         [_P, _LL, _P, _P,                         # xz (row stride), conv weight / bias
          _P, _I, _LL, _LL, _P, _I, _LL, _LL,      # conv state in / out

@@ -439,6 +439,41 @@ extern "C" long long vm_conv_proj_workspace_bytes(int batch, int out_len, int di
   return conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
 }
 
+// Which form vm_conv_proj_fwd runs (the split-K / fused small-batch form for batch <=
+// kSkMaxBatch, else the wide kernel), and whether the wide kernel's 31-bit buffer offsets
+// cover the operands: the x rows of the sequences one workgroup's 64 rows touch, the conv
+// state, the u rows.  Shared by the launcher and the host query vm_conv_proj_fits.
+static bool conv_proj_small_form(int batch, int dim, int e, int r_pad, int spd, int out_len) {
+  return batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= kSkMaxEp &&
+         r_pad <= 80 && out_len >= 8;
+}
+static bool conv_proj_wide_offsets_ok(int batch, int out_len, int seqlen, int dim,
+                                      long long xz_sb, long long xz_sl, bool has_cs_in,
+                                      int cs_in_dtype, long long csi_sb, long long csi_sd,
+                                      int width, long long u_sl) {
+  constexpr long long kOff31 = 0x7fffff00LL;
+  const int cs_es = has_cs_in && cs_in_dtype == VM_DTYPE_BF16 ? 2 : 4;
+  return ((long long)(kCPTok / out_len + 1) * xz_sb + (long long)seqlen * xz_sl + dim) * 2 <=
+             kOff31 &&
+         (!has_cs_in ||
+          ((long long)(batch - 1) * csi_sb + (long long)(dim - 1) * csi_sd + width) * cs_es <=
+              kOff31) &&
+         (long long)kCPTok * u_sl * 2 <= kOff31;
+}
+
+extern "C" int vm_conv_proj_fits(int batch, int out_len, int seqlen, int dim, int e, int r_pad,
+                                 int dt_softplus, long long xz_sb, long long xz_sl,
+                                 int has_conv_state_in, int cs_in_dtype, long long csi_sb,
+                                 long long csi_sd, int width, long long u_sl) {
+  if (batch <= 0 || out_len <= 0) return 1;
+  if (conv_proj_small_form(batch, dim, e, r_pad, dt_softplus != 0, out_len)) return 1;
+  return conv_proj_wide_offsets_ok(batch, out_len, seqlen, dim, xz_sb, xz_sl,
+                                   has_conv_state_in != 0, cs_in_dtype, csi_sb, csi_sd, width,
+                                   u_sl)
+             ? 1
+             : 0;
+}
+
 extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl,
                                 const float* conv_weight, const float* conv_bias,
                                 const void* cs_in, int cs_in_dtype, long long csi_sb, long long csi_sd,
@@ -500,8 +535,7 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
   // skips it (conv + x_proj only: a consumer that projects dt itself)
   const bool fused_dt = dt != nullptr;
   const bool spd = dt_softplus != 0;
-  if (batch <= kSkMaxBatch && !spd && dim <= 2048 && (e + 3) / 4 * 4 <= kSkMaxEp &&
-      r_pad <= 80 && out_len >= 8) {
+  if (conv_proj_small_form(batch, dim, e, r_pad, spd, out_len)) {
     // small batch: the split-K form (vm_conv_proj_sk.hip) fills the chip and keeps the
     // x_proj reduction order fixed per token
     const long long need = conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
@@ -524,13 +558,8 @@ extern "C" int vm_conv_proj_fwd(const void* xz, long long xz_sb, long long xz_sl
     else conv_proj_sk_launch(a, static_cast<float*>(workspace), st);
     return vmhost::launch_status("vm_conv_proj_fwd");
   }
-  // the wide kernel's buffer offsets: x rows of the sequences one workgroup's 64 rows
-  // touch, the conv state
-  constexpr long long kOff31 = 0x7fffff00LL;
-  const int cs_es = cs_in && cs_in_dtype == VM_DTYPE_BF16 ? 2 : 4;
-  if (((long long)(kCPTok / out_len + 1) * xz_sb + (long long)seqlen * xz_sl + dim) * 2 > kOff31 ||
-      (cs_in && ((long long)(batch - 1) * csi_sb + (long long)(dim - 1) * csi_sd + width) * cs_es > kOff31) ||
-      (long long)kCPTok * u_sl * 2 > kOff31) {
+  if (!conv_proj_wide_offsets_ok(batch, out_len, seqlen, dim, xz_sb, xz_sl, cs_in != nullptr,
+                                 cs_in_dtype, csi_sb, csi_sd, width, u_sl)) {
     vmhost::set_error("vm_conv_proj_fwd: batch > %d needs a sequence of xz under 1 GiB "
                       "(31-bit buffer offsets)", kSkMaxBatch);
     return VM_E_INVALID;

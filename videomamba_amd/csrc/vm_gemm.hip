@@ -493,6 +493,12 @@ extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long l
                       "dimensions multiples of 8; 16-byte aligned operands under 2 GB");
     return VM_E_INVALID;
   }
+  switch (k / kLinBK) {  // the unrolled K-step counts both kernel forms are built for
+    case 3: case 6: case 9: case 12: case 18: case 24: break;
+    default:
+      vmhost::set_error("vm_linear_fwd: k = %d (supported: 192, 384, 576, 768, 1152, 1536)", k);
+      return VM_E_INVALID;
+  }
   if (m == 0) return VM_OK;
   LinParams p{};
   p.x = static_cast<const bf16_t*>(x); p.ldx = ldx;

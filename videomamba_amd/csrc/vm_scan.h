@@ -78,6 +78,7 @@ struct DtpArgs {
   long long dtl_sl;   // row (step) stride (elements)
   const bf16_t* wdt;  // W_dt padded: (dim, wdt_ld) bf16, columns >= dt_rank zero
   int wdt_ld;
+  int dt_rank;        // x_dbl columns >= dt_rank (the B values) are never read as dt_low
 };
 bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_rank);
 void seq_dtp_launch(const ScanParams& p, const DtpArgs& q, int dt_rank, hipStream_t s);

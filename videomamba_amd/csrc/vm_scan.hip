@@ -629,10 +629,10 @@ extern "C" int vm_selective_scan_dtproj_fwd(
   p.split = batch;
   DtpArgs q{};
   q.dtl = static_cast<const bf16_t*>(dt_low); q.dtl_sb = dtl_sb; q.dtl_sl = dtl_sl;
-  q.wdt = static_cast<const bf16_t*>(w_dt); q.wdt_ld = w_dt_ld;
+  q.wdt = static_cast<const bf16_t*>(w_dt); q.wdt_ld = w_dt_ld; q.dt_rank = dt_rank;
   if (!seq_dtp_supported(p, q, dtype, dt_rank)) {
     vmhost::set_error("%s: needs bf16 token-major operands with z, softplus, 16 states, C "
-                      "directly after B in the x_dbl rows, dim %% 128 == 0, dt_rank <= 64, "
+                      "directly after B in the x_dbl rows, dim %% 128 == 0, dt_rank <= 64 and a multiple of 4, "
                       "8-byte aligned dt_low rows and a (dim, >= 16*ceil(r/16)) W_dt", name);
     return VM_E_INVALID;
   }

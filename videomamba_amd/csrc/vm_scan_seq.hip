@@ -605,10 +605,17 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
 
   // ---- the dt block: A fragments (dt_low rows tg .. tg+15) in `af`, W_dt^T from LDS ----
   const int a_voff = ((lane & 15) * static_cast<int>(q.dtl_sl) + 4 * (lane >> 4)) * ES;
+  // the last 16-column block's lanes past dt_rank (dt_rank % 4 == 0) read 0 through an
+  // out-of-range offset instead of the row's B values: the reference's dt never reads
+  // them, and a non-finite B times the zero W_dt padding would make dt NaN
+  const int a_last = 16 * (NKS - 1) + 4 * (lane >> 4) < q.dt_rank
+                         ? a_voff + 16 * (NKS - 1) * ES
+                         : static_cast<int>(0x80000000u);
   auto a_load = [&](int tg, uint2 (&af)[NKS]) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(dtr, a_voff + 16 * ks * ES, tg * dls, 0);
+      const int off = ks == NKS - 1 ? a_last : a_voff + 16 * ks * ES;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(dtr, off, tg * dls, 0);
       af[ks] = uint2{v[0], v[1]};
     }
   };
@@ -1614,7 +1621,8 @@ bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_
   const long long dl_span = static_cast<long long>(p.out_len) * q.dtl_sl * 2;
   return dtype == VM_DTYPE_BF16 && seq_supported(p, dtype) && seq_sgpr_bc(p, 2) && bc1 &&
          p.dstate == kMaxN && p.z && p.softplus && p.split == p.batch &&
-         p.dim % (64 * kSeqNW) == 0 && dt_rank >= 1 && dt_rank <= 64 && q.dtl && q.wdt &&
+         p.dim % (64 * kSeqNW) == 0 && dt_rank >= 1 && dt_rank <= 64 && dt_rank % 4 == 0 &&
+         q.dt_rank == dt_rank && q.dtl && q.wdt &&
          q.wdt_ld >= 16 * nks && q.wdt_ld % 4 == 0 &&
          (reinterpret_cast<uintptr_t>(q.wdt) & 7) == 0 &&
          (reinterpret_cast<uintptr_t>(q.dtl) & 7) == 0 && q.dtl_sl % 4 == 0 &&

@@ -171,7 +171,7 @@ class StreamingChunkGraph:
         """Raise if a replayed one-launch scan ever timed out on a block hand-off (its
         outputs were NaN); synchronises with the queued replays.  See K.check_scan_sync."""
         if self._sync is not None and K.scan_sync_status(self._sync):
-            self._sync[:K.SYNC_HEADER_BYTES].zero_()
+            K.clear_scan_sync_error(self._sync)
             raise RuntimeError("StreamingChunkGraph: a replayed one-launch scan timed out on a "
                                "block hand-off; the affected outputs were NaN")
 

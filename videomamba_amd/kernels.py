@@ -184,6 +184,7 @@ def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tens
 
 
 SYNC_HEADER_BYTES = 16  # error word, epoch, start count, pad (ABI v9)
+SYNC_ERROR_BYTES = 4  # the error word alone
 
 
 def scan_sync_status(buf: Tensor) -> int:
@@ -199,6 +200,13 @@ def scan_sync_status(buf: Tensor) -> int:
     return rc
 
 
+def clear_scan_sync_error(buf: Tensor) -> None:
+    """Re-arm a sync buffer after a reported timeout: zero its error word (header word 0)
+    only.  The epoch (word 1) must keep growing — granules of earlier launches never match a
+    later launch's tag only because every launch uses a higher one (ABI v9)."""
+    buf.reshape(-1)[:SYNC_ERROR_BYTES].zero_()
+
+
 def check_scan_sync(clear: bool = True) -> None:
     """Raise RuntimeError if any sync buffer this process has used (the per-stream ones and
     those passed through :class:`sync_override`, e.g. a captured graph's) recorded a
@@ -210,7 +218,7 @@ def check_scan_sync(clear: bool = True) -> None:
         if scan_sync_status(buf):
             bad += 1
             if clear:
-                buf.reshape(-1)[:SYNC_HEADER_BYTES].zero_()
+                clear_scan_sync_error(buf)
     if bad:
         raise RuntimeError(f"one-launch selective scan: {bad} sync buffer(s) recorded a "
                            "timed-out block hand-off; the affected outputs are NaN")
@@ -327,6 +335,17 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
         _p(dt_bias32), int(dt_softplus), out_len, batch, dim, seqlen, width, dtype_code(u.dtype),
         _p(ws), nbytes, stream)
     _lib.check(rc, "vm_conv_proj_fwd")
+
+
+def conv_proj_fits(batch: int, out_len: int, seqlen: int, dim: int, e: int, r_pad: int,
+                   xz_s, u_sl: int, cs_in: Optional[Tensor], width: int) -> bool:
+    """Whether ``vm_conv_proj_fwd`` accepts this token-major shape (``vm_conv_proj_fits``):
+    the wide form (batch > 8) addresses its operands through 31-bit buffer offsets, so very
+    long sequences go to the unfused conv + projection path instead of raising."""
+    csi = (cs_in.stride(0), cs_in.stride(1)) if cs_in is not None else (0, 0)
+    return bool(_lib.load().vm_conv_proj_fits(
+        batch, out_len, seqlen, dim, e, r_pad, 0, xz_s[0], xz_s[1], int(cs_in is not None),
+        dtype_code(cs_in.dtype) if cs_in is not None else 0, csi[0], csi[1], width, u_sl))
 
 
 def conv_proj_workspace_bytes(batch: int, out_len: int, dim: int, e: int) -> int:

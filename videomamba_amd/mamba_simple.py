@@ -213,12 +213,23 @@ class Mamba(nn.Module):
             self._wpad_key = key
         return self._wpad
 
-    def _fused_conv_proj_ok(self, hn: Tensor, seqlen: int) -> bool:
+    def _fused_conv_proj_ok(self, hn: Tensor, seqlen: int, conv_state_in: Optional[Tensor] = None,
+                            tm: bool = True) -> bool:
+        """The fused conv + x_proj (+ dt_proj) kernel applies: bf16, its shape limits and,
+        token-major (``tm``), buffer extents its 31-bit offsets cover (vm_conv_proj_fits: a
+        very long sequence at batch > 8 takes the unfused conv + projection path)."""
         E = self.dt_rank + 2 * self.d_state
-        return (hn.dtype == torch.bfloat16 and seqlen >= 1 and self.d_inner % 64 == 0
+        if not (hn.dtype == torch.bfloat16 and seqlen >= 1 and self.d_inner % 64 == 0
                 and self.d_conv <= 4 and E <= 128 and self.dt_rank <= 64
                 and self.x_proj.bias is None and self.dt_proj.weight.dtype == torch.bfloat16
-                and options.get().fused_conv_proj)
+                and options.get().fused_conv_proj):
+            return False
+        if not tm:
+            return True
+        Bsz, Lp = hn.shape[0], hn.shape[1]
+        Dm = self.d_inner
+        return K.conv_proj_fits(Bsz, Lp, seqlen, Dm, E, 32 if self.dt_rank <= 32 else 64,
+                                (Lp * 2 * Dm, 2 * Dm), Dm, conv_state_in, self.d_conv)
 
     # ------------------------------------------------------------------ core
     def _forward_padded(self, hn: Tensor, seqlen: int, *, conv_state_in: Optional[Tensor] = None,
@@ -249,7 +260,7 @@ class Mamba(nn.Module):
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
                  if conv_state_out is not None else (0, 0))
-        if self._fused_conv_proj_ok(hn, seqlen):
+        if self._fused_conv_proj_ok(hn, seqlen, tm=False):
             # conv + silu -> x_proj -> dt_proj with a fixed reduction order
             # (vm_conv_proj_cm.hip): faster than the latency-bound library GEMMs at small
             # batch, and chunk-invariant (every token's bits independent of L)
@@ -276,7 +287,7 @@ class Mamba(nn.Module):
             out += self.out_proj.bias.to(out.dtype)
         return out.view(Bsz, Lp, C)
 
-    def _dtp_ok(self, hn: Tensor, seqlen: int) -> bool:
+    def _dtp_ok(self, hn: Tensor, seqlen: int, conv_state_in: Optional[Tensor] = None) -> bool:
         """Fold dt_proj into the scan (vm_selective_scan_dtproj_fwd): bf16 fused conv_proj
         path, 16 states, D % 128 == 0, and a single-pass scan at this batch (the segmented
         small-batch forms read a dt row); "auto" only above the split-K batch (> 8), where
@@ -285,8 +296,8 @@ class Mamba(nn.Module):
         Bsz = hn.shape[0]
         if mode == "off" or (mode == "auto" and Bsz <= 8):
             return False
-        return (self._fused_conv_proj_ok(hn, seqlen) and self.d_state == 16
-                and self.d_inner % 128 == 0 and self.dt_rank <= 64
+        return (self._fused_conv_proj_ok(hn, seqlen, conv_state_in) and self.d_state == 16
+                and self.d_inner % 128 == 0 and self.dt_rank <= 64 and self.dt_rank % 4 == 0
                 and K.scan_workspace_bytes(Bsz, self.d_inner, seqlen, self.d_state) == 0)
 
     def _tm_front(self, hn, seqlen, conv_state_in, conv_state_out, bufs=None, want_dt=True):
@@ -314,7 +325,7 @@ class Mamba(nn.Module):
                  if conv_state_in is not None else (0, 0))
         cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
                  if conv_state_out is not None else (0, 0))
-        if self._fused_conv_proj_ok(hn, seqlen):
+        if self._fused_conv_proj_ok(hn, seqlen, conv_state_in):
             # conv + silu -> x_proj -> dt_proj in one kernel (vm_conv_proj.hip).  The scan
             # keeps the delta activation softplus(dt + bias): moved into conv_proj's dt
             # epilogue it measured a wash at B = 336 (scan -222 us, conv_proj +385 us per
@@ -348,7 +359,7 @@ class Mamba(nn.Module):
         stream = torch.cuda.current_stream(hn.device).cuda_stream
         A, Dv, dbias, _, _ = self._fp32_params()
         s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
-        dtp = self._dtp_ok(hn, seqlen)
+        dtp = self._dtp_ok(hn, seqlen, conv_state_in)
         xz, u, x_dbl, dt = self._tm_front(hn, seqlen, conv_state_in, conv_state_out,
                                           want_dt=not dtp)
         y = torch.empty_like(u)
