@@ -27,8 +27,9 @@
  *                                 per-frame / whole-clip column sums of the pooling
  *   vm_pool_finish_fwd         <- the pooling tail: means, CLS add / concat and pool_norm
  *                                 LayerNorm (videomamba.py:983-1062, :702-751 masked)
- *   vm_linear_fwd              <- the mixer's in_proj / out_proj nn.Linear at one clip's
- *                                 token count (mamba_simple.py:333-339, :445-446)
+ *   vm_linear_fwd              <- the mixer's in_proj / out_proj nn.Linear at every batch
+ *                                 (mamba_simple.py:333-339, :445-446); vm_linear_fwd_form
+ *                                 names the kernel form (tests, benches)
  *   vm_linear_add_norm_fwd     <- out_proj + the next Block's fused add + RMSNorm
  *                                 (mamba_simple.py:445-446, videomamba.py:141-166)
  *   vm_patch_embed_fwd         <- PatchEmbed Conv3d + pos/temporal embedding add
@@ -362,6 +363,21 @@ int vm_pool_finish_fwd(const void* workspace, int batch, int groups, int group_r
 int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
                   const float* bias, void* out, long long ldo, int m, int n, int k, int dtype,
                   vm_stream_t stream);
+
+/*
+ * vm_linear_fwd with the kernel form named (ABI v10): 0 = chosen by shape (what
+ * vm_linear_fwd does), 1 = the LDS-DMA tile kernel (128-row tiles, one launch wave), 2 = the
+ * persistent 256-row tile kernel (one workgroup per CU walking XCD-contiguous runs of
+ * 256 x 256 or 256 x 192 tiles; needs bias == NULL and n a multiple of 256 or 192).  Every
+ * form computes each output element as the same chain of MFMAs (K in 64-wide steps, in
+ * order), so their outputs are bit-identical and a row never depends on m — the form only
+ * changes speed.  Form 0 takes the persistent kernel from 3 tiles per CU up (the mixer's
+ * projections above a few clips: in_proj / out_proj at 448 clips, mamba_simple.py:333-339,
+ * :445-446).
+ */
+int vm_linear_fwd_form(const void* x, long long ldx, const void* w, long long ldw,
+                       const float* bias, void* out, long long ldo, int m, int n, int k,
+                       int dtype, int form, vm_stream_t stream);
 
 /*
  * out_proj fused with the NEXT block's residual add + RMSNorm (mamba_simple.py:445-446, then

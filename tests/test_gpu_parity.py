@@ -889,20 +889,28 @@ def test_small_m_linear_matches_fp32_reference(m, n, k):
 
 
 def test_b1_mixer_projections_run_on_the_hip_gemm():
-    """At one clip's token count the mixer's out_proj takes vm_linear_fwd (the native path;
-    in_proj's N = 2304 stays on the library GEMM, faster there), and the mixer output matches
-    the library-GEMM path within bf16 rounding."""
+    """The mixer's projections take vm_linear_fwd (the native path) at every batch by
+    default (options.projection_gemm = "hip": rows independent of the row count); at one
+    clip's token count the mixer output matches the library-GEMM path ("library" mode, the
+    round-3 rule) within bf16 rounding."""
     from videomamba_amd.mamba_simple import Mamba, _small_gemm_ok
     torch.manual_seed(0)
     m = Mamba(d_model=576, layer_idx=0).to(DEV, torch.bfloat16).eval()
     x = torch.randn(1, 3137, 576, device=DEV).to(torch.bfloat16)
     hp = torch.zeros(1, 3144, 576, device=DEV, dtype=torch.bfloat16)
-    assert not _small_gemm_ok(hp.view(3144, 576), m.in_proj.weight, None)
+    assert _small_gemm_ok(hp.view(3144, 576), m.in_proj.weight, None)
     y = torch.zeros(3144, 1152, device=DEV, dtype=torch.bfloat16)
     assert _small_gemm_ok(y, m.out_proj.weight, None)
+    big = torch.zeros(448 * 3144, 1152, device=DEV, dtype=torch.bfloat16)
+    assert _small_gemm_ok(big, m.out_proj.weight, None)  # past 2 GB: the persistent form
+    with options.override(projection_gemm="library"):
+        assert not _small_gemm_ok(hp.view(3144, 576), m.in_proj.weight, None)
+        assert not _small_gemm_ok(big, m.out_proj.weight, None)
+    del big
     with torch.no_grad():
         y_hip = m(x)
-        with options.override(small_gemm_rows=0):
+        with options.override(projection_gemm="library", small_gemm_rows=0,
+                              row_invariant_gemm_clips=0):
             y_lib = m(x)
     rel = ((y_hip.float() - y_lib.float()).norm() / y_lib.float().norm()).item()
     assert rel < 1e-2, rel
@@ -935,3 +943,56 @@ def test_linear_add_norm_bitwise_equals_linear_then_add_norm(m, n, k):
         assert torch.equal(hn, hn_ref)
     cnt = K.counter_buffer(x.device, torch.cuda.current_stream().cuda_stream, 0)
     assert not cnt.any()
+
+
+@pytest.mark.parametrize("m,n,k", [(70001, 2304, 576), (70001, 576, 1152), (4097, 2304, 576),
+                                   (300, 576, 1152), (9001, 768, 192), (9001, 192, 384),
+                                   (5555, 1536, 384), (5555, 384, 768), (1, 2304, 576)])
+def test_persistent_linear_bitwise_equals_dma_tiles(m, n, k):
+    """The persistent 256-row tile GEMM (vm_gemm_tile.hip: persistent workgroups, LDS-DMA
+    half-tiles, out^T MFMA tiles stored through v_permlane16_swap) against the 128-row LDS-DMA
+    tile kernel on the same operands: bit-identical outputs (every element the same MFMA
+    chain in K order), within one bf16 rounding of an fp32 torch reference.  Shapes: the
+    mixer's in_proj / out_proj of M, Ti and S, ragged m (a partial last 256-row tile, odd
+    tile counts per workgroup, a run that ends mid tile pair, m = 1), both tile widths."""
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) * k ** -0.5).to(torch.bfloat16)
+    y_dma = K.linear(x, w, form="dma")
+    y_tile = torch.full((m + 3, n), 7.0, device=DEV, dtype=torch.bfloat16)
+    K.linear(x, w, out=y_tile[:m], form="persistent")
+    torch.cuda.synchronize()
+    assert torch.equal(y_tile[:m], y_dma)
+    assert (y_tile[m:] == 7.0).all()  # nothing past row m
+    ref = x.float() @ w.float().t()
+    assert ((y_tile[:m].float() - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-3).all()
+
+
+@pytest.mark.parametrize("m,n,k", [(20000, 2304, 576), (20000, 576, 1152)])
+def test_persistent_linear_rows_independent_of_m_and_output_stride(m, n, k):
+    """Chunk invariance of the projections at chip-filling batches: a row's
+    bits do not depend on how many rows the call holds (a prefix run on the LDS-DMA form, a
+    middle slice on the persistent form) nor on a column-sliced output view (ldo > n), and
+    repeated launches are bit-identical."""
+    torch.manual_seed(3 * m + n)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) * k ** -0.5).to(torch.bfloat16)
+    y = K.linear(x, w, form="persistent")
+    assert torch.equal(K.linear(x, w, form="persistent"), y)
+    assert torch.equal(K.linear(x[:3001].contiguous(), w, form="dma"), y[:3001])
+    assert torch.equal(K.linear(x[5000:17777].contiguous(), w, form="persistent"), y[5000:17777])
+    out = torch.full((m, 2 * n), 7.0, device=DEV, dtype=torch.bfloat16)
+    K.linear(x, w, out=out[:, n:], form="persistent")
+    assert torch.equal(out[:, n:], y) and (out[:, :n] == 7.0).all()
+    assert torch.equal(K.linear(x, w), y)  # the auto choice at this size: same bits
+
+
+def test_persistent_linear_rejects_unsupported_shapes():
+    """The persistent form needs no bias and n a multiple of 192 or 256; asked for anyway it
+    returns VM_E_INVALID (nothing launched), while the auto form falls back to LDS-DMA tiles."""
+    x = torch.randn(4096, 576, device=DEV).to(torch.bfloat16)
+    w = torch.randn(200, 576, device=DEV).to(torch.bfloat16)
+    with pytest.raises(RuntimeError, match="persistent"):
+        K.linear(x, w, form="persistent")
+    y = K.linear(x, w)
+    assert torch.equal(y, K.linear(x, w, form="dma"))

@@ -109,6 +109,7 @@ _SIGNATURES = {
          _P, _I, _LL, _I, _I,                     # cls, dtype, stride, mode, keep_temporal
          _P, _P, c_float, _P, _I, _I, _P], _I),   # LN w / b / eps, x_pool, dtype, cols
     "vm_linear_fwd": ([_P, _LL, _P, _LL, _P, _P, _LL, _I, _I, _I, _I, _P], _I),
+    "vm_linear_fwd_form": ([_P, _LL, _P, _LL, _P, _P, _LL, _I, _I, _I, _I, _I, _P], _I),
     "vm_linear_add_norm_fwd": (
         [_P, _LL, _P, _LL,                        # x, ldx, w, ldw
          _P, _LL, _P, _LL,                        # h (out), ldo, residual (fp32), ldr

@@ -474,6 +474,28 @@ static void linear_dma_launch(const LinParams& p, hipStream_t s) {
 #undef VM_LDMA_TILE
 constexpr bool kLinearDma = true;  // vm_linear_fwd runs the pipelined form
 
+// The persistent 256-row tile kernel (vm_gemm_tile.hip): bit-identical rows, used once the
+// tile count fills every CU several times over.
+int gemm_tile_bn(int m, int n, int k, long long ldx, long long ldw, long long ldo);
+long long gemm_tile_count(int m, int n, int bn);
+void gemm_tile_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long ldw,
+                      bf16_t* out, long long ldo, int m, int n, int k, int bn, int workgroups,
+                      hipStream_t s);
+constexpr int kTileMinPerCU = 3;  // tiles per CU from which the persistent kernel runs
+
+// CUs of the current device, cached per device id (one query per device per process)
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 }  // namespace vm
 
 using namespace vm;
@@ -481,16 +503,25 @@ using namespace vm;
 extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
                              const float* bias, void* out, long long ldo, int m, int n, int k,
                              int dtype, vm_stream_t stream) {
+  return vm_linear_fwd_form(x, ldx, w, ldw, bias, out, ldo, m, n, k, dtype, 0, stream);
+}
+
+extern "C" int vm_linear_fwd_form(const void* x, long long ldx, const void* w, long long ldw,
+                                  const float* bias, void* out, long long ldo, int m, int n,
+                                  int k, int dtype, int form, vm_stream_t stream) {
   if (!x || !w || !out) {
     vmhost::set_error("vm_linear_fwd: null required pointer");
     return VM_E_INVALID;
   }
+  if (form < 0 || form > 2) {
+    vmhost::set_error("vm_linear_fwd_form: form %d (0 auto, 1 LDS-DMA tiles, 2 persistent)", form);
+    return VM_E_INVALID;
+  }
   if (dtype != VM_DTYPE_BF16 || m < 0 || n < 1 || k < kLinBK || n % 8 || k % kLinBK ||
       ldx < k || ldw < k || ldo < n || ldx % 8 || ldw % 8 || ldo % 8 || !vmhost::aligned16(x) ||
-      !vmhost::aligned16(w) || !vmhost::aligned16(out) ||
-      (long long)m * ldx * 2 >= (1ll << 31) || (long long)n * ldw * 2 >= (1ll << 31)) {
+      !vmhost::aligned16(w) || !vmhost::aligned16(out) || (long long)n * ldw * 2 >= (1ll << 31)) {
     vmhost::set_error("vm_linear_fwd: bf16 only; k a multiple of 64; n and the leading "
-                      "dimensions multiples of 8; 16-byte aligned operands under 2 GB");
+                      "dimensions multiples of 8; 16-byte aligned operands, w under 2 GB");
     return VM_E_INVALID;
   }
   switch (k / kLinBK) {  // the unrolled K-step counts both kernel forms are built for
@@ -506,6 +537,26 @@ extern "C" int vm_linear_fwd(const void* x, long long ldx, const void* w, long l
   p.bias = bias; p.out = static_cast<bf16_t*>(out); p.ldo = ldo;
   p.m = m; p.n = n; p.k = k;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int bn = bias ? 0 : gemm_tile_bn(m, n, k, ldx, ldw, ldo);
+  if (form == 2 && !bn) {
+    vmhost::set_error("vm_linear_fwd_form: the persistent form needs no bias, n a multiple of "
+                      "192 or 256 and 256-row ranges under 2 GB");
+    return VM_E_INVALID;
+  }
+  if (form != 1 && bn) {
+    const int wgs = device_cus() / 8 * 8;
+    if (wgs >= 8 && (form == 2 || gemm_tile_count(m, n, bn) >=
+                                      static_cast<long long>(kTileMinPerCU) * wgs)) {
+      gemm_tile_launch(p.x, ldx, p.w, ldw, p.out, ldo, m, n, k, bn, wgs, s);
+      return vmhost::launch_status("vm_linear_fwd");
+    }
+  }
+  // the LDS-DMA and register-ring forms address x through one buffer (31-bit offsets)
+  if ((long long)m * ldx * 2 >= (1ll << 31)) {
+    vmhost::set_error("vm_linear_fwd: x past 2 GB needs the persistent form (no bias, n a "
+                      "multiple of 192 or 256)");
+    return VM_E_INVALID;
+  }
   if (kLinearDma) {
     linear_dma_launch(p, s);
     return vmhost::launch_status("vm_linear_fwd");

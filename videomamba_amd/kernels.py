@@ -387,16 +387,22 @@ def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_r
     _lib.check(rc, "vm_add_norm_fwd")
 
 
+LINEAR_FORMS = {"auto": 0, "dma": 1, "persistent": 2}
+
+
 def linear(x: Tensor, w: Tensor, b32: Optional[Tensor] = None,
-           out: Optional[Tensor] = None) -> Tensor:
-    """``x @ w.T (+ b)`` on the HIP small-M GEMM (``vm_linear_fwd``): x (m, k), w (n, k)
-    bf16 with unit column stride; ``out`` (m, n) may be a column-sliced view."""
+           out: Optional[Tensor] = None, form: str = "auto") -> Tensor:
+    """``x @ w.T (+ b)`` on the HIP GEMM (``vm_linear_fwd_form``): x (m, k), w (n, k) bf16
+    with unit column stride; ``out`` (m, n) may be a column-sliced view.  ``form`` names the
+    kernel ("dma": 128-row LDS-DMA tiles, "persistent": the 256-row persistent kernel,
+    "auto": by shape); every form gives the same bits."""
     m, k = x.shape
     n = w.shape[0]
     if out is None:
         out = torch.empty((m, n), dtype=x.dtype, device=x.device)
-    rc = _lib.load().vm_linear_fwd(_p(x), x.stride(0), _p(w), w.stride(0), _p(b32), _p(out),
-                                   out.stride(0), m, n, k, dtype_code(x.dtype), _stream(x))
+    rc = _lib.load().vm_linear_fwd_form(_p(x), x.stride(0), _p(w), w.stride(0), _p(b32),
+                                        _p(out), out.stride(0), m, n, k, dtype_code(x.dtype),
+                                        LINEAR_FORMS[form], _stream(x))
     _lib.check(rc, "vm_linear_fwd")
     return out
 

@@ -53,20 +53,29 @@ _SMALL_GEMM_K = (192, 384, 576, 768, 1152, 1536)  # vm_linear_fwd's unrolled K-s
 
 def _small_gemm_ok(x: Tensor, w: Tensor, b: Optional[Tensor], out: Optional[Tensor] = None,
                    clips: Optional[int] = None) -> bool:
-    """bf16 projections run on the HIP GEMM (vm_linear_fwd, each output row computed in the
-    same order whatever the row count) instead of the library GEMM when
-      * the mixer holds at most ``options.row_invariant_gemm_clips`` clips (streaming
-        batches): at every token count, so a chunked stream equals the one-pass forward bit
-        for bit — the library picks M-dependent kernels (C5, 16 x 64-frame chunks vs one
-        1,024-frame pass: 6.2e-4 relative on the last chunk with the library, 0.0 with this
-        GEMM; scripts/diag/c5_invariance.py); or
-      * one clip's rows with a narrow output (out_proj at B = 1: 11.0 vs 13.4 us)."""
+    """Whether a bf16 projection runs on the HIP GEMM (vm_linear_fwd) instead of the library.
+
+    ``options.projection_gemm == "hip"`` (default): whenever the HIP GEMM takes the shape
+    (bf16, no bias, K in its unrolled set, 16-byte rows; x past 2 GB only on the persistent
+    form, n a multiple of 192 or 256).  Its two kernel forms compute every output element as
+    the same MFMA chain in K order, so a row's bits never depend on the row count: a chunked
+    stream equals the one-pass forward at every batch (C4 at 72 clips was 1.4e-4 on the
+    library GEMM, whose kernel choice depends on M), and at the bench batch the persistent
+    form outruns the library.
+    ``"library"``: the round-3 rule — the HIP GEMM for mixers of at most
+    ``row_invariant_gemm_clips`` clips (C5, 16 x 64-frame chunks vs one 1,024-frame pass:
+    6.2e-4 relative on the library, 0.0 here; scripts/diag/c5_invariance.py) and for one
+    clip's narrow projections; hipBLASLt otherwise."""
     o = options.get()
     ok16 = lambda t: t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(1) == 1  # noqa: E731
     if not (x.shape[0] > 0 and b is None and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.is_cuda and x.shape[1] in _SMALL_GEMM_K
-            and w.shape[0] % 8 == 0 and ok16(x) and ok16(w) and (out is None or ok16(out))
-            and x.shape[0] * x.stride(0) * 2 < (1 << 31)):
+            and w.shape[0] % 8 == 0 and ok16(x) and ok16(w) and (out is None or ok16(out))):
+        return False
+    small_x = x.shape[0] * x.stride(0) * 2 < (1 << 31)
+    if o.projection_gemm == "hip":
+        return small_x or w.shape[0] % 192 == 0 or w.shape[0] % 256 == 0
+    if not small_x:
         return False
     if clips is not None and 0 < clips <= o.row_invariant_gemm_clips:
         return True
@@ -75,8 +84,8 @@ def _small_gemm_ok(x: Tensor, w: Tensor, b: Optional[Tensor], out: Optional[Tens
 
 def _linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None,
             clips: Optional[int] = None) -> Tensor:
-    """A projection GEMM of the mixer: the HIP GEMM for streaming-sized batches and one
-    clip's narrow projections, else the library GEMM with the shipped tuning results."""
+    """A projection GEMM of the mixer: the HIP GEMM where :func:`_small_gemm_ok` says so,
+    else the library GEMM with the shipped tuning results."""
     if _small_gemm_ok(x, w, b, clips=clips):
         return K.linear(x, w)
     with tuned():

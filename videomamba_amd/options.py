@@ -25,8 +25,14 @@ documented options object; tests and sweeps change them with :func:`override`.
                      bf16 token-major mixer folds dt_proj into the scan
                      (vm_selective_scan_dtproj_fwd) and conv_proj skips its dt rows; "on":
                      whenever the single-pass scan runs (tests); "off": conv_proj writes dt.
+    projection_gemm  "hip" (default): the mixer's bf16 in_proj / out_proj run on the HIP GEMM
+                     (vm_linear_fwd: the LDS-DMA tile kernel for small row counts, the
+                     persistent 256-row kernel from 3 tiles per CU up; bit-identical forms)
+                     at every batch, so every row is computed the same way whatever the
+                     row count — chunked streaming == the one-pass forward bit for bit at any
+                     batch; "library": the round-3 rule below (hipBLASLt above 8 clips).
     row_invariant_gemm_clips
-                     mixers holding at most this many clips (default 8: streaming batches)
+                     ("library" mode) mixers holding at most this many clips (default 8)
                      run in_proj / out_proj on the HIP GEMM at every token count, whose rows
                      do not depend on the row count — chunked streaming == the one-pass
                      forward bit for bit; 0: only the small_gemm_* rule below.
@@ -36,7 +42,7 @@ documented options object; tests and sweeps change them with :func:`override`.
                      Measured slower at B = 1 (48 vs 10.9 + 6.9 us per layer: the granule's
                      last workgroup reads the other tiles' rows back from beyond L2), so it
                      is off by default.
-    small_gemm_rows  in_proj / out_proj with at most this many token rows (one clip's
+    small_gemm_rows  ("library" mode) in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
     small_gemm_max_n ... and at most this many output columns (default 1024: out_proj;
@@ -66,6 +72,7 @@ class Options:
     scan_one_launch: bool = True
     scan_dt_proj: str = "auto"
     gemm_tuning: str = "on"
+    projection_gemm: str = "hip"
     row_invariant_gemm_clips: int = 8
     fuse_out_norm: bool = False
     small_gemm_rows: int = 4096
@@ -80,6 +87,8 @@ class Options:
             raise ValueError("small_gemm_rows must be >= 0")
         if self.scan_dt_proj not in ("auto", "on", "off"):
             raise ValueError(f"scan_dt_proj must be auto / on / off, got {self.scan_dt_proj!r}")
+        if self.projection_gemm not in ("hip", "library"):
+            raise ValueError(f"projection_gemm must be hip / library, got {self.projection_gemm!r}")
         if self.gemm_tuning not in _TUNING:
             raise ValueError(f"gemm_tuning must be one of {_TUNING}, got {self.gemm_tuning!r}")
 
