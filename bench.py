@@ -79,8 +79,7 @@ def _args():
     ap.add_argument("--no-b1", action="store_true",
                     help="skip the B=1 chunk latency and per-stage B=1 rooflines (batch sweeps)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="oracle threads (0: os.cpu_count(), SURVEY 8(d); the rate at a one-GPU "
-                         "box's share, min(16, affinity) threads, is reported beside it)")
+                    help="oracle threads (0: every CPU this process may use, see _cpu_share)")
     ap.add_argument("--scan-dt-proj", default="auto", choices=("auto", "on", "off"),
                     help="options.scan_dt_proj: dt_proj inside the scan at chip-filling batches")
     ap.add_argument("--full-sequence", action="store_true",
@@ -93,6 +92,11 @@ def _args():
         # in the partial second round (profiles/r03c_batch_sweep.txt)
         a.batch = CONFIGS[a.config].get("batch", 448)
     return a
+
+
+def _progress(msg):
+    """One progress line on stderr per bench stage (the JSON line stays alone on stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def _sync_barrier(world):
@@ -357,6 +361,24 @@ def _cpu_info():
     return model, affinity
 
 
+def _cpu_share(affinity):
+    """The host CPUs this process may actually run on: OMP_NUM_THREADS when the launcher set
+    it (16 on a one-GPU box), else the cgroup CPU quota, else the affinity mask.
+    os.cpu_count() counts the whole shared host (256 on the GPU boxes): the round-4 bench at
+    256 oracle threads on a 16-CPU share ran past the box's 180 s no-output limit."""
+    env = os.environ.get("OMP_NUM_THREADS", "").strip()
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, affinity or os.cpu_count() or 1)
+
+
 def cpu_baseline(cfg, threads):
     """the CPU path on the host cores, fp32 B=1, one clip of the bench
     config and of C1 (Ti 8x224^2).  The code timed is the oracle (the CPU restatement
@@ -364,21 +386,18 @@ def cpu_baseline(cfg, threads):
     (profiles/r03_cpu_calibration.json, one session, same threads), so the headline
     ``value`` is the reference's rate on these cores estimated from it (the measured
     oracle rate divided by that calibration ratio); the oracle's own rate is ``port_value``.
-    ``threads`` 0 = os.cpu_count(); the rate at a one-GPU box's share of the
-    host (min(16, affinity) threads) is kept beside it.  Median of 2 after 1 warm-up per
-    thread count: a bounded sample (~10-30 s of CPU work) so the bench stays within minutes."""
+    ``threads`` 0 = every CPU this process may use (``_cpu_share``: the box's share of the
+    host; SURVEY 8(d)'s os.cpu_count() counts the whole shared host and oversubscribes the
+    share 16x there).  Median of 2 after 1 warm-up: a bounded sample (~10-30 s of CPU work)
+    so the bench stays within minutes."""
     model, affinity = _cpu_info()
+    share = _cpu_share(affinity)
     if threads <= 0:
-        threads = os.cpu_count() or 1
-    share = max(1, min(16, affinity or 1))
+        threads = share
     ti = CONFIGS["ti8"]
     torch.set_num_threads(threads)
     dt = _oracle_clip_seconds(cfg, runs=2)
     dt_c1 = _oracle_clip_seconds(ti, runs=2)
-    dt_share = None
-    if share != threads:
-        torch.set_num_threads(share)
-        dt_share = _oracle_clip_seconds(cfg, runs=1)
     cal = _cpu_calibration()
     key = {16: "m16", 8: "ti8"}.get(cfg["frames"]) if cfg["embed_dim"] in (576, 192) else None
     ratios = (cal or {}).get("oracle_over_reference_s_per_clip", {})
@@ -392,9 +411,9 @@ def cpu_baseline(cfg, threads):
                             f"({ratio})" if ratio else "the timed oracle's rate (no calibration)"),
             "port_value": round(port, 2),
             "cpu_model": model, "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
-            "share_threads": share,
-            "port_value_share_threads": (round(cfg["frames"] * 196 / dt_share, 2)
-                                         if dt_share else round(port, 2)),
+            "cpu_share": share,
+            "threads_policy": "the CPUs this process may use (OMP_NUM_THREADS / cgroup quota / "
+                              "affinity); os.cpu_count() counts the whole shared host",
             "calibration": cal,
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
                       f"median of 2 after 1 warm-up ({dt:.2f} s at {threads} threads), "
@@ -527,9 +546,11 @@ def main():
             return model(x)
         return model(x, ssm_state=state, temporal_pos_offset=0)
 
+    _progress(f"model built, B={B}: {args.warmup} warm-up + {args.steps} timed steps")
     elapsed, out = _timed_steps(step, args.steps, args.warmup, world, device,
                                 torch.cuda.synchronize)
     assert torch.isfinite(out[1].float()).all()
+    _progress(f"timed: {elapsed / args.steps * 1e3:.1f} ms per step")
     from videomamba_amd import kernels as K
     K.check_scan_sync()  # no one-launch scan hand-off timed out (outside the timed region)
     line = _base_line(args, cfg, world, global_batch, B, elapsed, strong)
@@ -555,6 +576,7 @@ def main():
 
         p50_eager = p50_graph = None
         if not args.no_b1:
+            _progress("B=1 chunk latency (eager, then graph replay)")
             outs = []
             p50_eager = chunk_lat(lambda: outs.append(
                 model(x1, ssm_state=st1, temporal_pos_offset=0)[1]))
@@ -569,6 +591,7 @@ def main():
         mx0 = model.layers[0].mixer
         hn0 = torch.empty((1, 1, cfg["embed_dim"]), device=device,
                           dtype=torch.bfloat16).expand(max(B, 1), 3144, cfg["embed_dim"])
+        _progress("scan roofline leg")
         roof = scan_roofline(max(B, 1), args.scan_reps, device,
                              mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device),
                              dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))
@@ -584,6 +607,7 @@ def main():
         if b1 is not None:
             line["b1_kernels"] = b1
         if world == 1 and not args.no_cpu_baseline:
+            _progress("CPU baseline (oracle)")
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         print(json.dumps(line), flush=True)
     if world > 1:
