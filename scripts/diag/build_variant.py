@@ -54,6 +54,10 @@ VARIANTS = {
                 "  if (cact && tok0 < 0) {\n#pragma unroll\n    for (int i = 0; i < 16; ++i) {\n      const int tok = tok0 + t0 + i;")],
     "cx_noload": [("vm_conv_proj_sk.hip", "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch)",
                    "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch && tok0 < 0)")],
+    # persistent GEMM: tight wait before the output stores, the next tile's first two waits
+    # skipped (kTileStoreWait 1) instead of draining the stores at the next wait
+    "tg_sw1": [("vm_gemm_tile.hip", "constexpr int kTileStoreWait = 0;",
+                "constexpr int kTileStoreWait = 1;")],
     # dt_proj-in-scan kernel (scan_seq_dtp_kernel) pricing (results wrong): no dt block
     # (dtp_nodt), no per-quad LDS reads of dt (dtp_noquad)
     "dtp_nodt": [("vm_scan_seq.hip", """    if (j == 12) dt_store();""",

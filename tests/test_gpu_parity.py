@@ -996,3 +996,20 @@ def test_persistent_linear_rejects_unsupported_shapes():
         K.linear(x, w, form="persistent")
     y = K.linear(x, w)
     assert torch.equal(y, K.linear(x, w, form="dma"))
+
+
+def test_persistent_linear_is_repeatable_at_chip_filling_rows():
+    """The persistent GEMM at the C4 B=72 projection shapes (226,368 rows: ~3.5 tiles per
+    workgroup run) gives the same bits launch after launch.  Its first build counted the
+    previous tile's output stores as ops younger than an awaited LDS-DMA half-tile; a store
+    that completed before an older load let a wave read a half-tile that had not landed (1
+    launch in 30 differed, scripts/diag/determinism_b72.py)."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    m = 72 * 3144
+    for n, k in [(2304, 576), (576, 1152)]:
+        x = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
+        w = (torch.randn(n, k, device=DEV, generator=g) * k ** -0.5).to(torch.bfloat16)
+        r0 = K.linear(x, w, form="persistent")
+        bad = sum(int(not torch.equal(K.linear(x, w, form="persistent"), r0)) for _ in range(40))
+        assert bad == 0, (n, k, bad)
+        del x, w, r0

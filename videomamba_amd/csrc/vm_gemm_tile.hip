@@ -22,6 +22,11 @@
 //     registers for the quadrants that reuse them), one half-tile is issued per phase, and
 //     each is issued 4-5 phases before its read: counted vmcnt waits (8, never 0), raw
 //     s_barrier, two barriers per phase;
+//   * vmcnt counts the output stores too, and a store may complete before an older
+//     LDS-DMA load (LLVM treats mixed VMEM reads / writes on vmcnt as out of order): a wait
+//     that allowed the S stores of the previous tile as "younger ops" let a wave read a
+//     half-tile that had not landed (1 launch in 30 differed at B = 72,
+//     scripts/diag/determinism_b72.py).  No wait counts a store; see kTileStoreWait;
 //   * waves 4-7 (the SIMD partners of waves 0-3) run one barrier behind (stagger), so a
 //     SIMD's two waves alternate MFMA and LDS / issue segments;
 //   * the MFMA computes out^T tiles (A operand = W rows, B operand = x rows): a lane holds 4
@@ -99,6 +104,14 @@ struct TileRes {  // one output tile: its x rows' buffer, its w rows' offset, it
   int t;      // tile index, -1 past the workgroup's run
 };
 
+// How the waits around a tile's output stores stay exact (stores never count as "younger"):
+//   0: every wait is vmcnt(8): the first wait after the stores (the next tile's first phase)
+//      also waits for them to complete;
+//   1: the last phase before the stores waits vmcnt(4) (also covering the two half-tiles
+//      the next tile's first two waits would retire), those two waits are skipped, and the
+//      next tile's phase-3 wait, vmcnt(8), drains the stores a K-tile later.
+constexpr int kTileStoreWait = 0;
+
 }  // namespace
 
 template <int WGM, int TMH, int TNH, int NK>
@@ -114,7 +127,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   constexpr int VM = 8;                  // loads younger than an awaited half-tile: 4 x 2
   static_assert(WGM * WGN == 8 && HA == 128 && (HB == 128 || HB == 96), "tile geometry");
   static_assert(NK >= 3, "the prefetch reaches two K-tiles ahead inside one tile");
-  static_assert(VM + S < 64, "vmcnt range");
+  static_assert(S <= 16, "output stores per wave per tile");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
   const int tid = threadIdx.x;
@@ -283,21 +296,16 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   // of descriptors captured by the lambdas below stays in memory and loses uniformity)
   TileRes cur0 = tile_res(0), cur1 = tile_res(TPI == 2 ? 1 : ntiles), nxt = tile_res(TPI);
 
-  // ---- prologue: K-tiles 0 (all four halves) and 1 (A top, B left) of the first tile,
-  // then S out-of-range stores so every tile's first K-tile sees the same vmcnt history
+  // ---- prologue: K-tiles 0 (all four halves) and 1 (A top, B left) of the first tile;
+  // the wait retires what the first phases read before their own waits run (A top / B left
+  // of K-tile 0; kTileStoreWait 1 skips the first two waits: all of K-tile 0)
   issue(cur0, 0, 0, 0);
   issue(cur0, 2, 0, 0);
   issue(cur0, 3, 0, 0);
   issue(cur0, 1, 0, 0);
   issue(cur0, 0, 1, 1);
   issue(cur0, 2, 1, 1);
-  tg_wait_vm<VM>();
-  {
-    const auto null_o = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0, 0x00020000);
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      __builtin_amdgcn_raw_buffer_store_b128(tg_i32x4{0, 0, 0, 0}, null_o, 0, 0, 0);
-  }
+  tg_wait_vm<kTileStoreWait == 1 ? VM / 2 : VM>();
   tg_barrier();
   if (wave >= 4) tg_barrier();  // stagger: waves 4-7 run one barrier behind
 
@@ -319,9 +327,13 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       if constexpr (P == 2) read_a(buf, 1);
       __builtin_amdgcn_sched_barrier(0);
       tg_wait_lgkm0();
-      // 3. retire the half-tile(s) the next phase reads (stores of the previous tile are
-      //    younger than them during a tile's first K-tile)
-      if constexpr (P != 2) tg_wait_vm<kt == 0 ? VM + S : VM>();
+      // 3. retire the half-tile(s) the next phase reads (never counting output stores)
+      if constexpr (kTileStoreWait == 0) {
+        if constexpr (P != 2) tg_wait_vm<VM>();
+      } else {
+        if constexpr (P == 3 && kt == NK - 1) tg_wait_vm<VM / 2>();  // before the stores
+        else if constexpr (P == 3 || (P == 0 && kt != 0) || (P == 1 && kt != 0)) tg_wait_vm<VM>();
+      }
       tg_barrier();
       // 4. the quadrant's MFMAs
       if constexpr (P == 0) mfma(0, 0);
