@@ -54,6 +54,14 @@ VARIANTS = {
                 "  if (cact && tok0 < 0) {\n#pragma unroll\n    for (int i = 0; i < 16; ++i) {\n      const int tok = tok0 + t0 + i;")],
     "cx_noload": [("vm_conv_proj_sk.hip", "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch)",
                    "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch && tok0 < 0)")],
+    # persistent GEMM: s_setprio around each MFMA quadrant (tg_prio1) / waves 4-7 at
+    # priority 1 throughout (tg_prio2)
+    "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
+    "tg_prio2": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 2;")],
+    # chunked scan: 16-wave workgroups (one state per wave in the composition / hand-off,
+    # 4 waves per SIMD) instead of 8
+    "ch16": [("vm_scan_seq.hip", "constexpr int kChW = 8;  // segments (waves) per workgroup",
+              "constexpr int kChW = 16;  // segments (waves) per workgroup")],
     # persistent GEMM: tight wait before the output stores, the next tile's first two waits
     # skipped (kTileStoreWait 1) instead of draining the stores at the next wait
     "tg_sw1": [("vm_gemm_tile.hip", "constexpr int kTileStoreWait = 0;",

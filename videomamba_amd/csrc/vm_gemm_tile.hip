@@ -111,6 +111,9 @@ struct TileRes {  // one output tile: its x rows' buffer, its w rows' offset, it
 //      the next tile's first two waits would retire), those two waits are skipped, and the
 //      next tile's phase-3 wait, vmcnt(8), drains the stores a K-tile later.
 constexpr int kTileStoreWait = 0;
+// s_setprio around the MFMA clusters: 0 none, 1 setprio(1) / (0) around each quadrant's MFMAs
+// (cdna_hip_programming.md T5), 2 waves 4-7 at priority 1 for the whole loop (T5 static form)
+constexpr int kTilePrio = 0;
 
 }  // namespace
 
@@ -308,6 +311,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   tg_wait_vm<kTileStoreWait == 1 ? VM / 2 : VM>();
   tg_barrier();
   if (wave >= 4) tg_barrier();  // stagger: waves 4-7 run one barrier behind
+  if constexpr (kTilePrio == 2) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
 
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
@@ -336,10 +342,12 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       }
       tg_barrier();
       // 4. the quadrant's MFMAs
+      if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(1);
       if constexpr (P == 0) mfma(0, 0);
       if constexpr (P == 1) mfma(0, 1);
       if constexpr (P == 2) mfma(1, 1);
       if constexpr (P == 3) mfma(1, 0);
+      if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(0);
       tg_barrier();
       // 5. the tile is done after its last quadrant: store it, restart the accumulators
       if constexpr (P == 3 && kt == NK - 1) {

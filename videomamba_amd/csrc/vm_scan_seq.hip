@@ -794,6 +794,9 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
 // Compared with the summary / carry / final form it replaces for SGPR-eligible operands,
 // the carry never leaves the chip's LDS except for one aggregate per block.
 constexpr int kChW = 8;  // segments (waves) per workgroup
+constexpr int kChSPW = kMaxN / kChW;  // states a wave composes / publishes / walks
+constexpr int kChPoll = kChSPW == 2 ? 8 : 4;  // preceding blocks polled per round (one-launch)
+static_assert(kMaxN % kChW == 0 && (kChSPW == 1 || kChSPW == 2), "1 or 2 states per wave");
 
 struct ChunkWork {
   float* segE;  // [B][nblk][kChW][D][kMaxN]  entry offsets (log2 units)
@@ -810,6 +813,9 @@ struct ChunkWork {
 };
 
 template <bool V> struct BoolTag { static constexpr bool value = V; };
+// a thread's share of a block aggregate row (K consecutive states of one channel), loaded as
+// one 4 * K-byte access
+template <int K> struct alignas(4 * K) AggShare { float v[K] = {}; };
 
 template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>
 __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w) {
@@ -821,6 +827,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   __shared__ float sH[kChW][kMaxN][64];
   __shared__ float sS[kChW][64];
   __shared__ float sA[kMaxN][64];
+  __shared__ float sHb[PASS == 3 ? kMaxN : 1][64];  // one-launch form: the block entry state
   __shared__ unsigned s_tag;  // one-launch form: this launch's hand-off tag
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -848,29 +855,37 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // touched ~32 cache lines per wave-instruction, and with 8 waves each issuing ~80 of them
   // the address path, not the memory, set the kernel's start-up time at B = 1.
   //   A: the group's 64 x N floats are contiguous — 2 coalesced dwords per thread
-  float aval[2];
+  float aval[kChSPW];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kChSPW; ++k) {
     const int e = tid + k * 64 * kChW;  // element of the [64][N] tile
     aval[k] = e < nch * N ? ps.A[static_cast<long long>(d0) * N + e] : 0.0f;
   }
   const float Dv = (ps.D ? ps.D[d] : 0.0f) * kLog2e;
   const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * kLog2e;
-  // states this wave composes across segments / blocks: 2 * wave, 2 * wave + 1
-  const int n0 = 2 * wave;
+  // states this wave composes across segments / blocks: kChSPW * wave (+ 1)
+  const int n0 = kChSPW * wave;
 
   // PASS 2 entry operands: this segment's entry offset and delta prefix, the entry state's
   // two composed states, and the aggregates of up to kCW preceding blocks (each block's 64
   // channels x 16 states are one contiguous 4 KB row: a coalesced float2 per thread)
   constexpr int kCW = 16;
-  float Pj = 0.0f, H0 = 0.0f, H1 = 0.0f;
+  // one thread's share of a block aggregate's 64 channels x 16 states: kChSPW consecutive
+  // states of channel tid / (16 / kChSPW)
+  constexpr int kTPC = kMaxN / kChSPW;  // threads per channel
+  typedef AggShare<kChSPW> agv_t;
+  float Pj = 0.0f;
+  float Hs[kChSPW];
+#pragma unroll
+  for (int i = 0; i < kChSPW; ++i) Hs[i] = 0.0f;
   f2 Ej[kMaxN / 2];
-  f2 agH[kCW];
+  agv_t agH[kCW];
   float agS[kCW * 64 / (64 * kChW)];
   if constexpr (PASS == 3) {
     if (ps.h0) {
-      if (n0 < N) H0 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0, p.h0_dtype);
-      if (n0 + 1 < N) H1 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + 1, p.h0_dtype);
+#pragma unroll
+      for (int i = 0; i < kChSPW; ++i)
+        if (n0 + i < N) Hs[i] = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + i, p.h0_dtype);
     }
   }
   if constexpr (PASS == 2) {
@@ -883,15 +898,16 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       Ej[2 * q + 1] = f2{v.z, v.w};
     }
     if (ps.h0) {
-      if (n0 < N) H0 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0, p.h0_dtype);
-      if (n0 + 1 < N) H1 = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + 1, p.h0_dtype);
+#pragma unroll
+      for (int i = 0; i < kChSPW; ++i)
+        if (n0 + i < N) Hs[i] = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + i, p.h0_dtype);
     }
-    const int ci = tid >> 3;  // channel of this thread's state pair
+    const int ci = tid / kTPC;  // channel of this thread's states
 #pragma unroll
     for (int j = 0; j < kCW; ++j) {
-      agH[j] = f2{0.0f, 0.0f};
+      agH[j] = agv_t{};
       if (j < blk && ci < nch)
-        agH[j] = *reinterpret_cast<const f2*>(&w.aggH[(rowA + j * D + d0) * kMaxN + 2 * tid]);
+        agH[j] = *reinterpret_cast<const agv_t*>(&w.aggH[(rowA + j * D + d0) * kMaxN + kChSPW * tid]);
     }
 #pragma unroll
     for (int k = 0; k < kCW / kChW; ++k) {
@@ -899,6 +915,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       agS[k] = j < blk && lane < nch ? w.aggS[rowA + j * D + d0 + lane] : 0.0f;
     }
   }
+  // a thread's aggregate share -> LDS sH[j][state][channel]
+  auto stage_agg = [&](int j, const agv_t& v) {
+    const int c = tid / kTPC, n = kChSPW * (tid % kTPC);
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) sH[j][n + i][c] = v.v[i];
+  };
   const int voff = lane * ES;
   const int voff_st = active ? voff : kSeqDead;
   const auto ur = uniform_rsrc(static_cast<const T*>(p.u) + b * p.u_sb + d0);
@@ -988,7 +1010,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   }
   // A transposed into LDS: sA[n][c] (zero for n >= N and for channels past dim)
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kChSPW; ++k) {
     const int e = tid + k * 64 * kChW;
     if (e < 64 * N) sA[e % N][e / N] = aval[k];
     if (e >= 64 * N && e < 64 * kMaxN) sA[e >> 6][e & 63] = 0.0f;
@@ -996,10 +1018,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   if constexpr (PASS == 2) {
     // the first kChW block aggregates go to LDS with A: [block][state][channel]
 #pragma unroll
-    for (int j = 0; j < kChW; ++j) {
-      sH[j][2 * (tid & 7)][tid >> 3] = agH[j].x;
-      sH[j][2 * (tid & 7) + 1][tid >> 3] = agH[j].y;
-    }
+    for (int j = 0; j < kChW; ++j) stage_agg(j, agH[j]);
     sS[tid >> 6][lane] = agS[0];
   }
   __syncthreads();
@@ -1009,10 +1028,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};
     h[q] = f2{0.0f, 0.0f};
   }
-  const float An0 = sA[n0][lane], An1 = sA[n0 + 1][lane];
+  float Ans[kChSPW];
+#pragma unroll
+  for (int i = 0; i < kChSPW; ++i) Ans[i] = sA[n0 + i][lane];
   if constexpr (PASS == 2) {
-    H0 *= kLog2e;  // log2 units
-    H1 *= kLog2e;
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) Hs[i] *= kLog2e;  // log2 units
     // walk the preceding blocks' aggregates from h0 to this block's entry, kChW at a time
     // through LDS (the second group from registers loaded with the start-up round)
     for (int r0 = 0; r0 < blk; r0 += kChW) {
@@ -1020,20 +1041,17 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         __syncthreads();  // every wave is done reading the previous group
         if (r0 < kCW) {
 #pragma unroll
-          for (int j = 0; j < kChW; ++j) {
-            sH[j][2 * (tid & 7)][tid >> 3] = agH[kChW + j].x;
-            sH[j][2 * (tid & 7) + 1][tid >> 3] = agH[kChW + j].y;
-          }
-          sS[tid >> 6][lane] = agS[1];
+          for (int j = 0; j < kChW; ++j) stage_agg(j, agH[(kChW + j) % kCW]);
+          sS[tid >> 6][lane] = agS[(kCW / kChW) - 1];
         } else {  // long sequences: later groups are loaded here
-          const int ci = tid >> 3;
+          const int ci = tid / kTPC;
 #pragma unroll
           for (int j = 0; j < kChW; ++j) {
-            f2 v{0.0f, 0.0f};
+            agv_t v{};
             if (r0 + j < blk && ci < nch)
-              v = *reinterpret_cast<const f2*>(&w.aggH[(rowA + (r0 + j) * D + d0) * kMaxN + 2 * tid]);
-            sH[j][2 * (tid & 7)][ci] = v.x;
-            sH[j][2 * (tid & 7) + 1][ci] = v.y;
+              v = *reinterpret_cast<const agv_t*>(
+                  &w.aggH[(rowA + (r0 + j) * D + d0) * kMaxN + kChSPW * tid]);
+            stage_agg(j, v);
           }
           const int j = r0 + (tid >> 6);
           sS[tid >> 6][lane] = j < blk && lane < nch ? w.aggS[rowA + j * D + d0 + lane] : 0.0f;
@@ -1043,13 +1061,14 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       const int nj = min(kChW, blk - r0);
       for (int j = 0; j < nj; ++j) {
         const float Sj = sS[j][lane];
-        H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, sH[j][n0][lane]);
-        H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, sH[j][n0 + 1][lane]);
+#pragma unroll
+        for (int i = 0; i < kChSPW; ++i)
+          Hs[i] = fmaf(__builtin_amdgcn_exp2f(Ans[i] * Sj), Hs[i], sH[j][n0 + i][lane]);
       }
     }
     __syncthreads();  // sH[0] is rewritten with the block entry
-    sH[0][n0][lane] = H0;
-    sH[0][n0 + 1][lane] = H1;
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) sH[0][n0 + i][lane] = Hs[i];
     __syncthreads();
     // this segment's entry: exp2(A P_j) * H_blk + E_j
 #pragma unroll
@@ -1173,28 +1192,34 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // compose the block's segments for states n0, n0 + 1: entry offsets E_j, delta prefixes
   // P_j and the block aggregate (PASS 1: all to the workspace; one-launch form: E_j back into
   // sH[j] in place, the aggregate to the workspace for the blocks after this one)
-  float E0 = 0.0f, E1 = 0.0f, P = 0.0f, Pw = 0.0f;
+  float Es[kChSPW], P = 0.0f, Pw = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kChSPW; ++i) Es[i] = 0.0f;
 #pragma unroll
   for (int j = 0; j < kChW; ++j) {
     const float Sj = sS[j][lane];
-    const float Hj0 = sH[j][n0][lane], Hj1 = sH[j][n0 + 1][lane];
+    float Hj[kChSPW];
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) Hj[i] = sH[j][n0 + i][lane];
     if constexpr (PASS == 1) {
       if (active) {
-        *reinterpret_cast<f2*>(&w.segE[(rowE + j * D + d) * kMaxN + n0]) = f2{E0, E1};
+#pragma unroll
+        for (int i = 0; i < kChSPW; ++i) w.segE[(rowE + j * D + d) * kMaxN + n0 + i] = Es[i];
         if (wave == 0) w.segP[rowE + j * D + d] = P;
       }
     } else {
-      sH[j][n0][lane] = E0;
-      sH[j][n0 + 1][lane] = E1;
+#pragma unroll
+      for (int i = 0; i < kChSPW; ++i) sH[j][n0 + i][lane] = Es[i];
       if (j == wave) Pw = P;
     }
-    E0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), E0, Hj0);
-    E1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), E1, Hj1);
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) Es[i] = fmaf(__builtin_amdgcn_exp2f(Ans[i] * Sj), Es[i], Hj[i]);
     P += Sj;
   }
   if constexpr (PASS != 3) {
     if (active) {
-      *reinterpret_cast<f2*>(&w.aggH[(rowA + blk * D + d) * kMaxN + n0]) = f2{E0, E1};
+#pragma unroll
+      for (int i = 0; i < kChSPW; ++i) w.aggH[(rowA + blk * D + d) * kMaxN + n0 + i] = Es[i];
       if (wave == 0) w.aggS[rowA + blk * D + d] = P;
     }
   }
@@ -1212,10 +1237,10 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     unsigned long long* gb =
         w.gran + ((static_cast<long long>(b) * gridDim.x + gx) * w.nblk) * ((kMaxN + 1) * 64);
     unsigned long long* gmine = gb + static_cast<long long>(blk) * ((kMaxN + 1) * 64);
-    __hip_atomic_store(gmine + n0 * 64 + lane, tg | __float_as_uint(E0), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(gmine + (n0 + 1) * 64 + lane, tg | __float_as_uint(E1), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i)
+      __hip_atomic_store(gmine + (n0 + i) * 64 + lane, tg | __float_as_uint(Es[i]),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == 0)
       __hip_atomic_store(gmine + kMaxN * 64 + lane, tg | __float_as_uint(P), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -1224,10 +1249,6 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    // this segment's entry offsets (composed by the 8 waves) into registers
-    f2 Ew[kMaxN / 2];
-#pragma unroll
-    for (int q = 0; q < kMaxN / 2; ++q) Ew[q] = f2{sH[wave][2 * q][lane], sH[wave][2 * q + 1][lane]};
     // PASS 2 operands of the first kPF steps, in flight during the wait
     if (t_beg < t_end) {
       bc_load(t_beg, bcw[0]);
@@ -1241,62 +1262,66 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       }
     }
     // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----
-    // Wave w needs only its own states n0, n0 + 1 (and the delta sums) of each preceding
-    // block: 3 granules per block and lane, polled 8 blocks at a time.  Blocks are
+    // Wave w needs only its own states n0 (, n0 + 1) and the delta sums of each preceding
+    // block: kChSPW + 1 granules per block and lane, polled kChPoll blocks at a time.  Blocks are
     // dispatched in order and the host launches this form only when the whole grid is
     // co-resident, so every block waited on is running or done; the poll is bounded anyway
     // so a broken assumption can never hang the GPU: a wave whose poll runs out sets the
     // sticky error word and poisons its states with NaN, so every output and h_last of the
     // block is NaN — never a plausible wrong value.
-    H0 *= kLog2e;  // log2 units
-    H1 *= kLog2e;
-    for (int r0 = 0; r0 < blk; r0 += kChW) {
-      const int nj = min(kChW, blk - r0);
-      unsigned long long g0[kChW], g1[kChW], gs[kChW];
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) Hs[i] *= kLog2e;  // log2 units
+    for (int r0 = 0; r0 < blk; r0 += kChPoll) {
+      const int nj = min(kChPoll, blk - r0);
+      unsigned long long gh[kChSPW][kChPoll], gs[kChPoll];
       unsigned spins = 0;
       for (;;) {
         bool ok = true;
 #pragma unroll
-        for (int j = 0; j < kChW; ++j) {
+        for (int j = 0; j < kChPoll; ++j) {
           const unsigned long long* gj =
               gb + static_cast<long long>(r0 + (j < nj ? j : 0)) * ((kMaxN + 1) * 64);
-          g0[j] = __hip_atomic_load(gj + n0 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          g1[j] = __hip_atomic_load(gj + (n0 + 1) * 64 + lane, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int i = 0; i < kChSPW; ++i)
+            gh[i][j] = __hip_atomic_load(gj + (n0 + i) * 64 + lane, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
           gs[j] = __hip_atomic_load(gj + kMaxN * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
 #pragma unroll
-        for (int j = 0; j < kChW; ++j)
-          ok = ok && static_cast<unsigned>(g0[j] >> 32) == tag &&
-               static_cast<unsigned>(g1[j] >> 32) == tag && static_cast<unsigned>(gs[j] >> 32) == tag;
+        for (int j = 0; j < kChPoll; ++j) {
+          ok = ok && static_cast<unsigned>(gs[j] >> 32) == tag;
+#pragma unroll
+          for (int i = 0; i < kChSPW; ++i) ok = ok && static_cast<unsigned>(gh[i][j] >> 32) == tag;
+        }
         if (__all(ok)) break;
         if (++spins >= (1u << 20)) {
           if (lane == 0) __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          H0 = __builtin_nanf("");
-          H1 = __builtin_nanf("");
+#pragma unroll
+          for (int i = 0; i < kChSPW; ++i) Hs[i] = __builtin_nanf("");
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
 #pragma unroll
-      for (int j = 0; j < kChW; ++j) {
+      for (int j = 0; j < kChPoll; ++j) {
         if (j < nj) {  // (static register indices: a runtime bound would spill the arrays)
           const float Sj = __uint_as_float(static_cast<unsigned>(gs[j]));
-          H0 = fmaf(__builtin_amdgcn_exp2f(An0 * Sj), H0, __uint_as_float(static_cast<unsigned>(g0[j])));
-          H1 = fmaf(__builtin_amdgcn_exp2f(An1 * Sj), H1, __uint_as_float(static_cast<unsigned>(g1[j])));
+#pragma unroll
+          for (int i = 0; i < kChSPW; ++i)
+            Hs[i] = fmaf(__builtin_amdgcn_exp2f(Ans[i] * Sj), Hs[i],
+                         __uint_as_float(static_cast<unsigned>(gh[i][j])));
         }
       }
     }
-    __syncthreads();  // sH[0] is rewritten with the block entry
-    sH[0][n0][lane] = H0;
-    sH[0][n0 + 1][lane] = H1;
+#pragma unroll
+    for (int i = 0; i < kChSPW; ++i) sHb[n0 + i][lane] = Hs[i];
     __syncthreads();
-    // this segment's entry: exp2(A P_j) * H_blk + E_j
+    // this segment's entry: exp2(A P_j) * H_blk + E_j (E_j composed into sH[j] above)
 #pragma unroll
     for (int q = 0; q < kMaxN / 2; ++q) {
       const f2 x = A2[q] * f2{Pw, Pw};
-      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), sH[0][2 * q][lane], Ew[q].x),
-                fmaf(__builtin_amdgcn_exp2f(x.y), sH[0][2 * q + 1][lane], Ew[q].y)};
+      h[q] = f2{fmaf(__builtin_amdgcn_exp2f(x.x), sHb[2 * q][lane], sH[wave][2 * q][lane]),
+                fmaf(__builtin_amdgcn_exp2f(x.y), sHb[2 * q + 1][lane], sH[wave][2 * q + 1][lane])};
     }
     run_steps(BoolTag<true>{});
     finish();
