@@ -57,6 +57,7 @@ VARIANTS = {
     # persistent GEMM: s_setprio around each MFMA quadrant (tg_prio1) / waves 4-7 at
     # priority 1 throughout (tg_prio2)
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
+    "tg_lgkm0": [("vm_gemm_tile.hip", "constexpr bool kTileLgkmLate = true;", "constexpr bool kTileLgkmLate = false;")],
     "tg_prio2": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 2;")],
     # chunked scan: 16-wave workgroups (one state per wave in the composition / hand-off,
     # 4 waves per SIMD) instead of 8

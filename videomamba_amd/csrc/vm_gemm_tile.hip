@@ -114,6 +114,14 @@ constexpr int kTileStoreWait = 0;
 // s_setprio around the MFMA clusters: 0 none, 1 setprio(1) / (0) around each quadrant's MFMAs
 // (cdna_hip_programming.md T5), 2 waves 4-7 at priority 1 for the whole loop (T5 static form)
 constexpr int kTilePrio = 0;
+// where a phase waits for its own fragment reads: false before its first barrier, true after
+// it (just before the MFMAs: the reads overlap the barrier wait; cdna_hip_programming.md's
+// 8-phase template order)
+constexpr bool kTileLgkmLate = true;
+// (Reading phase 1's B-right fragments right after phase 0's first barrier, to overlap
+// phase 0's MFMAs, reads an unlanded half-tile: waves 4-7 pass their phase-0 wait only after
+// that barrier — the stagger needs the read one phase after the wait; measured wrong in every
+// launch.)
 
 }  // namespace
 
@@ -332,7 +340,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       if constexpr (P == 1) read_b(buf, 1);
       if constexpr (P == 2) read_a(buf, 1);
       __builtin_amdgcn_sched_barrier(0);
-      tg_wait_lgkm0();
+      if constexpr (!kTileLgkmLate) tg_wait_lgkm0();
       // 3. retire the half-tile(s) the next phase reads (never counting output stores)
       if constexpr (kTileStoreWait == 0) {
         if constexpr (P != 2) tg_wait_vm<VM>();
@@ -341,6 +349,10 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
         else if constexpr (P == 3 || (P == 0 && kt != 0) || (P == 1 && kt != 0)) tg_wait_vm<VM>();
       }
       tg_barrier();
+      if constexpr (kTileLgkmLate) {
+        tg_wait_lgkm0();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // 4. the quadrant's MFMAs
       if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(1);
       if constexpr (P == 0) mfma(0, 0);
