@@ -57,8 +57,17 @@ VARIANTS = {
     # persistent GEMM: s_setprio around each MFMA quadrant (tg_prio1) / waves 4-7 at
     # priority 1 throughout (tg_prio2)
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
+    # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
+    "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",
+                  "constexpr bool kTileStamps = true;\n\n}  // namespace\n\n__device__ unsigned long long g_tg_stamps[1024];\n"
+                  "__device__ void tg_stamp_sink(int idx, unsigned long long t) { if (idx < 1024) g_tg_stamps[idx] = t; }"),
+                 ("vm_gemm_tile.hip", "#undef VM_TG_CFG\n#undef VM_TG_K\n",
+                  "#undef VM_TG_CFG\n#undef VM_TG_K\n}  // namespace vm\nextern \"C\" int vm_tile_stamps(unsigned long long* host) {\n"
+                  "  return hipMemcpyFromSymbol(host, HIP_SYMBOL(vm::g_tg_stamps), sizeof(vm::g_tg_stamps)) == hipSuccess ? 0 : -1;\n}\nnamespace vm {\n")],
     "tg_lgkm0": [("vm_gemm_tile.hip", "constexpr bool kTileLgkmLate = true;", "constexpr bool kTileLgkmLate = false;")],
     "tg_prio2": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 2;")],
+    # dt_proj-in-scan kernel: each step's y epilogue in its own step's region (before r04)
+    "dtp_yearly": [("vm_scan_seq.hip", "constexpr bool kDtpYLate = true;", "constexpr bool kDtpYLate = false;")],
     # chunked scan: 16-wave workgroups (one state per wave in the composition / hand-off,
     # 4 waves per SIMD) instead of 8
     "ch16": [("vm_scan_seq.hip", "constexpr int kChW = 8;  // segments (waves) per workgroup",

@@ -123,7 +123,14 @@ constexpr bool kTileLgkmLate = true;
 // that barrier — the stagger needs the read one phase after the wait; measured wrong in every
 // launch.)
 
+// Phase timestamps for probe builds (scripts/diag/build_variant.py tg_stamp): s_memtime at
+// five points of every phase of one steady-state iteration, waves 0 and 4 of workgroup 0.
+// Off in the product (the calls are discarded; the sink is defined only by the probe build).
+constexpr bool kTileStamps = false;
+
 }  // namespace
+
+__device__ void tg_stamp_sink(int idx, unsigned long long t);
 
 template <int WGM, int TMH, int TNH, int NK>
 __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) {
@@ -328,6 +335,14 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
     static_for<QI * 4>([&](auto ic) __attribute__((always_inline)) {
       constexpr int q = decltype(ic)::value / 4, P = decltype(ic)::value % 4;
       constexpr int kt = q % NK, tp = q / NK, buf = q & 1;
+      auto stamp = [&](int point) __attribute__((always_inline)) {
+        if constexpr (kTileStamps) {
+          if (blockIdx.x == 0 && it == 2 && (wave == 0 || wave == 4) && lane == 0)
+            tg_stamp_sink(((wave >> 2) * (QI * 4) + decltype(ic)::value) * 5 + point,
+                          __builtin_amdgcn_s_memtime());
+        }
+      };
+      stamp(0);
       // 1. this phase's half-tile: p0 B right (q+1), p1 A bottom (q+1), p2 A top (q+2),
       //    p3 B left (q+2); past the iteration it belongs to the next one's first tile
       constexpr int qt = q + (P < 2 ? 1 : 2);
@@ -348,7 +363,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
         if constexpr (P == 3 && kt == NK - 1) tg_wait_vm<VM / 2>();  // before the stores
         else if constexpr (P == 3 || (P == 0 && kt != 0) || (P == 1 && kt != 0)) tg_wait_vm<VM>();
       }
+      stamp(1);
       tg_barrier();
+      stamp(2);
       if constexpr (kTileLgkmLate) {
         tg_wait_lgkm0();
         __builtin_amdgcn_sched_barrier(0);
@@ -360,7 +377,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       if constexpr (P == 2) mfma(1, 1);
       if constexpr (P == 3) mfma(1, 0);
       if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(0);
+      stamp(3);
       tg_barrier();
+      stamp(4);
       // 5. the tile is done after its last quadrant: store it, restart the accumulators
       if constexpr (P == 3 && kt == NK - 1) {
         if constexpr (tp == 0) store_tile(cur0);

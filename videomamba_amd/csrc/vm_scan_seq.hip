@@ -518,6 +518,10 @@ __global__ __launch_bounds__(64 * NW) void scan_seq_kernel(const ScanParams p, c
 // Every token's dt is computed from its own x_dbl row in a fixed order, so the result does
 // not depend on the sequence length (chunked == full stays exact).
 constexpr int kDtG = 16;    // steps per dt block
+// the y epilogue of a step (pair sum, gate, bf16 round, store) runs in the next step's
+// scheduling region, where the independent state updates fill the dependent chain's hazard
+// gaps (s_nop) instead of the step's tail
+constexpr bool kDtpYLate = true;
 constexpr int kDtRow = 10;  // dwords per channel row of the LDS dt block (16 bf16 + pad)
 
 typedef short dtp_s4 __attribute__((ext_vector_type(4)));
@@ -685,6 +689,15 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   __builtin_amdgcn_s_waitcnt(0);
   float dl_nx = delta_of(dt_of(dqa[0], 0));
   float g_nx = gate_of(rz[0]);
+  // kDtpYLate: the previous step's y accumulators, gate and store offset (dead: out of range)
+  f2 ya_p = {0.0f, 0.0f}, yb_p = {0.0f, 0.0f};
+  float gf_p = 0.0f;
+  int vo_p = kSeqDead, so_p = 0;
+  auto y_finish = [&](const f2& ya, const f2& yb, float gf, int vo, int so) {
+    const f2 ys = ya + yb;
+    const float y = (ys.x + ys.y) * gf;
+    bstore<T>(from_f32<T>(y), orr, vo, so);
+  };
 
   // One step: t, slot j = t % 16 within the dt block; refill slot j % kPF at (vu, su)/(vz, sz).
   auto step = [&](const int t, const int j, const bool live, const int vu, const int su,
@@ -699,6 +712,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     // the block bookkeeping goes after that wait, so the next step's lgkmcnt(0) (a step
     // later) is the first to wait for its LDS reads / writes
     mid();
+    if constexpr (kDtpYLate) y_finish(ya_p, yb_p, gf_p, vo_p, so_p);
     // the next step's delta and gate a step early (as scan_seq_kernel); its dt sits in the
     // current quad, the next quad (j % 4 == 3), or the next block's first quad (j == 15)
     float dl = dl_nx;
@@ -725,9 +739,15 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
       if (qq & 1) yb = __builtin_elementwise_fma(h[qq], Cp, yb);
       else ya = __builtin_elementwise_fma(h[qq], Cp, ya);
     }
-    const f2 ys = ya + yb;
-    const float y = (ys.x + ys.y) * gf;
-    bstore<T>(from_f32<T>(y), orr, live ? voff : kSeqDead, t * os);
+    if constexpr (kDtpYLate) {
+      ya_p = ya;
+      yb_p = yb;
+      gf_p = gf;
+      vo_p = live ? voff : kSeqDead;
+      so_p = t * os;
+    } else {
+      y_finish(ya, yb, gf, live ? voff : kSeqDead, t * os);
+    }
   };
   // block bookkeeping in step j of the block starting at tg: prefetch the next block's
   // A fragments at j == 0, the next quad at j % 4 == 0 (j < 12); the next block's dt: the
@@ -766,6 +786,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
       step(t, j, t < L, voff, tn * us, voff, tn * zs, [&]() { around(t0, j); });
     }
   }
+  if constexpr (kDtpYLate) y_finish(ya_p, yb_p, gf_p, vo_p, so_p);  // the last step's y
   if (L > 0) {
 #pragma unroll
     for (int n = 0; n < kMaxN; ++n)
