@@ -115,6 +115,21 @@ def test_bench_metric_name_is_the_baseline_metric_for_c3():
     assert bench.metric_name(bench.CONFIGS["m16"]) == want
 
 
+def test_bench_cpu_baseline_threads_are_the_process_share(monkeypatch):
+    """The CPU baseline runs on the CPUs the bench process may use: OMP_NUM_THREADS when set
+    (16 on a one-GPU box), else the cgroup quota or the affinity mask — never the whole
+    shared host that os.cpu_count() reports."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench._cpu_share(256) == 16
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    share = bench._cpu_share(3)
+    assert 1 <= share <= max(3, os.cpu_count() or 1)
+
+
 def test_bench_control_flow_world2_global_batch_split():
     """--global-batch (C4): one global batch split by shard_range — 5 clips on 2 ranks is
     3 + 2; scaling is strong and value counts the global batch once."""
