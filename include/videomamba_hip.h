@@ -371,7 +371,7 @@ int vm_linear_fwd(const void* x, long long ldx, const void* w, long long ldw,
  * 256 x 256 or 256 x 192 tiles; needs bias == NULL and n a multiple of 256 or 192).  Every
  * form computes each output element as the same chain of MFMAs (K in 64-wide steps, in
  * order), so their outputs are bit-identical and a row never depends on m — the form only
- * changes speed.  Form 0 takes the persistent kernel from 3 tiles per CU up (the mixer's
+ * changes speed.  Form 0 takes the persistent kernel from 1.5 tiles per CU up (the mixer's
  * projections above a few clips: in_proj / out_proj at 448 clips, mamba_simple.py:333-339,
  * :445-446).
  */

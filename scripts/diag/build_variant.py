@@ -64,11 +64,6 @@ VARIANTS = {
                  ("vm_gemm_tile.hip", "#undef VM_TG_CFG\n#undef VM_TG_K\n",
                   "#undef VM_TG_CFG\n#undef VM_TG_K\n}  // namespace vm\nextern \"C\" int vm_tile_stamps(unsigned long long* host) {\n"
                   "  return hipMemcpyFromSymbol(host, HIP_SYMBOL(vm::g_tg_stamps), sizeof(vm::g_tg_stamps)) == hipSuccess ? 0 : -1;\n}\nnamespace vm {\n")],
-    # persistent GEMM from 1.5 tiles per CU (C5's in_proj: 441 tiles) instead of 3
-    "tg_min15": [("vm_gemm.hip", "constexpr int kTileMinPerCU = 3;  // tiles per CU from which the persistent kernel runs",
-                  "constexpr int kTileMinPerCU = 3;  // tiles per CU from which the persistent kernel runs\nconstexpr bool kTileMinHalf = true;"),
-                 ("vm_gemm.hip", "gemm_tile_count(m, n, bn) >=\n                                      static_cast<long long>(kTileMinPerCU) * wgs",
-                  "2 * gemm_tile_count(m, n, bn) >=\n                                      static_cast<long long>(3) * wgs")],
     "tg_lgkm0": [("vm_gemm_tile.hip", "constexpr bool kTileLgkmLate = true;", "constexpr bool kTileLgkmLate = false;")],
     "tg_prio2": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 2;")],
     # dt_proj-in-scan kernel: each step's y epilogue in its own step's region (before r04)

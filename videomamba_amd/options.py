@@ -27,7 +27,7 @@ documented options object; tests and sweeps change them with :func:`override`.
                      whenever the single-pass scan runs (tests); "off": conv_proj writes dt.
     projection_gemm  "hip" (default): the mixer's bf16 in_proj / out_proj run on the HIP GEMM
                      (vm_linear_fwd: the LDS-DMA tile kernel for small row counts, the
-                     persistent 256-row kernel from 3 tiles per CU up; bit-identical forms)
+                     persistent 256-row kernel from 1.5 tiles per CU up; bit-identical forms)
                      at every batch, so every row is computed the same way whatever the
                      row count — chunked streaming == the one-pass forward bit for bit at any
                      batch; "library": the round-3 rule below (hipBLASLt above 8 clips).
