@@ -238,8 +238,9 @@ def b1_kernel_rooflines(device, reps=50):
     shape (L=3137, padded 3144 rows): each stage launched alone, HIP-event timed on the
     launch stream, against its algorithmic bytes (HBM-bound kernels) or flops (GEMMs).
     Stages: add+RMSNorm (x bf16 + residual fp32 in, residual fp32 + normed bf16 out),
-    in_proj GEMM, fused conv+x_proj+dt_proj (+ conv state out), the scan (scan_roofline at
-    B=1: the segmented chunk form), out_proj GEMM — each the kernel the mixer runs for a
+    in_proj GEMM, fused conv+x_proj (+ conv state out; + dt_proj only when the mixer keeps it
+    there), the scan (scan_roofline at B=1: the segmented chunk form, computing dt_proj per
+    segment when the mixer does), out_proj GEMM — each the kernel the mixer runs for a
     one-clip chunk (the projections on the row-invariant HIP GEMM, clips=1)."""
     from videomamba_amd import kernels as K
     from videomamba_amd.layers import round_up
@@ -285,14 +286,19 @@ def b1_kernel_rooflines(device, reps=50):
         hn.normal_()
         mfma("in_proj", _event_us(lambda: _linear(hn, mx.in_proj.weight, clips=1), reps),
              2 * Lp * C * 2 * Dm)
+        # the mixer's choice at this shape: dt_proj inside the segmented scan (no dt rows)
+        dtp = mx._dtp_ok(hn.view(1, Lp, C), L)
+        wd, dto = (None, None) if dtp else (wdt_pad, dt)
         hbm("conv_proj", _event_us(lambda: K.conv_proj_raw(
             xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs_in, (cs_in.stride(0), cs_in.stride(1)),
-            cs_out, (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, wdt_pad, R, u,
-            (Lp * Dm, Dm), xdbl, (Lp * E, E), dt, (Lp * Dm, Dm), Lp, 1, Dm, L, W, stream), reps),
-            2 * Lp * (3 * Dm + E) + 2 * (wx_pad.numel() + wdt_pad.numel()))
-        sc = scan_roofline(1, reps, device, "tm")
+            cs_out, (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, wd, R, u,
+            (Lp * Dm, Dm), xdbl, (Lp * E, E), dto, (Lp * Dm, Dm), Lp, 1, Dm, L, W, stream), reps),
+            2 * Lp * ((2 if dtp else 3) * Dm + E) + 2 * wx_pad.numel()
+            + (0 if dtp else 2 * wdt_pad.numel()))
+        sc = scan_roofline(1, reps, device, "tm", dtp=dtp)
         out["scan"] = {k: sc[k] for k in ("avg_us", "bound", "achieved", "peak", "unit", "frac")}
         out["scan"]["us"] = out["scan"].pop("avg_us")
+        out["scan"]["dt_proj_inside"] = bool(dtp)
         mfma("out_proj", _event_us(lambda: _linear(y, mx.out_proj.weight, clips=1), reps),
              2 * Lp * Dm * C)
     out["layer_us_sum"] = round(sum(v["us"] for v in out.values()), 2)

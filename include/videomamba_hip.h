@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 10
+#define VM_ABI_VERSION 11
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -147,11 +147,21 @@ int vm_selective_scan_bidir_fwd(
  *   dt_low: rows of the x_dbl buffer (batch stride dtl_sb, row stride dtl_sl elements;
  *           dt_low = the first dt_rank columns), 8-byte aligned rows;
  *   w_dt:   (dim, w_dt_ld) bf16 with columns >= dt_rank zero, w_dt_ld >= 16*ceil(r/16);
- * everything else as vm_selective_scan_fwd.  Single pass only (no segments, no
- * workspace): bf16, token-major, 16 states with C directly after B in the x_dbl row (the
- * mixer's layout), z present, delta_softplus = 1, dim % 128 == 0, dt_rank <= 64 and a
- * multiple of 4 (ABI v10: x_dbl columns >= dt_rank are never read as dt_low).  Each
- * token's dt is computed from its own row in a fixed order (sequence-length independent).
+ * everything else as vm_selective_scan_fwd.  bf16, token-major, 16 states with C directly
+ * after B in the x_dbl row (the mixer's layout), z present, delta_softplus = 1, dt_rank a
+ * multiple of 4 (ABI v10: x_dbl columns >= dt_rank are never read as dt_low).
+ *   Single pass (the cost model picks one segment: chip-filling batches): dim % 128 == 0,
+ *   dt_rank <= 64; each 16-step block's dt by v_mfma_f32_16x16x16_bf16 over
+ *   ceil(dt_rank / 16) k-steps.
+ *   Segmented (ABI v11; segments, workspace and sync as vm_selective_scan_fwd): segments of
+ *   at most 64 steps (vm_selective_scan_chunk_steps), w_dt_ld = 32 or 64 (the r_pad of
+ *   vm_conv_proj_fwd's W_dt); each wave computes its segment's dt exactly as
+ *   vm_conv_proj_fwd's dt_proj does (v_mfma_f32_16x16x32_bf16 over w_dt_ld / 32 k-steps,
+ *   x_dbl columns >= dt_rank as 0), so it equals the dt rows that call would write, bit for
+ *   bit — the streaming batches' replacement for conv_proj's dt rows
+ *   (mamba_simple.py:409-416).
+ * Each token's dt is computed from its own row in a fixed order (sequence-length
+ * independent).
  */
 int vm_selective_scan_dtproj_fwd(
     const void* u, long long u_sb, long long u_sd, long long u_sl,
@@ -164,7 +174,14 @@ int vm_selective_scan_dtproj_fwd(
     const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd,
     void* out, long long o_sb, long long o_sd, long long o_sl, int out_len,
-    int batch, int dim, int seqlen, int dstate, int dtype, vm_stream_t stream);
+    int batch, int dim, int seqlen, int dstate, int dtype,
+    int segments, void* workspace, long long workspace_bytes, void* sync,
+    long long sync_bytes, vm_stream_t stream);
+
+/* Steps per segment the token-major scan would run for this shape and segment request
+ * (0 = the single pass), ABI v11: vm_selective_scan_dtproj_fwd's segmented form takes
+ * segments of at most 64 steps. */
+int vm_selective_scan_chunk_steps(int batch, int dim, int seqlen, int dstate, int segments);
 
 /* Scratch bytes vm_selective_scan_fwd wants for token-major operands of this shape and
  * segment request (0 = the cost model's choice). */

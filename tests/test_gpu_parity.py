@@ -295,7 +295,9 @@ def _dtproj_case(Bz, D, L, R, seed, exact):
                 bias=bias.to(DEV), h0=h0, cpu=(u, dt_ref, z, Bm, Cm, A, Dv, bias))
 
 
-def _run_dtproj(c, Bz, D, L, R, dtp):
+def _run_dtproj(c, Bz, D, L, R, dtp, segments=1, one_launch=True):
+    """dtp: vm_selective_scan_dtproj_fwd; else the scan reading c["DT"] rows.  ``segments``
+    (options.scan_segments): 1 = the single pass, 0 = the cost model, > 1 forced."""
     N, E, Lp = c["N"], c["E"], c["Lp"]
     s_u, s_z, s_bc = (Lp * D, 1, D), (Lp * 2 * D, 1, 2 * D), (Lp * E, 1, E)
     XD, XZ = c["XD"], c["XZ"]
@@ -303,12 +305,12 @@ def _run_dtproj(c, Bz, D, L, R, dtp):
     h = c["h0"].to(DEV).contiguous()
     hs = (D * N, N)
     stream = torch.cuda.current_stream().cuda_stream
-    if dtp:
-        K.scan_dtproj_raw(c["U"], s_u, XD, (Lp * E, E), R, c["wpad"], c["A"], XD[:, R:R + N],
-                          s_bc, XD[:, R + N:], s_bc, c["Dv"], XZ[:, D:], s_z, c["bias"], h, hs,
-                          h, hs, y, s_u, Lp, Bz, D, L, N, stream)
-    else:
-        with options.override(scan_segments=1):
+    with options.override(scan_segments=segments, scan_one_launch=one_launch):
+        if dtp:
+            K.scan_dtproj_raw(c["U"], s_u, XD, (Lp * E, E), R, c["wpad"], c["A"],
+                              XD[:, R:R + N], s_bc, XD[:, R + N:], s_bc, c["Dv"], XZ[:, D:],
+                              s_z, c["bias"], h, hs, h, hs, y, s_u, Lp, Bz, D, L, N, stream)
+        else:
             K.scan_raw(c["U"], s_u, c["DT"], s_u, c["A"], XD[:, R:R + N], s_bc, XD[:, R + N:],
                        s_bc, c["Dv"], XZ[:, D:], s_z, c["bias"], True, h, hs, h, hs, y, s_u, Lp,
                        Bz, D, L, N, K.dtype_code(torch.bfloat16), stream)
@@ -348,6 +350,82 @@ def test_scan_dtproj_never_reads_b_columns_as_dt(R):
     assert torch.equal(y1.view(torch.int16), y0.view(torch.int16))
     assert torch.equal(h1.view(torch.int32), h0.view(torch.int32))
     assert torch.isfinite(h1[:, :, 1:]).all()  # only state 0 saw the infinite B
+
+
+@pytest.mark.parametrize("one_launch", [True, False])
+@pytest.mark.parametrize("Bz,D,L,R,segments", [(1, 1152, 3137, 36, 0), (2, 1152, 3137, 36, 0),
+                                                (1, 384, 1000, 12, 0), (3, 256, 777, 24, 40),
+                                                (1, 1152, 100, 36, 3), (2, 768, 1569, 36, 0)])
+def test_scan_dtproj_segmented_bitwise_equals_dt_rows_then_segmented_scan(Bz, D, L, R, segments,
+                                                                         one_launch):
+    """ABI v11: at streaming batches the dt_proj-in-scan entry runs the segmented form, each
+    segment (<= 64 steps) computing its dt on the matrix cores in conv_proj's arithmetic.  On
+    exact dt sums it is bit-identical to the same segmented scan reading precomputed dt rows
+    (y, h_last, zeroed padded rows), one-launch and two-launch, for the cost model's segment
+    counts at the M / Ti / S shapes of the B = 1 and 2 chunks and forced counts."""
+    assert 0 < K.scan_chunk_steps(Bz, D, L, 16, segments) <= K.SCAN_DTPROJ_MAX_SEGMENT
+    c = _dtproj_case(Bz, D, L, R, 300 + L + R, exact=True)
+    y1, h1 = _run_dtproj(c, Bz, D, L, R, True, segments, one_launch)
+    y0, h0 = _run_dtproj(c, Bz, D, L, R, False, segments, one_launch)
+    assert torch.equal(y1, y0)
+    assert torch.equal(h1, h0)
+    assert not y1[:, L:].float().abs().any()
+
+
+@pytest.mark.parametrize("R", [12, 36])
+def test_scan_dtproj_segmented_never_reads_b_columns_as_dt(R):
+    """The segmented form's dt operand zeroes the x_dbl columns >= dt_rank (the B values), as
+    conv_proj's zero-padded operand does: an infinite B at one step leaves every other
+    state's dt finite, bit-identical to the segmented scan reading precomputed dt rows."""
+    Bz, D, L = 1, 256, 300
+    c = _dtproj_case(Bz, D, L, R, 9 + R, exact=True)
+    N, Lp = c["N"], c["Lp"]
+    c["XD"].view(Bz, Lp, -1)[0, 50, R] = float("inf")
+    y1, h1 = _run_dtproj(c, Bz, D, L, R, True, 0)
+    y0, h0 = _run_dtproj(c, Bz, D, L, R, False, 0)
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16))
+    assert torch.equal(h1.view(torch.int32), h0.view(torch.int32))
+
+
+def test_scan_dtproj_rejects_segments_past_64_steps():
+    """The segmented dt_proj-in-scan form holds a segment's dt in LDS: a segment count that
+    gives more than 64 steps per segment is refused (VM_E_INVALID, nothing launched) and the
+    mixer keeps conv_proj's dt rows there (Mamba._dtp_ok)."""
+    Bz, D, L, R = 1, 256, 2000, 36
+    assert K.scan_chunk_steps(Bz, D, L, 16, 10) == 200
+    c = _dtproj_case(Bz, D, L, R, 11, exact=True)
+    with pytest.raises(RuntimeError, match="64 steps"):
+        _run_dtproj(c, Bz, D, L, R, True, 10)
+
+
+@pytest.mark.parametrize("bsz,d_model", [(1, 576), (2, 576), (4, 576), (1, 192), (3, 384)])
+def test_mixer_segmented_dtproj_bitwise_equals_conv_proj_dt_rows(bsz, d_model):
+    """The streaming-batch mixer with dt_proj inside the segmented scan (round 4 default)
+    against conv_proj writing the dt rows the scan reads (options.scan_dt_proj = "off"):
+    bit-identical outputs and states on real-valued weights and inputs — the dt arithmetic
+    is conv_proj's own, so moving it changes no result (and chunked == full keeps holding
+    whichever form a chunk length picks)."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(bsz + d_model)
+    m = Mamba(d_model=d_model, layer_idx=0).to(DEV, torch.bfloat16).eval()
+    L = 3137
+    x = torch.randn(bsz, L, d_model, device=DEV).to(torch.bfloat16)
+    hn = torch.empty(1, 1, d_model, device=DEV, dtype=torch.bfloat16).expand(bsz, 3144, d_model)
+    steps = K.scan_chunk_steps(bsz, m.d_inner, L, 16)
+    assert m._dtp_ok(hn, L) == (0 < steps <= K.SCAN_DTPROJ_MAX_SEGMENT)
+    with options.override(scan_dt_proj="off"):
+        assert not m._dtp_ok(hn, L)
+    outs = {}
+    st0 = m.allocate_state(bsz, dtype=torch.float32)
+    st0[1].normal_()
+    st0[0].normal_()
+    for mode in ("auto", "off"):
+        st = tuple(s.clone() for s in st0)  # the same entry states for both forms
+        with torch.no_grad(), options.override(scan_dt_proj=mode):
+            y, (cs, ss) = m(x, state=st, return_state=True)
+        outs[mode] = (y, cs, ss)
+    for a, b in zip(outs["auto"], outs["off"]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("Bz,D,L,R", [(2, 256, 301, 36), (1, 1152, 777, 36)])

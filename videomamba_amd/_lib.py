@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _P = c_void_p
 _LL = c_longlong
@@ -63,7 +63,9 @@ _SIGNATURES = {
          _P, _I, _LL, _LL,        # h_last
          _P, _LL, _LL, _LL, _I,   # out, out_len
          _I, _I, _I, _I, _I,      # batch, dim, seqlen, dstate, dtype
+         _I, _P, _LL, _P, _LL,    # segments, workspace, sync (ABI v11)
          _P], _I),
+    "vm_selective_scan_chunk_steps": ([_I, _I, _I, _I, _I], _I),
     "vm_selective_scan_workspace_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_scan_sync_bytes": ([_I, _I, _I, _I, _I], _LL),
     "vm_selective_scan_sync_status": ([_P, _LL], _I),

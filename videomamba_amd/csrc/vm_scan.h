@@ -82,5 +82,10 @@ struct DtpArgs {
 };
 bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_rank);
 void seq_dtp_launch(const ScanParams& p, const DtpArgs& q, int dt_rank, hipStream_t s);
+int seq_chunk_steps(int batch, int dim, int seqlen, int segments);
+bool seq_dtp_chunk_supported(const ScanParams& p, const DtpArgs& q, int dtype, int segments,
+                             size_t workspace_bytes);
+void seq_dtp_chunk_launch(const ScanParams& p, const DtpArgs& q, int segments, void* workspace,
+                          size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s);
 
 }  // namespace vm

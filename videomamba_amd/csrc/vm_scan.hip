@@ -604,7 +604,8 @@ extern "C" int vm_selective_scan_dtproj_fwd(
     int delta_softplus, const void* h0, int h0_dtype, long long h0_sb, long long h0_sd,
     void* h_last, int hl_dtype, long long hl_sb, long long hl_sd, void* out, long long o_sb,
     long long o_sd, long long o_sl, int out_len, int batch, int dim, int seqlen, int dstate,
-    int dtype, vm_stream_t stream) {
+    int dtype, int segments, void* workspace, long long workspace_bytes, void* sync,
+    long long sync_bytes, vm_stream_t stream) {
   const char* name = "vm_selective_scan_dtproj_fwd";
   if (!u || !dt_low || !w_dt || !A || !B || !C || !z || !out) {
     vmhost::set_error("%s: null required pointer", name);
@@ -630,6 +631,26 @@ extern "C" int vm_selective_scan_dtproj_fwd(
   DtpArgs q{};
   q.dtl = static_cast<const bf16_t*>(dt_low); q.dtl_sb = dtl_sb; q.dtl_sl = dtl_sl;
   q.wdt = static_cast<const bf16_t*>(w_dt); q.wdt_ld = w_dt_ld; q.dt_rank = dt_rank;
+  if (segments < 0 || workspace_bytes < 0 || sync_bytes < 0) {
+    vmhost::set_error("%s: negative segments / workspace / sync size", name);
+    return VM_E_INVALID;
+  }
+  // the segmented form when the cost model (or `segments`) asks for one: dt_proj inside the
+  // chunked scan, in conv_proj's arithmetic (ABI v11)
+  if (seq_chunk_steps(batch, dim, seqlen, segments) > 0) {
+    if (!seq_dtp_chunk_supported(p, q, dtype, segments, static_cast<size_t>(workspace_bytes)) ||
+        !workspace) {
+      vmhost::set_error("%s: the segmented form needs bf16 token-major operands with z, "
+                        "softplus, 16 states, C directly after B in the x_dbl rows, segments of "
+                        "at most 64 steps (vm_selective_scan_chunk_steps), a (dim, 32 | 64) W_dt "
+                        "with dt_rank <= its width and a multiple of 4, and the workspace of "
+                        "vm_selective_scan_workspace_bytes", name);
+      return VM_E_INVALID;
+    }
+    seq_dtp_chunk_launch(p, q, segments, workspace, static_cast<size_t>(workspace_bytes), sync,
+                         static_cast<size_t>(sync_bytes), static_cast<hipStream_t>(stream));
+    return vmhost::launch_status(name);
+  }
   if (!seq_dtp_supported(p, q, dtype, dt_rank)) {
     vmhost::set_error("%s: needs bf16 token-major operands with z, softplus, 16 states, C "
                       "directly after B in the x_dbl rows, dim %% 128 == 0, dt_rank <= 64 and a multiple of 4, "
@@ -638,6 +659,13 @@ extern "C" int vm_selective_scan_dtproj_fwd(
   }
   seq_dtp_launch(p, q, dt_rank, static_cast<hipStream_t>(stream));
   return vmhost::launch_status(name);
+}
+
+extern "C" int vm_selective_scan_chunk_steps(int batch, int dim, int seqlen, int dstate,
+                                             int segments) {
+  if (batch <= 0 || dim <= 0 || seqlen < 0 || dstate < 1 || dstate > kMaxN || segments < 0)
+    return 0;
+  return seq_chunk_steps(batch, dim, seqlen, segments);
 }
 
 extern "C" long long vm_selective_scan_workspace_bytes(int batch, int dim, int seqlen,

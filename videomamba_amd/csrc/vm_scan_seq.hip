@@ -838,11 +838,23 @@ template <bool V> struct BoolTag { static constexpr bool value = V; };
 // one 4 * K-byte access
 template <int K> struct alignas(4 * K) AggShare { float v[K] = {}; };
 
-template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>
-__global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w) {
+// dt_proj inside the chunked scan (DTP, ABI v11): each wave computes its own segment's dt
+// (at most kChDtpT steps) on the matrix cores into an LDS block before its step loops, with
+// exactly the fused conv_proj's dt_proj arithmetic (vm_conv_proj_sk.hip: A = the x_dbl rows'
+// first R columns zero-padded to r_pad, B = W_dt rows, v_mfma_f32_16x16x32_bf16 over
+// r_pad / 32 k-steps in order, bf16 by round-to-nearest-even), so dt is bit-identical to the
+// rows conv_proj would have written: conv_proj skips them and the scan reads x_dbl instead.
+constexpr int kChDtpT = 64;              // max segment length with dt_proj inside
+constexpr int kChDtpPitch = kChDtpT + 8;  // bf16 per channel row of a wave's dt block
+constexpr int kChDtpWPitch = 64 + 8;      // bf16 per W_dt row in LDS (r_pad <= 64)
+
+template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>
+__global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w,
+                                                               const DtpArgs q) {
   typedef __attribute__((address_space(4))) const uint32_t* cptr;
   constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
   constexpr int ES = sizeof(T);
+  static_assert(!DTP || sizeof(T) == 2, "dt_proj inside the scan is bf16 only");
   // sH: PASS 1 segment end states; PASS 2 the staged block aggregates, then H_blk in sH[0].
   // sA: A of the workgroup's 64 channels, transposed to [state][channel].
   __shared__ float sH[kChW][kMaxN][64];
@@ -850,6 +862,9 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   __shared__ float sA[kMaxN][64];
   __shared__ float sHb[PASS == 3 ? kMaxN : 1][64];  // one-launch form: the block entry state
   __shared__ unsigned s_tag;  // one-launch form: this launch's hand-off tag
+  // DTP: the group's W_dt rows [channel][r_pad] and each wave's dt block [channel][step]
+  __shared__ __attribute__((aligned(16))) bf16_t sWd[DTP ? 64 * kChDtpWPitch : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t sDT[DTP ? kChW * 64 * kChDtpPitch : 8];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1003,9 +1018,23 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     for (int j = 0; j < kPF; ++j) {
       const int t = min(t_beg + j, tlast);
       ru[j] = bload<T>(ur, voff, t * us);
-      rd[j] = bload<T>(dr_, voff, t * ds);
+      rd[j] = DTP ? 0u : bload<T>(dr_, voff, t * ds);
       rz[j] = HZ && PASS == 2 ? bload<T>(zr, voff, t * zs) : 0u;
       __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // DTP: the group's W_dt rows into LDS (16-byte pieces; rows past dim read 0)
+  if constexpr (DTP) {
+    const int rp = q.wdt_ld;  // r_pad: 32 or 64
+    const int ppr = rp >> 3;  // pieces per row
+    const auto wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(q.wdt + static_cast<long long>(d0) * rp), 0, nch * rp * 2, 0x00020000);
+    for (int i = tid; i < 64 * ppr; i += 64 * kChW) {
+      const int row = i / ppr, pc = i - row * ppr;
+      typedef __attribute__((ext_vector_type(4))) unsigned wv4;
+      const wv4 v = __builtin_bit_cast(
+          wv4, __builtin_amdgcn_raw_buffer_load_b128(wr, (row * rp + pc * 8) * 2, 0, 0));
+      *reinterpret_cast<wv4*>(&sWd[row * kChDtpWPitch + pc * 8]) = v;
     }
   }
   // one wait for every start-up load (parameters, entry operands, prologue): left pending
@@ -1043,6 +1072,58 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     sS[tid >> 6][lane] = agS[0];
   }
   __syncthreads();
+  // DTP: this wave's dt for steps t_beg .. t_end - 1 (blocks of 16) -> sDT[wave][ch][step]
+  bf16_t* myDT = &sDT[DTP ? wave * 64 * kChDtpPitch : 0];
+  auto dt_lds = [&](int t) -> uint32_t {  // the raw bf16 of step t (clamped into the block)
+    const int i = min(max(t - t_beg, 0), kChDtpPitch - 1);
+    return static_cast<uint32_t>(*reinterpret_cast<const unsigned short*>(&myDT[lane * kChDtpPitch + i]));
+  };
+  if constexpr (DTP) {
+    typedef __attribute__((ext_vector_type(8))) __bf16 dbf16x8;
+    typedef __attribute__((ext_vector_type(4))) float df32x4;
+    typedef __attribute__((ext_vector_type(2))) unsigned du2;
+    const int rp = q.wdt_ld;
+    const int R = q.dt_rank;
+    const auto dtr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(q.dtl + static_cast<long long>(b) * q.dtl_sb), 0,
+        static_cast<int>(static_cast<long long>(p.out_len) * q.dtl_sl * 2), 0x00020000);
+    constexpr int kOut = 0x7ffffff0;
+    for (int t0 = t_beg; t0 < t_end; t0 += 16) {
+      dbf16x8 af[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        // A = x_dbl row t0 + lane % 16, k = 32 ks + 8 (lane / 16) .. + 7; k >= R reads 0
+        const int k0 = 32 * ks + 8 * (lane >> 4);
+        const int off = ((t0 + (lane & 15)) * static_cast<int>(q.dtl_sl) + k0) * 2;
+        const du2 lo = __builtin_bit_cast(du2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   dtr, k0 + 4 <= R && 32 * ks < rp ? off : kOut, 0, 0));
+        const du2 hi = __builtin_bit_cast(du2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   dtr, k0 + 8 <= R && 32 * ks < rp ? off + 8 : kOut, 0, 0));
+        af[ks] = __builtin_bit_cast(dbf16x8, (__attribute__((ext_vector_type(4))) unsigned){lo.x, lo.y, hi.x, hi.y});
+      }
+#pragma unroll
+      for (int tile = 0; tile < 4; ++tile) {
+        df32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (32 * ks < rp) {
+            const dbf16x8 bw = *reinterpret_cast<const dbf16x8*>(
+                &sWd[(16 * tile + (lane & 15)) * kChDtpWPitch + 32 * ks + 8 * (lane >> 4)]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bw, acc, 0, 0, 0);
+          }
+        }
+        // D[step 4 (lane/16) + i][channel 16 tile + lane % 16] -> [channel][step]
+        const uint32_t p01 = cvt_pk_bf16(acc[0], acc[1]), p23 = cvt_pk_bf16(acc[2], acc[3]);
+        *reinterpret_cast<uint2*>(&myDT[(16 * tile + (lane & 15)) * kChDtpPitch + (t0 - t_beg) +
+                                        4 * (lane >> 4)]) = uint2{p01, p23};
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the block is written
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) rd[j] = dt_lds(min(t_beg + j, tlast));
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
   f2 A2[kMaxN / 2], h[kMaxN / 2];
 #pragma unroll
   for (int q = 0; q < kMaxN / 2; ++q) {
@@ -1127,10 +1208,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         const float zz = raw_f32<T>(rz[j]);
         const int tn = min(t + kPF, tlast);
         ru[j] = bload<T>(ur, voff, tn * us);
-        rd[j] = bload<T>(dr_, voff, tn * ds);
+        if constexpr (!DTP) rd[j] = bload<T>(dr_, voff, tn * ds);
         if (HZ && EMIT) rz[j] = bload<T>(zr, voff, tn * zs);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
         bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+        // DTP: the LDS read goes after that wait, so the next step's wait is its first
+        if constexpr (DTP) rd[j] = dt_lds(tn);
         __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
         float dl = dl_nx;
         dl_nx = delta_of(rd[(j + 1) & (kPF - 1)]);
@@ -1277,7 +1360,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       for (int j = 0; j < kPF; ++j) {
         const int t = min(t_beg + j, tlast);
         ru[j] = bload<T>(ur, voff, t * us);
-        rd[j] = bload<T>(dr_, voff, t * ds);
+        rd[j] = DTP ? dt_lds(t) : bload<T>(dr_, voff, t * ds);
         rz[j] = HZ ? bload<T>(zr, voff, t * zs) : 0u;
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1558,18 +1641,19 @@ bool seq_supported(const ScanParams& p, int dtype) {
          (p.z == nullptr || fits(p.z_sl));
 }
 
-template <typename T, bool SP, bool HZ, bool BC1, bool PAIR>
-static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t s) {
+template <typename T, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>
+static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t s,
+                           const DtpArgs& q = DtpArgs{}) {
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
   if (w.gran) {  // one launch: blocks hand their aggregates on through the sync buffer
-    hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
-                       p, w);
+    hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR, DTP>), grid, dim3(64 * kChW),
+                       0, s, p, w, q);
     return;
   }
-  hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
-                     p, w);
-  hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1, PAIR>), grid, dim3(64 * kChW), 0, s,
-                     p, w);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 1, SP, HZ, BC1, PAIR, DTP>), grid, dim3(64 * kChW), 0,
+                     s, p, w, q);
+  hipLaunchKernelGGL((scan_chunk_kernel<T, 2, SP, HZ, BC1, PAIR, DTP>), grid, dim3(64 * kChW), 0,
+                     s, p, w, q);
 }
 
 template <typename T, bool SP, bool HZ, bool BC1>
@@ -1674,6 +1758,60 @@ bool seq_dtp_supported(const ScanParams& p, const DtpArgs& q, int dtype, int dt_
          (reinterpret_cast<uintptr_t>(q.dtl) & 7) == 0 && q.dtl_sl % 4 == 0 &&
          q.dtl_sb % 4 == 0 && q.dtl_sl >= dt_rank && dl_span < (1ll << 31) &&
          static_cast<long long>(p.seqlen) * q.dtl_sl * 2 < (1ll << 31);
+}
+
+// Segment length the chunked form would run (0 = the single pass), for the host's choice of
+// dt_proj placement (inside the chunked scan up to kChDtpT steps).
+int seq_chunk_steps(int batch, int dim, int seqlen, int segments) {
+  const int S = segments_for(batch, dim, seqlen, segments, cus_or_calib(device_cus(nullptr)));
+  if (S <= 1) return 0;
+  int T, nblk;
+  chunk_geometry(seqlen, S, &T, &nblk);
+  return T;
+}
+
+// dt_proj inside the chunked scan (DTP): the mixer's bf16 token-major operands with the
+// conv_proj-form W_dt (r_pad = 32 or 64 columns) and segments of at most kChDtpT steps.
+bool seq_dtp_chunk_supported(const ScanParams& p, const DtpArgs& q, int dtype, int segments,
+                             size_t workspace_bytes) {
+  const bool bc1 = p.c_sl == p.b_sl && p.c_sb == p.b_sb &&
+                   static_cast<const bf16_t*>(p.C) == static_cast<const bf16_t*>(p.B) + kMaxN;
+  int S = 1;
+  const size_t need = seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S);
+  if (S <= 1) return false;
+  int T, nblk;
+  chunk_geometry(p.seqlen, S, &T, &nblk);
+  return dtype == VM_DTYPE_BF16 && seq_supported(p, dtype) && seq_sgpr_bc(p, 2) && bc1 &&
+         p.z && p.softplus && p.split == p.batch && T <= kChDtpT && workspace_bytes >= need &&
+         q.dtl && q.wdt && (q.wdt_ld == 32 || q.wdt_ld == 64) && q.dt_rank >= 1 &&
+         q.dt_rank <= q.wdt_ld && q.dt_rank % 4 == 0 && q.dtl_sl >= q.dt_rank &&
+         (reinterpret_cast<uintptr_t>(q.dtl) & 7) == 0 && q.dtl_sl % 4 == 0 && q.dtl_sb % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(q.wdt) & 15) == 0 &&
+         static_cast<long long>(p.out_len) * q.dtl_sl * 2 < (1ll << 31);
+}
+
+void seq_dtp_chunk_launch(const ScanParams& p, const DtpArgs& q, int segments, void* workspace,
+                          size_t workspace_bytes, void* sync, size_t sync_bytes, hipStream_t s) {
+  const int dev_cus = device_cus(s);
+  const int cus = cus_or_calib(dev_cus);
+  int S = 1;
+  seq_workspace_bytes(p.batch, p.dim, p.seqlen, segments, &S, cus);
+  ChunkWork w{};
+  chunk_geometry(p.seqlen, S, &w.T, &w.nblk);
+  const long long grid = static_cast<long long>((p.dim + 63) / 64) * w.nblk * p.batch;
+  if (sync && sync_bytes >= seq_sync_bytes(p.batch, p.dim, p.seqlen, segments, cus) &&
+      grid <= dev_cus) {
+    w.err = static_cast<unsigned*>(sync);
+    w.epoch = w.err + 1;
+    w.done = w.err + 2;
+    w.gran = reinterpret_cast<unsigned long long*>(w.err + kSyncHeaderWords);
+  }
+  const size_t nb = static_cast<size_t>(p.batch) * w.nblk;
+  w.segE = static_cast<float*>(workspace);
+  w.segP = w.segE + nb * kChW * p.dim * kMaxN;
+  w.aggH = w.segP + nb * kChW * p.dim;
+  w.aggS = w.aggH + nb * p.dim * kMaxN;
+  launch_chunk_p<bf16_t, true, true, true, false, true>(p, w, s, q);
 }
 
 void seq_dtp_launch(const ScanParams& p, const DtpArgs& q, int dt_rank, hipStream_t s) {

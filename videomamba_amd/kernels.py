@@ -280,15 +280,43 @@ def scan_raw(u, u_s, delta, dl_s, A32, B, b_s, C, c_s, D32, z, z_s, bias32, soft
     _lib.check(rc, "vm_selective_scan_bidir_fwd")
 
 
+def scan_chunk_steps(batch: int, dim: int, seqlen: int, dstate: int, segments: int = -1) -> int:
+    """Steps per segment the token-major scan runs for this shape (0: the single pass);
+    ``segments`` -1 = ``options.scan_segments`` (``vm_selective_scan_chunk_steps``)."""
+    seg = int(options.get().scan_segments) if segments < 0 else segments
+    return int(_lib.load().vm_selective_scan_chunk_steps(batch, dim, seqlen, dstate, seg))
+
+
+SCAN_DTPROJ_MAX_SEGMENT = 64  # the segmented dt_proj-in-scan form (ABI v11)
+
+
 def scan_dtproj_raw(u, u_s, dtl, dtl_s, dt_rank, wdt_pad, A32, B, b_s, C, c_s, D32, z, z_s,
                     bias32, h0, h0_s, h_last, hl_s, out, o_s, out_len, batch, dim, seqlen,
-                    dstate, stream):
-    """``vm_selective_scan_dtproj_fwd``: the single-pass token-major scan with dt_proj
-    folded in — delta = bf16(dt_low @ W_dt^T) per 16-step block on the matrix cores, then
-    softplus(delta + bias) as selective_scan_fn.  ``dtl`` = the x_dbl rows (dt_low = their
-    first ``dt_rank`` columns), ``dtl_s`` = (batch, row) element strides; ``wdt_pad`` = the
-    zero-padded (D, 32|64) bf16 W_dt.  bf16 only, z and softplus on."""
-    rc = _lib.load().vm_selective_scan_dtproj_fwd(
+                    dstate, stream, workspace: Optional[Tensor] = None):
+    """``vm_selective_scan_dtproj_fwd``: the token-major scan with dt_proj folded in —
+    delta = bf16(dt_low @ W_dt^T) on the matrix cores, then softplus(delta + bias) as
+    selective_scan_fn.  ``dtl`` = the x_dbl rows (dt_low = their first ``dt_rank`` columns),
+    ``dtl_s`` = (batch, row) element strides; ``wdt_pad`` = the zero-padded (D, 32|64) bf16
+    W_dt.  bf16 only, z and softplus on.  Single pass at chip-filling batches; below that
+    the segmented form (segments of at most 64 steps) computes each segment's dt exactly as
+    conv_proj's dt_proj would (ABI v11), with the scratch / sync buffers of ``scan_raw``."""
+    lib = _lib.load()
+    seg = int(options.get().scan_segments)
+    ws_bytes = scan_workspace_bytes(batch, dim, seqlen, dstate, seg)
+    ws, sync, sync_bytes = None, None, 0
+    if ws_bytes:
+        if workspace is not None:
+            if workspace.numel() < ws_bytes:
+                raise ValueError(f"scan workspace too small: {workspace.numel()} < {ws_bytes}")
+            ws = workspace
+        else:
+            ws = scratch(u.device, int(stream), ws_bytes)
+        if options.get().scan_one_launch:
+            sync_bytes = scan_sync_bytes(batch, dim, seqlen, dstate, seg)
+            sync = sync_buffer(u.device, int(stream), sync_bytes)
+            if sync is None:
+                sync_bytes = 0
+    rc = lib.vm_selective_scan_dtproj_fwd(
         _p(u), u_s[0], u_s[1], u_s[2], _p(dtl), dtl_s[0], dtl_s[1], int(dt_rank),
         _p(wdt_pad), wdt_pad.stride(0), _p(A32),
         _p(B), b_s[0], b_s[1], b_s[2], _p(C), c_s[0], c_s[1], c_s[2],
@@ -296,7 +324,7 @@ def scan_dtproj_raw(u, u_s, dtl, dtl_s, dt_rank, wdt_pad, A32, B, b_s, C, c_s, D
         _p(h0), dtype_code(h0.dtype) if h0 is not None else 0, h0_s[0], h0_s[1],
         _p(h_last), dtype_code(h_last.dtype) if h_last is not None else 0, hl_s[0], hl_s[1],
         _p(out), o_s[0], o_s[1], o_s[2], out_len, batch, dim, seqlen, dstate,
-        dtype_code(u.dtype), stream)
+        dtype_code(u.dtype), seg, _p(ws), ws_bytes, _p(sync), sync_bytes, stream)
     _lib.check(rc, "vm_selective_scan_dtproj_fwd")
 
 

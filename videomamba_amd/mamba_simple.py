@@ -297,17 +297,29 @@ class Mamba(nn.Module):
         return out.view(Bsz, Lp, C)
 
     def _dtp_ok(self, hn: Tensor, seqlen: int, conv_state_in: Optional[Tensor] = None) -> bool:
-        """Fold dt_proj into the scan (vm_selective_scan_dtproj_fwd): bf16 fused conv_proj
-        path, 16 states, D % 128 == 0, and a single-pass scan at this batch (the segmented
-        small-batch forms read a dt row); "auto" only above the split-K batch (> 8), where
-        conv_proj's wide kernel would otherwise write dt rows the scan reads straight back."""
+        """Fold dt_proj into the scan (vm_selective_scan_dtproj_fwd, conv_proj then writes no
+        dt rows): bf16 fused conv_proj path, 16 states, dt_rank a multiple of 4, and
+          * a segmented scan (streaming batches) of at most 64 steps per segment: each segment
+            computes its dt exactly as conv_proj's dt_proj would (ABI v11), so the bits are the
+            ones conv_proj writes otherwise — the choice never changes a result, and chunked
+            == full stays exact whichever form a chunk length selects; or
+          * the single-pass scan (D % 128 == 0) above the split-K batch (> 8 clips; "on":
+            at any batch), whose 16-step MFMA dt blocks are its own arithmetic — below 9
+            clips a short sequence's single pass keeps conv_proj's dt for the same
+            invariance."""
         mode = options.get().scan_dt_proj
         Bsz = hn.shape[0]
-        if mode == "off" or (mode == "auto" and Bsz <= 8):
+        if mode == "off":
             return False
-        return (self._fused_conv_proj_ok(hn, seqlen, conv_state_in) and self.d_state == 16
-                and self.d_inner % 128 == 0 and self.dt_rank <= 64 and self.dt_rank % 4 == 0
-                and K.scan_workspace_bytes(Bsz, self.d_inner, seqlen, self.d_state) == 0)
+        if not (self._fused_conv_proj_ok(hn, seqlen, conv_state_in) and self.d_state == 16
+                and self.dt_rank <= 64 and self.dt_rank % 4 == 0):
+            return False
+        steps = K.scan_chunk_steps(Bsz, self.d_inner, seqlen, self.d_state)
+        if steps > 0:
+            return steps <= K.SCAN_DTPROJ_MAX_SEGMENT
+        if mode == "auto" and Bsz <= 8:
+            return False
+        return self.d_inner % 128 == 0
 
     def _tm_front(self, hn, seqlen, conv_state_in, conv_state_out, bufs=None, want_dt=True):
         """in_proj -> conv + silu -> x_proj -> dt_proj of the token-major form: (xz, u,
