@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 11
+#define VM_ABI_VERSION 12
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -423,11 +423,16 @@ int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* w, long lon
  * weight: (embed, cin*kt*P*P) contiguous, dtype `dtype`; bias: (embed) fp32.
  * spos: (Gh*Gw, embed), tpos: (frames/kt, embed), dtype `dtype`, contiguous.
  * out: token rows of `embed` elements; token j of batch b at out + b*out_sb + (row0+j)*embed.
+ * ABI v12: cls / cls_pos (embed elements of `dtype`, both or neither) also write the rows
+ * [0, row0) of every batch as e(cls + cls_pos) — the reference's CLS token plus its
+ * positional embedding (videomamba.py:806-815) — and pad_rows zero rows follow the last
+ * token (the padded buffer's tail), inside the same launch.
  */
 int vm_patch_embed_fwd(const void* video, const void* weight, const float* bias,
                        const void* spos, const void* tpos, void* out, long long out_sb,
                        int row0, int batch, int cin, int frames, int height, int width,
                        int kt, int patch_h, int patch_w, int embed, int dtype,
+                       const void* cls, const void* cls_pos, int pad_rows,
                        vm_stream_t stream);
 
 #ifdef __cplusplus

@@ -1,7 +1,8 @@
 """Chunked token-major scan time vs forced segment count (M-16f mixer geometry, bf16,
 stateful, delta softplus, z gate), HIP events over back-to-back launches.  Used to fit the
 segment cost model in vm_scan_seq.hip::choose_segments.
-    python scripts/diag/scan_segments_sweep.py  (env CASES="B:L,..." SEGS="0 50 100 ...")"""
+    python scripts/diag/scan_segments_sweep.py  (env CASES="B:L,..." SEGS="0 50 100 ...")
+DTP=1: the dt_proj-inside form (vm_selective_scan_dtproj_fwd, segments of <= 64 steps)."""
 import json
 import os
 import sys
@@ -19,6 +20,8 @@ m = Mamba(d_model=576, d_state=16, d_conv=4, expand=2, layer_idx=0).to(dev, torc
 Dm, E, R, N = m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_state
 A, Dv, dbias, _, _ = m._fp32_params()
 st = torch.cuda.current_stream().cuda_stream
+DTP = os.environ.get("DTP", "0") == "1"
+wdt_pad = m._padded_proj_weights()[1] if DTP else None
 
 
 def timeit(fn, reps=30):
@@ -47,11 +50,20 @@ for B, L in cases:
     y = torch.empty_like(u)
     h = torch.zeros(B, Dm, N, device=dev)
     s_u, s_xz, s_bc = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm), (Lp * E, 1, E)
-    row = {"B": B, "L": L}
+    row = {"B": B, "L": L, "dtp": DTP}
     for S in segs:
         if S > (L + 7) // 8:
             continue
+        if DTP and not 0 < K.scan_chunk_steps(B, Dm, L, N, S) <= K.SCAN_DTPROJ_MAX_SEGMENT:
+            continue
         with options.override(scan_segments=S):
+            if DTP:
+                fn = lambda: K.scan_dtproj_raw(  # noqa: E731
+                    u, s_u, xd, (Lp * E, E), R, wdt_pad, A, xd[:, R:R + N], s_bc, xd[:, R + N:],
+                    s_bc, Dv, xz[:, Dm:], s_xz, dbias, h, (Dm * N, N), h, (Dm * N, N), y, s_u,
+                    Lp, B, Dm, L, N, st)
+                row[f"S{S}"] = round(timeit(fn), 2)
+                continue
             fn = lambda: K.scan_raw(u, s_u, dt, s_u, A, xd[:, R:R + N], s_bc, xd[:, R + N:],  # noqa: E731
                                     s_bc, Dv, xz[:, Dm:], s_xz, dbias, True, h, (Dm * N, N), h,
                                     (Dm * N, N), y, s_u, Lp, B, Dm, L, N, 1, st)

@@ -748,7 +748,8 @@ def test_c3_m_16f_chunked_equals_full_at_chip_filling_batch(bsz):
     g = torch.Generator(device=DEV).manual_seed(40 + bsz)
     x = torch.randn(bsz, 3, 16, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
     hn = torch.empty(1, 1, 576, device=DEV, dtype=torch.bfloat16).expand(bsz, 1576, 576)
-    assert mx._dtp_ok(hn, 1569) == (bsz == 72 or 0 < K.scan_chunk_steps(bsz, 1152, 1569, 16) <= 64)
+    assert mx._dtp_ok(hn, 1569) == (bsz == 72 or
+                                    K.scan_dtproj_segmented_pays(bsz, 1152, 1569, 16, DEV))
     assert _small_gemm_ok(torch.empty(bsz * 1576, 576, device=DEV, dtype=torch.bfloat16),
                           mx.in_proj.weight, None, clips=bsz)
     with torch.no_grad():
@@ -904,8 +905,8 @@ def test_m_mixer_token_major_bench_kernels_match_oracle(segments, dtp):
     with options.override(mixer_layout="tm", scan_segments=segments, scan_dt_proj=dtp), \
             torch.no_grad():
         steps = K.scan_chunk_steps(2, 1152, 1000, 16)
-        assert m._dtp_ok(xd, 1000) == (dtp == "on" if steps == 0 else
-                                       dtp != "off" and steps <= K.SCAN_DTPROJ_MAX_SEGMENT)
+        assert m._dtp_ok(xd, 1000) == (dtp == "on" if steps == 0 else dtp != "off" and
+                                       K.scan_dtproj_segmented_pays(2, 1152, 1000, 16, DEV))
         full = m(xd)
         st = m.allocate_state(2, dtype=torch.float32)
         o1, st = m(xd[:, :601], state=st, return_state=True)

@@ -400,8 +400,9 @@ def test_scan_dtproj_rejects_segments_past_64_steps():
 
 @pytest.mark.parametrize("bsz,d_model", [(1, 576), (2, 576), (4, 576), (1, 192), (3, 384)])
 def test_mixer_segmented_dtproj_bitwise_equals_conv_proj_dt_rows(bsz, d_model):
-    """The streaming-batch mixer with dt_proj inside the segmented scan (round 4 default)
-    against conv_proj writing the dt rows the scan reads (options.scan_dt_proj = "off"):
+    """The streaming-batch mixer with dt_proj inside the segmented scan (round 4; the
+    default where its grid fits the chip, forced here by "on") against conv_proj writing
+    the dt rows the scan reads (options.scan_dt_proj = "off"):
     bit-identical outputs and states on real-valued weights and inputs — the dt arithmetic
     is conv_proj's own, so moving it changes no result (and chunked == full keeps holding
     whichever form a chunk length picks)."""
@@ -411,20 +412,22 @@ def test_mixer_segmented_dtproj_bitwise_equals_conv_proj_dt_rows(bsz, d_model):
     L = 3137
     x = torch.randn(bsz, L, d_model, device=DEV).to(torch.bfloat16)
     hn = torch.empty(1, 1, d_model, device=DEV, dtype=torch.bfloat16).expand(bsz, 3144, d_model)
-    steps = K.scan_chunk_steps(bsz, m.d_inner, L, 16)
-    assert m._dtp_ok(hn, L) == (0 < steps <= K.SCAN_DTPROJ_MAX_SEGMENT)
+    pays = K.scan_dtproj_segmented_pays(bsz, m.d_inner, L, 16, DEV)
+    assert m._dtp_ok(hn, L) == pays
     with options.override(scan_dt_proj="off"):
         assert not m._dtp_ok(hn, L)
+    with options.override(scan_dt_proj="on"):  # any grid
+        assert m._dtp_ok(hn, L) == (0 < K.scan_chunk_steps(bsz, m.d_inner, L, 16) <= 64)
     outs = {}
     st0 = m.allocate_state(bsz, dtype=torch.float32)
     st0[1].normal_()
     st0[0].normal_()
-    for mode in ("auto", "off"):
+    for mode in ("on", "off"):
         st = tuple(s.clone() for s in st0)  # the same entry states for both forms
         with torch.no_grad(), options.override(scan_dt_proj=mode):
             y, (cs, ss) = m(x, state=st, return_state=True)
         outs[mode] = (y, cs, ss)
-    for a, b in zip(outs["auto"], outs["off"]):
+    for a, b in zip(outs["on"], outs["off"]):
         assert torch.equal(a, b)
 
 
@@ -680,10 +683,17 @@ def test_patch_embed_matches_oracle(dt, Bz, T, H, W, P, kt, C):
     spos = (0.02 * torch.randn(hw, C, generator=g)).to(dt)
     tpos = (0.02 * torch.randn(T // kt, C, generator=g)).to(dt)
     ref = _patch_oracle(video, w, b, spos, tpos, kt, dt)
-    out = torch.empty(Bz, ref.shape[1] + 3, C, dtype=dt, device=DEV)
+    cls = torch.randn(C, generator=g).to(dt)
+    cls_pos = (0.02 * torch.randn(C, generator=g)).to(dt)
+    out = torch.full((Bz, ref.shape[1] + 3, C), 7.0, dtype=dt, device=DEV)
+    # ABI v12: the head rows (CLS + its positional embedding, added in the model dtype as
+    # the reference's cls_token + pos_embed[:, :1]) and the padding row in the same launch
     K.patch_embed(video.to(DEV), w.to(DEV), b.to(DEV), spos.to(DEV), tpos.to(DEV), out, 2,
-                  out.stride(0))
+                  out.stride(0), cls=cls.to(DEV), cls_pos=cls_pos.to(DEV), pad_rows=1)
     _close(out[:, 2:2 + ref.shape[1]], ref, 1e-5 if dt == torch.float32 else 2e-2)
+    head = (cls + cls_pos).to(DEV)  # torch's own add in dt
+    assert torch.equal(out[:, :2], head.expand(Bz, 2, C))
+    assert not out[:, -1].float().abs().any()
 
 
 @pytest.mark.parametrize("T,kt,C", [(32, 1, 576), (16, 2, 192), (32, 1, 192)])
@@ -701,11 +711,18 @@ def test_patch_embed_kernels_agree_bitwise(T, kt, C):
     spos = (0.02 * torch.randn(196, C, generator=g)).to(bf).to(DEV)
     tpos = (0.02 * torch.randn(T // kt, C, generator=g)).to(bf).to(DEV)
     n = (T // kt) * 196
-    big = torch.zeros(Bz, n + 1, C, dtype=bf, device=DEV)
-    K.patch_embed(video, w, b, spos, tpos, big, 1, big.stride(0))
-    one = torch.zeros(1, n + 1, C, dtype=bf, device=DEV)
-    K.patch_embed(video[Bz - 1:].contiguous(), w, b, spos, tpos, one, 1, one.stride(0))
+    cls = torch.randn(C, generator=g).to(bf).to(DEV)
+    cls_pos = (0.02 * torch.randn(C, generator=g)).to(bf).to(DEV)
+    big = torch.full((Bz, n + 8, C), 7.0, dtype=bf, device=DEV)
+    K.patch_embed(video, w, b, spos, tpos, big, 1, big.stride(0), cls=cls, cls_pos=cls_pos,
+                  pad_rows=7)
+    one = torch.full((1, n + 8, C), 7.0, dtype=bf, device=DEV)
+    K.patch_embed(video[Bz - 1:].contiguous(), w, b, spos, tpos, one, 1, one.stride(0),
+                  cls=cls, cls_pos=cls_pos, pad_rows=7)
     assert torch.equal(big[Bz - 1:], one)
+    assert torch.equal(big[:, 0], (cls + cls_pos).expand(Bz, C))
+    assert not big[:, n + 1:].float().abs().any()
+    one = one[:, :n + 1]
     ref = _patch_oracle(video[Bz - 1:].cpu(), w.cpu(), b.cpu(), spos.cpu(), tpos.cpu(), kt, bf)
     _close(one[:, 1:], ref, 2e-2)
 

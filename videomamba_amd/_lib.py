@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _P = c_void_p
 _LL = c_longlong
@@ -119,7 +119,8 @@ _SIGNATURES = {
          _I, _I, _I, _P, _LL, _P], _I),           # m, n, k, counters, bytes, stream
     "vm_linear_add_norm_counter_bytes": ([_I], _LL),
     "vm_patch_embed_fwd": (
-        [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P], _I),
+        [_P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
+         _P, _P, _I, _P], _I),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -25,10 +25,39 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 struct PatchParams {
   const void* video; const void* w; const float* bias; const void* spos; const void* tpos;
   void* out;
+  const void* cls; const void* cls_pos;  // head rows [0, row0) = e(cls + cls_pos) (nullable)
   long long out_sb;
   int row0, batch, cin, frames, height, width, kt, ph, pw, embed;
+  int pad_rows;  // zero rows after the tokens (the padded buffer's tail)
   int tt, gh, gw, K, M;  // derived: temporal tokens, grid, reduction length, tokens
 };
+
+// The rows of the padded token buffer around the patch tokens, written by the launch's
+// blockIdx.y == 0 workgroups before their tiles (grid-stride over batch x rows x channels):
+// the CLS rows [0, row0) = e(cls + cls_pos) — the reference's cls_token + pos_embed[:, :1]
+// in the model dtype (videomamba.py:806-815) — and pad_rows zero rows after the last token.
+// Folded in here they cost no launches of their own (three small torch kernels before).
+template <typename T>
+__device__ __forceinline__ void patch_frame_rows(const PatchParams& p) {
+  const int head = p.cls ? p.row0 : 0;
+  const int per_b = head + p.pad_rows;
+  if (blockIdx.y != 0 || per_b == 0) return;
+  const int ntok = p.tt * p.gh * p.gw;
+  const int total = p.batch * per_b * p.embed;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int br = i / p.embed;
+    const int c = i - br * p.embed;
+    const int b = br / per_b;
+    const int r = br - b * per_b;
+    float v = 0.0f;
+    int row = p.row0 + ntok + (r - head);
+    if (r < head) {
+      row = r;
+      v = to_f32(static_cast<const T*>(p.cls)[c]) + to_f32(static_cast<const T*>(p.cls_pos)[c]);
+    }
+    static_cast<T*>(p.out)[b * p.out_sb + static_cast<long long>(row) * p.embed + c] = from_f32<T>(v);
+  }
+}
 
 template <typename T>
 __device__ __forceinline__ void patch_store(const PatchParams& p, int m, int n, float acc) {
@@ -70,6 +99,7 @@ __device__ __forceinline__ long long k_offset(const PatchParams& p, int k) {
 }
 
 __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
+  patch_frame_rows<bf16_t>(p);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int m0 = blockIdx.x * 64 + (wave & 1) * 32;
@@ -131,6 +161,7 @@ __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
 // temporal adds and the stores run on 8-channel vectors of whole output rows.
 constexpr int kPT = 64, kPN = 192, kPJ = 6;  // tokens, channels per workgroup; 16-col tiles per wave
 __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) {
+  patch_frame_rows<bf16_t>(p);
   __shared__ __attribute__((aligned(16))) bf16_t stile[kPT * (kPN + 8)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -246,6 +277,7 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
 // patch_mfma16_kernel.  Same k order and rounding points as the 64x64 kernel.
 constexpr int kGT = 128, kGN = 192, kGP = 40;  // tile tokens, channels; LDS row pitch (bf16)
 __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
+  patch_frame_rows<bf16_t>(p);
   // staging: 2 buffers x (A 128 x 40 + B 192 x 40) bf16 = 40 KB; epilogue: 128 x 200 bf16
   __shared__ __attribute__((aligned(16))) bf16_t smem[kGT * (kGN + 8)];
   const int tid = threadIdx.x;
@@ -391,6 +423,7 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void patch_generic_kernel(const PatchParams p) {
+  patch_frame_rows<T>(p);
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (long long)p.M * p.embed) return;
   const int m = static_cast<int>(gid / p.embed);
@@ -411,18 +444,22 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
                                   const void* spos, const void* tpos, void* out, long long out_sb,
                                   int row0, int batch, int cin, int frames, int height, int width,
                                   int kt, int patch_h, int patch_w, int embed, int dtype,
+                                  const void* cls, const void* cls_pos, int pad_rows,
                                   vm_stream_t stream) {
   if (!video || !weight || !bias || !spos || !tpos || !out) {
     vmhost::set_error("vm_patch_embed_fwd: null required pointer");
     return VM_E_INVALID;
   }
   if (batch < 0 || cin < 1 || kt < 1 || patch_h < 1 || patch_w < 1 || embed < 1 ||
-      frames % kt != 0 || height < patch_h || width < patch_w || !vmhost::dtype_ok(dtype)) {
+      frames % kt != 0 || height < patch_h || width < patch_w || !vmhost::dtype_ok(dtype) ||
+      row0 < 0 || pad_rows < 0 || (cls == nullptr) != (cls_pos == nullptr) ||
+      1LL * batch * (pad_rows + (cls ? row0 : 0)) * embed > 0x7fffffffLL) {
     vmhost::set_error("vm_patch_embed_fwd: bad shape/dtype");
     return VM_E_INVALID;
   }
   PatchParams p{};
   p.video = video; p.w = weight; p.bias = bias; p.spos = spos; p.tpos = tpos; p.out = out;
+  p.cls = cls; p.cls_pos = cls_pos; p.pad_rows = pad_rows;
   p.out_sb = out_sb; p.row0 = row0; p.batch = batch; p.cin = cin; p.frames = frames;
   p.height = height; p.width = width; p.kt = kt; p.ph = patch_h; p.pw = patch_w; p.embed = embed;
   p.tt = frames / kt; p.gh = height / patch_h; p.gw = width / patch_w;

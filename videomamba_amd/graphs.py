@@ -14,8 +14,9 @@ chunk kind (first chunk with CLS, continuation chunk without) into a ``torch.cud
   eager ``model(x, ssm_state=..., temporal_pos_offset=...)`` would return minus the state
   container — views of static buffers, valid until the next ``run``;
 * the state advances in place (the ssm state is updated in place by the scan as in the
-  eager path; the conv kernels write every layer's new conv window into one stacked buffer
-  and the graph copies it back into the stacked state in one copy),
+  eager path; the conv windows live in two stacked buffers used in turn — a chunk reads
+  the current one and its conv kernels write the next, so no copy carries them over: each
+  chunk kind is captured once per buffer parity),
   so consecutive ``run`` calls stream exactly like the eager loop with carried state.
 
 Semantics are the eager path's (same kernels, same rounding points); tests check replay
@@ -83,14 +84,15 @@ class StreamingChunkGraph:
                                     device=self.device)
         self.static_tpos = torch.zeros(1, self.tt, model.embed_dim, dtype=self.dtype,
                                        device=self.device)
-        # per-layer states as views of two stacked buffers: the new conv states land in
-        # _conv_next (written by the conv kernels) and one copy per chunk carries them over
+        # per-layer conv states as views of two stacked buffers used in turn: a chunk reads
+        # _conv[_cur] and its conv kernels write _conv[1 - _cur] (a copy back cost a 4 us
+        # launch per chunk); the ssm states are updated in place
         st = model.allocate_state(batch, dtype=self.dtype, device=self.device)
-        self._conv_all = torch.stack([c for c, _ in st])
-        self._conv_next = torch.empty_like(self._conv_all)
-        self._state: List[Tuple[Tensor, Tensor]] = [
-            (self._conv_all[i], s) for i, (_, s) in enumerate(st)]
-        self._graphs: Dict[bool, Tuple[torch.cuda.CUDAGraph, object]] = {}
+        conv = torch.stack([c for c, _ in st])
+        self._conv = (conv, torch.zeros_like(conv))
+        self._ssm = [s for _, s in st]
+        self._cur = 0
+        self._graphs: Dict[Tuple[bool, int], Tuple[torch.cuda.CUDAGraph, object]] = {}
         self._pool = None
         self._param_key = None
         self._plist = None
@@ -100,32 +102,38 @@ class StreamingChunkGraph:
         self._cnt = None  # vm_linear_add_norm_fwd hand-off counters (zeroed, left zeroed)
 
     # ------------------------------------------------------------------ state
+    def _state_at(self, parity: int) -> List[Tuple[Tensor, Tensor]]:
+        conv = self._conv[parity]
+        return [(conv[i], s) for i, s in enumerate(self._ssm)]
+
     @property
     def state(self) -> List[Tuple[Tensor, Tensor]]:
-        """The carried per-layer (conv_state, ssm_state) — static buffers, updated by run()."""
-        return self._state
+        """The carried per-layer (conv_state, ssm_state): views of the runner's static
+        buffers, current until the next run() (which moves the conv states to the other
+        buffer of the pair)."""
+        return self._state_at(self._cur)
 
     def reset_state(self) -> None:
-        for c, s in self._state:
+        for c, s in self.state:
             c.zero_()
             s.zero_()
 
     def load_state(self, state) -> None:
-        for (c, s), (c2, s2) in zip(self._state, state):
+        for (c, s), (c2, s2) in zip(self.state, state):
             c.copy_(c2)
             s.copy_(s2)
 
     # ------------------------------------------------------------------ capture / replay
-    def _body(self, has_cls: bool):
+    def _body(self, has_cls: bool, parity: int):
         m = self.model
         offset = 0 if has_cls else 1  # only has_cls matters inside; tpos comes from the buffer
         pool = None
         if m.add_pool_norm:
             gh, gw = m._spatial_token_grid(self.static_x.shape[-2], self.static_x.shape[-1])
             pool = (False, self.tt, gh * gw)
-        feats, x_pool, _ = m._encode(self.static_x, None, self._state, offset,
-                                     tpos=self.static_tpos, pool=pool, conv_out=self._conv_next)
-        self._conv_all.copy_(self._conv_next)
+        feats, x_pool, _ = m._encode(self.static_x, None, self._state_at(parity), offset,
+                                     tpos=self.static_tpos, pool=pool,
+                                     conv_out=self._conv[1 - parity])
         if pool is None:
             return (feats,)
         return (feats[:, 1:] if has_cls else feats), x_pool
@@ -175,23 +183,27 @@ class StreamingChunkGraph:
             raise RuntimeError("StreamingChunkGraph: a replayed one-launch scan timed out on a "
                                "block hand-off; the affected outputs were NaN")
 
-    def _capture(self, has_cls: bool):
-        saved = [(c.clone(), s.clone()) for c, s in self._state]
+    def _capture(self, has_cls: bool, parity: int):
+        # the warm-up passes advance the ssm states in place and write the other conv
+        # buffer: keep the current states to restore them
+        saved = [(c.clone(), s.clone()) for c, s in self._state_at(parity)]
         ws = self._workspace()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.no_grad(), torch.cuda.stream(side), K.scratch_override(ws), \
                 K.sync_override(self._sync), K.counter_override(self._cnt):
             for _ in range(2):  # warm caches (fp32 params, padded weights) and GEMM plans
-                self._body(has_cls)
+                self._body(has_cls, parity)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws), \
                 K.sync_override(self._sync), K.counter_override(self._cnt):
-            outs = self._body(has_cls)
+            outs = self._body(has_cls, parity)
         self._pool = g.pool()
-        self.load_state(saved)  # warm-up passes advanced the state: restore it
-        self._graphs[has_cls] = (g, outs)
+        for (c, s), (c2, s2) in zip(self._state_at(parity), saved):
+            c.copy_(c2)
+            s.copy_(s2)
+        self._graphs[(has_cls, parity)] = (g, outs)
 
     def run(self, x: Tensor, temporal_pos_offset: int = 0):
         """One chunk: (x_vis, x_pool) with ``add_pool_norm``, else x_vis — as the eager
@@ -215,8 +227,10 @@ class StreamingChunkGraph:
             self.static_tpos.copy_(tpos)
             self._tpos_offset = temporal_pos_offset
         self.static_x.copy_(x)
-        if has_cls not in self._graphs:
-            self._capture(has_cls)
-        g, outs = self._graphs[has_cls]
+        key = (has_cls, self._cur)
+        if key not in self._graphs:
+            self._capture(*key)
+        g, outs = self._graphs[key]
         g.replay()
+        self._cur = 1 - self._cur  # the conv kernels wrote the other buffer
         return outs[0] if len(outs) == 1 else outs

@@ -288,6 +288,33 @@ def scan_chunk_steps(batch: int, dim: int, seqlen: int, dstate: int, segments: i
 
 
 SCAN_DTPROJ_MAX_SEGMENT = 64  # the segmented dt_proj-in-scan form (ABI v11)
+_SCAN_CHUNK_SEGS_PER_BLOCK = 8  # segments per workgroup of the chunked scan (kChW)
+_CU_COUNT = {}
+
+
+def _cu_count(device) -> int:
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _CU_COUNT:
+        _CU_COUNT[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count)
+    return _CU_COUNT[idx]
+
+
+def scan_dtproj_segmented_pays(batch: int, dim: int, seqlen: int, dstate: int, device,
+                               segments: int = -1) -> bool:
+    """Whether the mixer should fold dt_proj into the SEGMENTED scan for this shape: segments
+    of at most 64 steps, and a grid that fits the chip at one workgroup per CU.  Each wave's
+    dt block lives in LDS (119 KB per workgroup), which admits one workgroup per CU; where
+    the plain chunked scan would stack several per CU the folded form measured slower than
+    it saves in conv_proj (B = 4 M-16f: 138.6 vs 111.2 us per scan against ~19 us of dt
+    rows; B = 1 / 2 with 252-workgroup grids: +1.9 / +1.5 us per scan against 4.7 / ~9 us;
+    profiles/r04v_scan_segments_dtp.jsonl)."""
+    steps = scan_chunk_steps(batch, dim, seqlen, dstate, segments)
+    if not 0 < steps <= SCAN_DTPROJ_MAX_SEGMENT:
+        return False
+    segs = -(-seqlen // steps)
+    nblk = -(-segs // _SCAN_CHUNK_SEGS_PER_BLOCK)
+    return batch * (-(-dim // 64)) * nblk <= _cu_count(device)
 
 
 def scan_dtproj_raw(u, u_s, dtl, dtl_s, dt_rank, wdt_pad, A32, B, b_s, C, c_s, D32, z, z_s,
@@ -755,17 +782,31 @@ def layer_norm_fn(x: Tensor, weight: Tensor, bias: Optional[Tensor], residual: O
 
 # --------------------------------------------------------------------------- patch embed
 def patch_embed(video: Tensor, weight: Tensor, bias: Tensor, spos: Tensor, tpos: Tensor,
-                out: Tensor, row0: int, out_batch_stride: int) -> None:
+                out: Tensor, row0: int, out_batch_stride: int, cls: Optional[Tensor] = None,
+                cls_pos: Optional[Tensor] = None, pad_rows: int = 0,
+                bias32: Optional[Tensor] = None) -> None:
     """Conv3d tubelet embed + bias + spatial/temporal positional adds, written as token
-    rows into ``out`` (token j of batch b at ``out[b*out_batch_stride + (row0+j)*C]``)."""
+    rows into ``out`` (token j of batch b at ``out[b*out_batch_stride + (row0+j)*C]``).
+    ``cls`` / ``cls_pos`` (C values each): rows [0, row0) of every batch = cls + cls_pos in
+    the model dtype; ``pad_rows`` zero rows after the tokens (ABI v12, same launch).
+    ``bias32``: the bias already in fp32 (a cached copy), else converted here."""
     require_gpu(video, weight, bias, spos, tpos, out, what="patch_embed")
     Bsz, cin, T, H, W = video.shape
     C, _, kt, Ph, Pw = weight.shape
     dt = dtype_code(weight.dtype)
     video = video.to(weight.dtype).contiguous()
+    if (cls is None) != (cls_pos is None):
+        raise ValueError("patch_embed: pass cls and cls_pos together")
+    if cls is not None:
+        cls = cls.reshape(-1).to(weight.dtype).contiguous()
+        cls_pos = cls_pos.reshape(-1).to(weight.dtype).contiguous()
+        if cls.numel() != C or cls_pos.numel() != C:
+            raise ValueError(f"patch_embed: cls / cls_pos need {C} values")
     lib = _lib.load()
     rc = lib.vm_patch_embed_fwd(
-        _p(video), _p(weight.contiguous()), _p(f32c(bias)), _p(spos.to(weight.dtype).contiguous()),
+        _p(video), _p(weight.contiguous()), _p(bias32 if bias32 is not None else f32c(bias)),
+        _p(spos.to(weight.dtype).contiguous()),
         _p(tpos.to(weight.dtype).contiguous()), _p(out), out_batch_stride, row0,
-        Bsz, cin, T, H, W, kt, Ph, Pw, C, dt, _stream(video))
+        Bsz, cin, T, H, W, kt, Ph, Pw, C, dt, _p(cls), _p(cls_pos), int(pad_rows),
+        _stream(video))
     _lib.check(rc, "vm_patch_embed_fwd")

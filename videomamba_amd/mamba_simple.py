@@ -299,7 +299,9 @@ class Mamba(nn.Module):
     def _dtp_ok(self, hn: Tensor, seqlen: int, conv_state_in: Optional[Tensor] = None) -> bool:
         """Fold dt_proj into the scan (vm_selective_scan_dtproj_fwd, conv_proj then writes no
         dt rows): bf16 fused conv_proj path, 16 states, dt_rank a multiple of 4, and
-          * a segmented scan (streaming batches) of at most 64 steps per segment: each segment
+          * a segmented scan (streaming batches) of at most 64 steps per segment whose grid
+            fits the chip at one workgroup per CU (K.scan_dtproj_segmented_pays; "on": any
+            grid): each segment
             computes its dt exactly as conv_proj's dt_proj would (ABI v11), so the bits are the
             ones conv_proj writes otherwise — the choice never changes a result, and chunked
             == full stays exact whichever form a chunk length selects; or
@@ -316,7 +318,10 @@ class Mamba(nn.Module):
             return False
         steps = K.scan_chunk_steps(Bsz, self.d_inner, seqlen, self.d_state)
         if steps > 0:
-            return steps <= K.SCAN_DTPROJ_MAX_SEGMENT
+            if mode == "on":
+                return steps <= K.SCAN_DTPROJ_MAX_SEGMENT
+            return K.scan_dtproj_segmented_pays(Bsz, self.d_inner, seqlen, self.d_state,
+                                                hn.device)
         if mode == "auto" and Bsz <= 8:
             return False
         return self.d_inner % 128 == 0

@@ -23,9 +23,11 @@ documented options object; tests and sweeps change them with :func:`override`.
                      the two-launch form (identical results).
     scan_dt_proj     "auto" (default): the bf16 token-major mixer folds dt_proj into the scan
                      (vm_selective_scan_dtproj_fwd) and conv_proj skips its dt rows when the
-                     scan is segmented with <= 64-step segments (streaming batches; dt in
-                     conv_proj's own arithmetic, ABI v11) or single-pass above 8 clips; "on":
-                     also single-pass at <= 8 clips (tests); "off": conv_proj writes dt.
+                     scan is segmented with <= 64-step segments on a grid of at most one
+                     workgroup per CU (streaming batches 1-2 at M-16f; dt in conv_proj's own
+                     arithmetic, ABI v11) or single-pass above 8 clips; "on": also on larger
+                     segmented grids and single-pass at <= 8 clips (tests); "off": conv_proj
+                     writes dt.
     projection_gemm  "hip" (default): the mixer's bf16 in_proj / out_proj run on the HIP GEMM
                      (vm_linear_fwd: the LDS-DMA tile kernel for small row counts, the
                      persistent 256-row kernel from 1.5 tiles per CU up; bit-identical forms)

@@ -218,9 +218,12 @@ class PatchEmbed(nn.Module):
         self.proj = nn.Conv3d(in_chans, embed_dim, kernel_size=(kernel_size, patch[0], patch[1]),
                               stride=(kernel_size, patch[0], patch[1]))
 
-    def embed_tokens(self, x: Tensor, spos: Tensor, tpos: Tensor, out: Tensor, row0: int):
+    def embed_tokens(self, x: Tensor, spos: Tensor, tpos: Tensor, out: Tensor, row0: int,
+                     cls: Optional[Tensor] = None, cls_pos: Optional[Tensor] = None,
+                     pad_rows: int = 0):
         K.patch_embed(x, self.proj.weight, self.proj.bias, spos, tpos, out, row0,
-                      out.stride(0))
+                      out.stride(0), cls=cls, cls_pos=cls_pos, pad_rows=pad_rows,
+                      bias32=K.f32_cached(self, self.proj.bias, "b"))
 
     def forward(self, x: Tensor) -> Tensor:
         K.require_gpu(x, what="PatchEmbed")
@@ -566,11 +569,12 @@ class PretrainVideoMamba(nn.Module):
         L = Tt * Gh * Gw + (1 if has_cls else 0)
         Lp = round_up(L)
         buf = torch.empty((Bsz, Lp, self.embed_dim), dtype=dt, device=x.device)
-        self.patch_embed.embed_tokens(x, spos[0], tpos[0], buf, 1 if has_cls else 0)
-        if has_cls:
-            buf[:, 0] = (self.cls_token + self.pos_embed[:, :1].to(dtype=dt))[:, 0].to(dt)
-        if Lp > L:
-            buf[:, L:] = 0
+        # the CLS row (cls_token + pos_embed[:, :1] in the model dtype) and the zero padding
+        # rows are written by the patch-embed launch itself
+        cls = self.cls_token.detach().to(dt) if has_cls else None
+        cls_pos = self.pos_embed.detach()[0, 0].to(dt) if has_cls else None
+        self.patch_embed.embed_tokens(x, spos[0], tpos[0], buf, 1 if has_cls else 0,
+                                      cls=cls, cls_pos=cls_pos, pad_rows=Lp - L)
         return buf, L, Tt, Gh * Gw
 
     def forward_features(self, x: Tensor, mask: Optional[Tensor] = None, use_image: bool = False,
