@@ -308,16 +308,22 @@ __device__ __forceinline__ void dma_wait_vm_lgkm0() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
 }
 
-template <int BM, int BN, int NK, int NBUF>
-__global__ __launch_bounds__(256) void linear_dma_kernel(const LinParams p) {
+// NWM = wave rows (2: 4 waves in 2 x 2; 4: 8 waves in 4 x 2, two per SIMD at one workgroup
+// per CU — a wave's MFMA / LDS-read latency then has a partner to hide behind)
+template <int BM, int BN, int NK, int NBUF, int NWM = 2>
+__global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p) {
   constexpr int R = kDmaRow;
+  constexpr int NW = 2 * NWM;     // waves
+  constexpr int NT = 64 * NW;     // threads
   constexpr int STAGE = (BM + BN) * R;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / NWM, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int GA = BM * R / 4096, GB = BN * R / 4096;  // DMA instructions per wave per stage
+  constexpr int GA = BM * R / (1024 * NW), GB = BN * R / (1024 * NW);  // DMA instr. per wave per stage
   constexpr int G = GA + GB;
   static_assert(NBUF >= 2 && NBUF <= 4, "one to three stages in flight");
-  static_assert(GA * 4096 == BM * R && GB * 4096 == BN * R, "tile rows must fill whole DMA rounds");
+  static_assert(TM * 16 == WM && TN * 16 == WN, "wave tiles of whole 16 x 16 blocks");
+  static_assert(GA * 1024 * NW == BM * R && GB * 1024 * NW == BN * R,
+                "tile rows must fill whole DMA rounds");
   constexpr int kOutPitch = BN + 8;
   static_assert(BM * kOutPitch * 2 <= NBUF * STAGE, "output tile must fit the stage buffers");
   extern __shared__ __attribute__((aligned(16))) char dsm[];
@@ -436,9 +442,9 @@ __global__ __launch_bounds__(256) void linear_dma_kernel(const LinParams p) {
   __syncthreads();
   constexpr int kPieces = BM * BN / 8;
 #pragma unroll
-  for (int i = 0; i < (kPieces + 255) / 256; ++i) {
-    const int pc = tid + 256 * i;
-    if (kPieces % 256 != 0 && pc >= kPieces) break;
+  for (int i = 0; i < (kPieces + NT - 1) / NT; ++i) {
+    const int pc = tid + NT * i;
+    if (kPieces % NT != 0 && pc >= kPieces) break;
     const int row = pc / (BN / 8), cq = pc % (BN / 8);
     const int gm = m0 + row, gn = n0 + cq * 8;
     if (gm < p.m && gn < p.n)
@@ -450,25 +456,31 @@ __global__ __launch_bounds__(256) void linear_dma_kernel(const LinParams p) {
 // Tile choice for the pipelined form (row bits do not depend on it), measured at the B = 1
 // chunk shapes (scripts/diag/variant_linear.py): wide outputs (in_proj, N = 2 * d_inner)
 // on 128 x 128 tiles with two stage buffers (64 KB: two workgroups per CU; 14.1 us against
-// 17.6 for linear_kernel, three buffers 16.3); narrow ones (out_proj, N = d_model) on
-// 128 x 64 tiles with three buffers (72 KB; 9.1 against 11.3 us).
-#define VM_LDMA_TILE(BMV, BNV, NBV)                                                         \
-  {                                                                                         \
-    const dim3 grid((p.m + BMV - 1) / BMV, (p.n + BNV - 1) / BNV);                          \
-    const size_t lds = static_cast<size_t>(NBV) * (BMV + BNV) * kDmaRow;                    \
-    switch (p.k / kLinBK) {                                                                 \
-      VM_LDMA_K(BMV, BNV, NBV, 3) VM_LDMA_K(BMV, BNV, NBV, 6) VM_LDMA_K(BMV, BNV, NBV, 9)   \
-      VM_LDMA_K(BMV, BNV, NBV, 12) VM_LDMA_K(BMV, BNV, NBV, 18) VM_LDMA_K(BMV, BNV, NBV, 24) \
-      default: break;                                                                       \
-    }                                                                                       \
+// 17.6 for linear_kernel, three buffers 16.3), eight waves each since round 4 (four per
+// SIMD with the second workgroup: 13.2 against 14.3-14.7 us, B = 2 21.9 against 22.9;
+// 256 x 128 / 128 x 256 tiles at one workgroup per CU, 8 or 16 waves, 14.2-14.3 us;
+// profiles/r04x_linear_waves.jsonl); narrow ones (out_proj, N = d_model) on 128 x 64
+// tiles with three buffers and four waves (72 KB; 9.1 against 11.3 us; eight waves no
+// better at B = 1).
+#define VM_LDMA_TILE(BMV, BNV, NBV, NWMV)                                                     \
+  {                                                                                           \
+    const dim3 grid((p.m + BMV - 1) / BMV, (p.n + BNV - 1) / BNV);                            \
+    const size_t lds = static_cast<size_t>(NBV) * (BMV + BNV) * kDmaRow;                      \
+    switch (p.k / kLinBK) {                                                                   \
+      VM_LDMA_K(BMV, BNV, NBV, NWMV, 3) VM_LDMA_K(BMV, BNV, NBV, NWMV, 6)                     \
+      VM_LDMA_K(BMV, BNV, NBV, NWMV, 9) VM_LDMA_K(BMV, BNV, NBV, NWMV, 12)                    \
+      VM_LDMA_K(BMV, BNV, NBV, NWMV, 18) VM_LDMA_K(BMV, BNV, NBV, NWMV, 24)                   \
+      default: break;                                                                         \
+    }                                                                                         \
   }
-#define VM_LDMA_K(BMV, BNV, NBV, NKV)                                                        \
-  case NKV:                                                                                  \
-    hipLaunchKernelGGL((linear_dma_kernel<BMV, BNV, NKV, NBV>), grid, dim3(256), lds, s, p); \
+#define VM_LDMA_K(BMV, BNV, NBV, NWMV, NKV)                                                    \
+  case NKV:                                                                                    \
+    hipLaunchKernelGGL((linear_dma_kernel<BMV, BNV, NKV, NBV, NWMV>), grid, dim3(128 * NWMV), \
+                       lds, s, p);                                                             \
     break;
 static void linear_dma_launch(const LinParams& p, hipStream_t s) {
-  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2)
-  else VM_LDMA_TILE(128, 64, 3)
+  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)
+  else VM_LDMA_TILE(128, 64, 3, 2)
 }
 #undef VM_LDMA_K
 #undef VM_LDMA_TILE
