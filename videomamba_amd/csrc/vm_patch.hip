@@ -33,7 +33,7 @@ struct PatchParams {
 };
 
 // The rows of the padded token buffer around the patch tokens, written by the launch's
-// blockIdx.y == 0 workgroups before their tiles (grid-stride over batch x rows x channels):
+// blockIdx.y == 0 workgroups after their tiles (the scalar fallback: before) (grid-stride over batch x rows x channels):
 // the CLS rows [0, row0) = e(cls + cls_pos) — the reference's cls_token + pos_embed[:, :1]
 // in the model dtype (videomamba.py:806-815) — and pad_rows zero rows after the last token.
 // Folded in here they cost no launches of their own (three small torch kernels before).
@@ -99,7 +99,6 @@ __device__ __forceinline__ long long k_offset(const PatchParams& p, int k) {
 }
 
 __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
-  patch_frame_rows<bf16_t>(p);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int m0 = blockIdx.x * 64 + (wave & 1) * 32;
@@ -152,6 +151,7 @@ __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
         const int n = n0 + j * 16 + r;
         if (m < p.M && n < p.embed) patch_store<bf16_t>(p, m, n, acc[i][j][e]);
       }
+  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
 }
 
 // 16x16 patches, bf16, embed % 192 == 0 (the VideoMamba shapes): workgroup tile
@@ -161,7 +161,6 @@ __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
 // temporal adds and the stores run on 8-channel vectors of whole output rows.
 constexpr int kPT = 64, kPN = 192, kPJ = 6;  // tokens, channels per workgroup; 16-col tiles per wave
 __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) {
-  patch_frame_rows<bf16_t>(p);
   __shared__ __attribute__((aligned(16))) bf16_t stile[kPT * (kPN + 8)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -267,6 +266,7 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
     *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
         make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
+  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
 }
 
 // 16x16 patches, bf16, embed % 192 == 0, an LDS-staged GEMM: workgroup tile 128 tokens x
@@ -277,7 +277,6 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
 // patch_mfma16_kernel.  Same k order and rounding points as the 64x64 kernel.
 constexpr int kGT = 128, kGN = 192, kGP = 40;  // tile tokens, channels; LDS row pitch (bf16)
 __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
-  patch_frame_rows<bf16_t>(p);
   // staging: 2 buffers x (A 128 x 40 + B 192 x 40) bf16 = 40 KB; epilogue: 128 x 200 bf16
   __shared__ __attribute__((aligned(16))) bf16_t smem[kGT * (kGN + 8)];
   const int tid = threadIdx.x;
@@ -419,6 +418,7 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
     *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
         make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
+  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
 }
 
 template <typename T>
