@@ -796,15 +796,21 @@ __global__ __launch_bounds__(64 * kFuMaxSpl) void conv_proj_fused_kernel(const S
   };
   const int b0 = tok0 / p.out_len;  // batch row and step of the tile's first token
   const int s0 = tok0 - b0 * p.out_len;
+  // the channel pair's taps as packed operands: v_pk_fma_f32 does per lane exactly the
+  // scalar fmaf chain (same taps, same order), half the VALU issue
+  typedef __attribute__((ext_vector_type(2))) float fp2;
+  fp2 wp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wp[k] = fp2{wl[k], wh[k]};
   uint32_t upk[kFuTok];
 #pragma unroll
   for (int i = 0; i < kFuTok; ++i) {
-    float al = bl, ah = bh;
+    fp2 acc2 = fp2{bl, bh};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      al = fmaf(wl[k], __uint_as_float(xw[i + k] << 16), al);
-      ah = fmaf(wh[k], __uint_as_float(xw[i + k] & 0xffff0000u), ah);
-    }
+    for (int k = 0; k < 4; ++k)
+      acc2 = __builtin_elementwise_fma(
+          wp[k], fp2{__uint_as_float(xw[i + k] << 16), __uint_as_float(xw[i + k] & 0xffff0000u)}, acc2);
+    float al = acc2.x, ah = acc2.y;
     int st = s0 + i;
     if (st >= p.out_len) st -= p.out_len;  // out_len >= 16: at most one wrap
     if (st < 3) {  // uniform: the taps before the sequence start come from the old state
