@@ -111,6 +111,9 @@ VARIANTS = {
     # LDS-DMA GEMM tile alternatives for in_proj (N >= 1024) and out_proj at B = 1
     "ldma_i128x64": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                       "  if (p.n >= 1024) VM_LDMA_TILE(128, 64, 3, 2)")],
+    # wide conv_proj occupancy probe: LDS padded so 2 (cp_occ2) workgroups fit per CU instead of 3
+    "cp_occ2": [("vm_conv_proj.hip", "  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float);",
+                 "  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float) + 30000;")],
     # eight-wave (4 x 2) forms at one workgroup per CU (round 4)
     "ldma8_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                         "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 4)")],
