@@ -114,6 +114,8 @@ VARIANTS = {
     # wide conv_proj occupancy probe: LDS padded so 2 (cp_occ2) workgroups fit per CU instead of 3
     "cp_occ2": [("vm_conv_proj.hip", "  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float);",
                  "  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float) + 30000;")],
+    # final norm + pooling through the dtype-generic rows kernel only
+    "np_generic": [("vm_norm.hip", "constexpr bool kPoolFast = true;", "constexpr bool kPoolFast = false;")],
     # eight-wave (4 x 2) forms at one workgroup per CU (round 4)
     "ldma8_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                         "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 4)")],

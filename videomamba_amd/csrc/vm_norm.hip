@@ -252,6 +252,7 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const NormParams p) {
 // (and groups) in a fixed order, so the result is deterministic and independent of the
 // launch geometry; the reference's means are of the rounded patch tokens as well.
 constexpr int kPoolRB = 16;
+constexpr bool kPoolFast = true;  // bf16 rows through norm_pool_rows_bf16_kernel
 
 struct NormPoolParams {
   const void* x; const void* res; const float* w; const float* bias; void* out;
@@ -343,6 +344,137 @@ __global__ __launch_bounds__(256) void norm_pool_rows_kernel(const NormPoolParam
           acc[j][i] += y[i];
         }
         store4_dyn(p.out, on + c, p.out_dtype, y);
+      }
+    }
+  }
+  if (gy == 0 || !p.part) return;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane * 4 + 256 * j;
+    if (c < p.cols)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave * p.cols + c + i] = acc[j][i];
+  }
+  __syncthreads();
+  float* dst = p.part + (((long long)b * p.groups + gy - 1) * p.slices + s) * p.cols;
+  for (int c = threadIdx.x; c < p.cols; c += 256)
+    dst[c] = ((red[c] + red[p.cols + c]) + red[2 * p.cols + c]) + red[3 * p.cols + c];
+}
+
+// norm_pool_rows_kernel for bf16 x / out with an fp32 (or no) residual: the same arithmetic
+// in the same order, but every one of a wave's (at most kPoolRB / 4) rows is loaded by
+// branch-free buffer loads before the first is reduced.  The dtype-generic loads sit behind
+// branches whose joins make hipcc wait vmcnt(0): one dependent round trip per row and
+// chunk, which set the B = 1 chunk's final norm at ~15 us.
+template <int CPL>
+__global__ __launch_bounds__(256) void norm_pool_rows_bf16_kernel(const NormPoolParams p) {
+  extern __shared__ float red[];    // [4][cols]
+  constexpr int RPW = kPoolRB / 4;  // rows per wave
+  const int b = blockIdx.z, gy = blockIdx.y, s = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int lo, hi;
+  if (gy == 0) {
+    if (s) return;
+    lo = 0; hi = p.head;
+  } else if (p.bounds) {
+    lo = p.bounds[(long long)b * (p.groups + 1) + gy - 1];
+    hi = p.bounds[(long long)b * (p.groups + 1) + gy];
+  } else {
+    lo = p.head + (gy - 1) * p.group_rows;
+    hi = lo + p.group_rows;
+  }
+  const int r0 = lo + s * kPoolRB;
+  const int r1 = min(hi, r0 + kPoolRB);
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float v4f;
+  auto off = [&](int j, int es) {
+    int o = lane * 4 + 256 * j < p.cols ? (lane * 4 + 256 * j) * es : kNormOut;
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  uint32_t xq[RPW][CPL][2];
+  v4f rq[RPW][CPL];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int r = r0 + wave + 4 * k;
+    const bool live = r < r1;
+    int ri = live ? r : 0;
+    if (p.rev_frame > 0 && ri >= p.head) {
+      const int x = ri - p.head, F = p.rev_frame;
+      ri = p.head + x + (p.rows - p.head - F) - 2 * F * (x / F);
+    }
+    const long long in = (long long)b * p.in_bstride + (long long)ri * p.cols;
+    const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + in, live ? p.cols * 2 : 0);
+    const auto rr = norm_row_rsrc(p.res ? static_cast<const float*>(p.res) + in : p.w,
+                                  live && p.res ? p.cols * 4 : 0);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
+      xq[k][j][0] = q[0];
+      xq[k][j][1] = q[1];
+      rq[k][j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every row's loads in flight before any use
+  float acc[CPL][4];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int r = r0 + wave + 4 * k;
+    if (r >= r1) break;
+    const long long on = (long long)b * p.out_bstride + (long long)r * p.cols;
+    float v[CPL][4];
+    float sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const bool in_c = lane * 4 + 256 * j < p.cols;
+      v[j][0] = __uint_as_float(xq[k][j][0] << 16); v[j][1] = __uint_as_float(xq[k][j][0] & 0xffff0000u);
+      v[j][2] = __uint_as_float(xq[k][j][1] << 16); v[j][3] = __uint_as_float(xq[k][j][1] & 0xffff0000u);
+      if (p.res) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[j][i] += rq[k][j][i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!in_c) v[j][i] = 0.0f;
+        sum += v[j][i];
+      }
+    }
+    float mean = 0.0f, sq = 0.0f;
+    if (!p.is_rms) mean = wave_sum(sum) / p.cols;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const bool in_c = lane * 4 + 256 * j < p.cols;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dv = in_c ? v[j][i] - mean : 0.0f;
+        sq = fmaf(dv, dv, sq);
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(sq) / p.cols + p.eps);
+    const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + on, p.cols * 2);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane * 4 + 256 * j;
+      if (c < p.cols) {
+        const float4 w = *reinterpret_cast<const float4*>(p.w + c);
+        const float wv[4] = {w.x, w.y, w.z, w.w};
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          y[i] = (v[j][i] - mean) * rstd * wv[i];
+          if (p.bias) y[i] += p.bias[c + i];
+          y[i] = to_f32(from_f32<bf16_t>(y[i]));
+          acc[j][i] += y[i];
+        }
+        typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
+        const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
+                                         (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
+                        static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
+                                         (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
+        __builtin_amdgcn_raw_buffer_store_b64(o2, orr, c * 2, 0, 0);
       }
     }
   }
@@ -538,7 +670,15 @@ extern "C" int vm_norm_pool_fwd(const void* x, int x_dtype, const void* residual
   const size_t lds = 4 * cols * sizeof(float);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int cpl = (cols + 255) / 256;
-  if (cpl <= 1) hipLaunchKernelGGL(norm_pool_rows_kernel<1>, grid, dim3(256), lds, s, p);
+  const bool fast = kPoolFast && x_dtype == VM_DTYPE_BF16 && out_dtype == VM_DTYPE_BF16 &&
+                    (!residual || res_dtype == VM_DTYPE_F32) && cpl <= 4 &&
+                    (long long)(rows + 1) * cols * 4 < (1ll << 31);
+  if (fast) {
+    if (cpl <= 1) hipLaunchKernelGGL(norm_pool_rows_bf16_kernel<1>, grid, dim3(256), lds, s, p);
+    else if (cpl <= 2) hipLaunchKernelGGL(norm_pool_rows_bf16_kernel<2>, grid, dim3(256), lds, s, p);
+    else if (cpl <= 3) hipLaunchKernelGGL(norm_pool_rows_bf16_kernel<3>, grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL(norm_pool_rows_bf16_kernel<4>, grid, dim3(256), lds, s, p);
+  } else if (cpl <= 1) hipLaunchKernelGGL(norm_pool_rows_kernel<1>, grid, dim3(256), lds, s, p);
   else if (cpl <= 2) hipLaunchKernelGGL(norm_pool_rows_kernel<2>, grid, dim3(256), lds, s, p);
   else if (cpl <= 4) hipLaunchKernelGGL(norm_pool_rows_kernel<4>, grid, dim3(256), lds, s, p);
   else hipLaunchKernelGGL(norm_pool_rows_kernel<8>, grid, dim3(256), lds, s, p);
