@@ -104,9 +104,9 @@ VARIANTS = {
     # workgroup per CU); narrow outputs on 128x64 tiles with three buffers
     "ldma3": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 3, 2)")],
-    "ldma_o64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma_o64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                   "  else VM_LDMA_TILE(64, 64, 3, 2)")],
-    "ldma_o2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma_o2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                  "  else VM_LDMA_TILE(64, 64, 2, 2)")],
     # LDS-DMA GEMM tile alternatives for in_proj (N >= 1024) and out_proj at B = 1
     "ldma_i128x64": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
@@ -131,13 +131,13 @@ VARIANTS = {
                          "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 8)")],
     "ldma16_i128x128b3": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                            "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 3, 8)")],
-    "ldma16_o128x64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma16_o128x64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                         "  else VM_LDMA_TILE(128, 64, 3, 8)")],
-    "ldma8_o128x64b2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma8_o128x64b2": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                          "  else VM_LDMA_TILE(128, 64, 2, 4)")],
-    "ldma8_o128x64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma8_o128x64": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                        "  else VM_LDMA_TILE(128, 64, 3, 4)")],
-    "ldma8_o128x64b4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma8_o128x64b4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                          "  else VM_LDMA_TILE(128, 64, 4, 4)")],
     "ldma_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                        "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 2)")],
@@ -145,7 +145,7 @@ VARIANTS = {
                        "  if (p.n >= 1024) VM_LDMA_TILE(128, 256, 2, 2)")],
     "ldma_i64x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                       "  if (p.n >= 1024) VM_LDMA_TILE(64, 128, 3, 2)")],
-    "ldma_o64n4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 2)",
+    "ldma_o64n4": [("vm_gemm.hip", "  else VM_LDMA_TILE(128, 64, 3, 4)",
                     "  else VM_LDMA_TILE(64, 64, 4, 2)")],
     # one-launch chunked scan: the preceding blocks' flags polled one after another by
     # thread 0 (the round-2 form) instead of in parallel by wave 0

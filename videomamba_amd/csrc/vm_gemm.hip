@@ -460,8 +460,8 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
 // SIMD with the second workgroup: 13.2 against 14.3-14.7 us, B = 2 21.9 against 22.9;
 // 256 x 128 / 128 x 256 tiles at one workgroup per CU, 8 or 16 waves, 14.2-14.3 us;
 // profiles/r04x_linear_waves.jsonl); narrow ones (out_proj, N = d_model) on 128 x 64
-// tiles with three buffers and four waves (72 KB; 9.1 against 11.3 us; eight waves no
-// better at B = 1).
+// tiles with three buffers (72 KB; 9.1 against 11.3 us), eight waves since round 4 (B = 1
+// the same 9.4 us, B = 2 12.5-13.0 against 13.2-13.4; profiles/r04z_out_proj_waves.jsonl).
 #define VM_LDMA_TILE(BMV, BNV, NBV, NWMV)                                                     \
   {                                                                                           \
     const dim3 grid((p.m + BMV - 1) / BMV, (p.n + BNV - 1) / BNV);                            \
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
     break;
 static void linear_dma_launch(const LinParams& p, hipStream_t s) {
   if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)
-  else VM_LDMA_TILE(128, 64, 3, 2)
+  else VM_LDMA_TILE(128, 64, 3, 4)
 }
 #undef VM_LDMA_K
 #undef VM_LDMA_TILE
