@@ -116,6 +116,10 @@ VARIANTS = {
                  "  const size_t lds = static_cast<size_t>(dim) * 5 * sizeof(float) + 30000;")],
     # final norm + pooling through the dtype-generic rows kernel only
     "np_generic": [("vm_norm.hip", "constexpr bool kPoolFast = true;", "constexpr bool kPoolFast = false;")],
+    "ldma16_i128x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
+                         "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 8)")],
+    "ldma8_i64x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
+                       "  if (p.n >= 1024) VM_LDMA_TILE(64, 128, 2, 4)")],
     # eight-wave (4 x 2) forms at one workgroup per CU (round 4)
     "ldma8_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                         "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 4)")],
