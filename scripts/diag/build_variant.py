@@ -120,6 +120,17 @@ VARIANTS = {
                          "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 8)")],
     "ldma8_i64x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                        "  if (p.n >= 1024) VM_LDMA_TILE(64, 128, 2, 4)")],
+    # fused small-batch conv_proj pricing (results wrong): W_x fragments from an out-of-range
+    # offset (no traffic) / no x_proj MFMA / no u stores
+    "cf_nowx": [("vm_conv_proj_sk.hip",
+                 "                      wxr, opaque(kc < nch ? ((j * 16 + (lane & 15)) * p.dim + c0 + kc) * 2 : kOut),",
+                 "                      wxr, opaque(kOut + 0 * kc),")],
+    "cf_nomfma": [("vm_conv_proj_sk.hip",
+                   "      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wv[ks][j], acc[j], 0, 0, 0);\n  }\n  // u rows leave",
+                   "      acc[j][0] += av[0] + wv[ks][j][0];\n  }\n  // u rows leave")],
+    "cf_nou": [("vm_conv_proj_sk.hip",
+                "        opaque(ch < nch && tok0 + row < ntok ? ((tok0 + row) * static_cast<int>(p.u_tl) + c0 + ch) * 2\n                                             : kOut),",
+                "        opaque(kOut + 0 * ch),")],
     # eight-wave (4 x 2) forms at one workgroup per CU (round 4)
     "ldma8_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                         "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 4)")],
