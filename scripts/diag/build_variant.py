@@ -131,6 +131,10 @@ VARIANTS = {
     "cf_nou": [("vm_conv_proj_sk.hip",
                 "        opaque(ch < nch && tok0 + row < ntok ? ((tok0 + row) * static_cast<int>(p.u_tl) + c0 + ch) * 2\n                                             : kOut),",
                 "        opaque(kOut + 0 * ch),")],
+    # fused small-batch conv_proj with XCD-contiguous token tiles (the in_proj GEMM's row runs)
+    "cf_xcd": [("vm_conv_proj_sk.hip", "  const int tok0 = blockIdx.x * kFuTok;",
+                "  const int tok0 = [] { const int nwg = gridDim.x, h = blockIdx.x, x = h & 7, q = nwg >> 3, r = nwg & 7;"
+                " return ((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (h >> 3)) * kFuTok; }();")],
     # eight-wave (4 x 2) forms at one workgroup per CU (round 4)
     "ldma8_i256x128": [("vm_gemm.hip", "  if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)",
                         "  if (p.n >= 1024) VM_LDMA_TILE(256, 128, 2, 4)")],
