@@ -388,14 +388,14 @@ def _cpu_share(affinity):
 def cpu_baseline(cfg, threads):
     """the CPU path on the host cores, fp32 B=1, one clip of the bench
     config and of C1 (Ti 8x224^2).  The code timed is the oracle (the CPU restatement
-    pinned to the reference); it runs at 0.42x the reference's own time on M-16f
-    (profiles/r03_cpu_calibration.json, one session, same threads), so the headline
-    ``value`` is the reference's rate on these cores estimated from it (the measured
-    oracle rate divided by that calibration ratio); the oracle's own rate is ``port_value``.
-    ``threads`` 0 = every CPU this process may use (``_cpu_share``: the box's share of the
-    host; SURVEY 8(d)'s os.cpu_count() counts the whole shared host and oversubscribes the
-    share 16x there).  Median of 2 after 1 warm-up: a bounded sample (~10-30 s of CPU work)
-    so the bench stays within minutes."""
+    pinned to the reference), and ``value`` is its measured rate on these cores.  Beside it,
+    ``reference_estimate`` scales that rate by the oracle-vs-reference time ratio of one
+    calibration session (profiles/r03_cpu_calibration.json: 8 threads of the build
+    container's Xeon, not these cores) — an estimate of the reference's own CPU rate, never
+    the headline.  ``threads`` 0 = every CPU this process may use
+    (``_cpu_share``: the box's share of the host; SURVEY 8(d)'s os.cpu_count() counts the
+    whole shared host and oversubscribes the share 16x there).  Median of 2 after 1
+    warm-up: a bounded sample (~10-30 s of CPU work) so the bench stays within minutes."""
     model, affinity = _cpu_info()
     share = _cpu_share(affinity)
     if threads <= 0:
@@ -410,22 +410,26 @@ def cpu_baseline(cfg, threads):
     ratio, ratio_c1 = ratios.get(key), ratios.get("ti8")
     port = cfg["frames"] * 196 / dt
     port_c1 = ti["frames"] * 196 / dt_c1
-    return {"value": round(port * ratio, 2) if ratio else round(port, 2),
+    est = None
+    if ratio:
+        est = {"value": round(port * ratio, 2), "unit": "video-tokens/s",
+               "basis": f"the measured oracle rate x its time ratio to the reference's own CPU "
+                        f"forward ({ratio}), taken once at {cal.get('threads')} threads on "
+                        f"{cal.get('cpu_model')}; not re-measured on these cores",
+               "calibration": cal}
+    return {"value": round(port, 2),
             "unit": "video-tokens/s", "cores": threads, "kind": "port",
-            "value_basis": ("reference CPU path's rate on these cores, estimated: the timed "
-                            "oracle's rate x its one-session time ratio to the reference "
-                            f"({ratio})" if ratio else "the timed oracle's rate (no calibration)"),
-            "port_value": round(port, 2),
+            "value_basis": "the oracle (oracle/videomamba_oracle.py) timed on these cores",
+            "reference_estimate": est,
             "cpu_model": model, "host_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
             "cpu_share": share,
             "threads_policy": "the CPUs this process may use (OMP_NUM_THREADS / cgroup quota / "
                               "affinity); os.cpu_count() counts the whole shared host",
-            "calibration": cal,
             "sample": f"1 clip {cfg['name']} {cfg['frames']}x224^2 fp32 B=1, full forward, "
                       f"median of 2 after 1 warm-up ({dt:.2f} s at {threads} threads), "
                       "oracle/videomamba_oracle.py",
-            "c1": {"value": round(port_c1 * ratio_c1, 2) if ratio_c1 else round(port_c1, 2),
-                   "port_value": round(port_c1, 2), "unit": "video-tokens/s",
+            "c1": {"value": round(port_c1, 2), "unit": "video-tokens/s",
+                   "reference_estimate": round(port_c1 * ratio_c1, 2) if ratio_c1 else None,
                    "sample": f"C1: 1 clip {ti['name']} {ti['frames']}x224^2 fp32 B=1, median "
                              f"of 2 after 1 warm-up ({dt_c1:.2f} s)"}}
 

@@ -652,6 +652,36 @@ def test_graph_replay_matches_eager_streaming(layout, pool, add_pool_norm, dt):
                 torch.testing.assert_close(s1, s2, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_graph_replay_cls_chunk_on_odd_buffer_parity(dt):
+    """The (CLS chunk, conv buffer parity 1) graph: after an odd number of chunks the runner
+    reads its conv windows from the second stacked buffer; a reset then a new clip's first
+    (CLS) chunk replays that graph and equals the eager first chunk from zero state, and the
+    chunk after it equals the eager continuation.  ``runner.state`` is re-read
+    after every run (the views of the previous parity go stale by design)."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    torch.manual_seed(1)
+    model = _small_model(img_size=32, patch_size=16, depth=3, embed_dim=32, fused_add_norm=True,
+                         rms_norm=True, residual_in_fp32=True, num_frames=8, pool_type="avg",
+                         add_pool_norm=False).to(DEV, dt).eval()
+    x = torch.randn(2, 3, 8, 32, 32, device=DEV).to(dt)
+    runner = StreamingChunkGraph(model, batch=2, frames=2, height=32, width=32)
+    with torch.no_grad():
+        runner.run(x[:, :, 0:2], temporal_pos_offset=0)  # parity 0 -> 1
+        assert runner._cur == 1
+        runner.reset_state()
+        state = model.allocate_state(2, dtype=dt, device=DEV)
+        for c in range(2):
+            xc = x[:, :, 2 + 2 * c:4 + 2 * c]
+            eager, state = model(xc, ssm_state=state, temporal_pos_offset=2 * c)
+            got = runner.run(xc, temporal_pos_offset=2 * c)
+            torch.testing.assert_close(got, eager, rtol=0, atol=0)
+            for (c1, s1), (c2, s2) in zip(runner.state, state):
+                torch.testing.assert_close(c1, c2, rtol=0, atol=0)
+                torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    assert (True, 1) in runner._graphs and (False, 0) in runner._graphs
+
+
 # ------------------------------------------------------------------ BASELINE configs C2 / C4 / C5
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm()).item()
@@ -825,6 +855,65 @@ def test_c3_m_16f_bf16_bench_kernels_match_oracle():
     print(f"C3 M-16f bf16 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e} conv {rc:.3e}")
     assert rv <= 1e-2 and rp <= 1e-2 and rs <= 1e-2 and rc <= 1e-2, (rv, rp, rs, rc)
     torch.testing.assert_close(xv[:1].float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
+
+
+def test_c3_bench_batch_448_clips_bitwise_equal_small_batch_and_oracle():
+    """Correctness at the benched batch: the bench's exact C3 call —
+    VideoMamba-M 16x224^2 bf16, bf16 zero state, offset 0, cls+avg — at B = 448, where xz is
+    6.5 GB and u / y 3.2 GB (past every 31-bit buffer offset; the persistent projection GEMM,
+    the wide conv_proj without dt rows and the dt_proj-in-scan single-pass scan).  Clips
+    {0, 1, 223, 446, 447} of x_vis, x_pool and every layer's returned (conv, ssm) state are
+    bit-equal to the same clips run in a B = 9 batch with scan_segments = 1 (the same kernel
+    forms at small extents: every form is row-invariant by design), and clip 447 matches
+    orc.encoder_forward at the C3 tolerances (relative L2 <= 1e-2; reference
+    videomamba.py:943-1067, mamba_simple.py:331-339, :443-446)."""
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
+    with torch.no_grad():
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    model = model.to(torch.bfloat16).eval()
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(DEV)
+    B, picks = 448, [0, 1, 223, 446, 447]
+    g = torch.Generator(device=DEV).manual_seed(448)
+    x = torch.empty(B, 3, 16, 224, 224, device=DEV, dtype=torch.bfloat16)
+    for i in range(0, B, 64):
+        x[i:i + 64] = torch.randn(min(64, B - i), 3, 16, 224, 224, device=DEV, generator=g)
+    mx = model.layers[0].mixer
+    hn = torch.empty(1, 1, 576, device=DEV, dtype=torch.bfloat16).expand(B, 3144, 576)
+    assert mx._dtp_ok(hn, 3137)  # the bench's scan: dt_proj inside the single-pass scan
+    assert B * 3144 * 2304 * 2 > 2 ** 31 and B * 3144 * 1152 * 2 > 2 ** 31  # xz, u / y
+    with torch.no_grad():
+        st = model.allocate_state(B, dtype=torch.bfloat16, device=DEV)
+        xv, xp, st = model(x, ssm_state=st, temporal_pos_offset=0)
+        torch.cuda.synchronize()
+        K.check_scan_sync()
+        big_v = xv[picks].clone()
+        big_p = xp[picks].clone()
+        big_s = [(c[picks].clone(), s[picks].clone()) for c, s in st]
+        x9 = torch.cat([x[picks], x[2:6]]).contiguous()  # 9 clips, the picks first
+        x447 = x[447:448].cpu()
+        del xv, xp, st, x
+        torch.cuda.empty_cache()
+        st9 = model.allocate_state(9, dtype=torch.bfloat16, device=DEV)
+        with options.override(scan_segments=1):
+            v9, p9, st9 = model(x9, ssm_state=st9, temporal_pos_offset=0)
+    n = len(picks)
+    assert torch.equal(big_v, v9[:n]), (big_v.float() - v9[:n].float()).abs().max().item()
+    assert torch.equal(big_p, p9[:n])
+    for i, ((c, s), (c9, s9)) in enumerate(zip(big_s, st9)):
+        assert torch.equal(c, c9[:n]) and torch.equal(s, s9[:n]), i
+    cfg = dict(img_size=224, patch_size=16, depth=32, kernel_size=1, num_frames=16,
+               fused_add_norm=True, rms_norm=True, residual_in_fp32=True,
+               pool_type="cls+avg", norm_epsilon=1e-5, d_state=16, d_conv=4)
+    ost = [(torch.zeros(1, 1152, 4, dtype=torch.bfloat16),
+            torch.zeros(1, 1152, 16, dtype=torch.bfloat16)) for _ in range(32)]
+    torch.set_num_threads(16)
+    ref_v, ref_p, ref_st = orc.encoder_forward(p, cfg, x447, state=ost, temporal_pos_offset=0)
+    rv, rp = _rel(big_v[-1:].cpu(), ref_v), _rel(big_p[-1:].cpu(), ref_p)
+    rs = max(_rel(big_s[i][1][-1:].cpu(), ref_st[i][1]) for i in range(32))
+    print(f"C3 B=448 clip 447 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e}")
+    assert rv <= 1e-2 and rp <= 1e-2 and rs <= 1e-2, (rv, rp, rs)
 
 
 @pytest.mark.parametrize("bsz", [1, 3])

@@ -1093,6 +1093,32 @@ def test_persistent_linear_rejects_unsupported_shapes():
     assert torch.equal(y, K.linear(x, w, form="dma"))
 
 
+@pytest.mark.parametrize("m,n,k,past", [(470000, 2304, 576, "out"), (940000, 576, 1152, "x")])
+def test_persistent_linear_past_2gb_matches_slices_and_fp32(m, n, k, past):
+    """The bench's projection extents: at B = 448 xz is 6.5 GB and y 3.2 GB,
+    past every 31-bit buffer offset.  Here the output (in_proj shape, 2.17 GB) or x (out_proj
+    shape, 2.17 GB) crosses 2 GB.  Row slices straddling the byte-2^31 row, the first rows and
+    the last (partial) tile are bit-equal to the LDS-DMA form run on just those rows (rows do
+    not depend on the row count) and within one bf16 rounding of an fp32 torch product."""
+    g = torch.Generator(device=DEV).manual_seed(m % 1000 + n)
+    x = torch.empty(m, k, device=DEV, dtype=torch.bfloat16)
+    for r in range(0, m, 100000):  # fill in slabs: no fp32 copy of the whole operand
+        x[r:r + 100000] = torch.randn(min(100000, m - r), k, device=DEV, generator=g)
+    w = (torch.randn(n, k, device=DEV, generator=g) * k ** -0.5).to(torch.bfloat16)
+    row_bytes = (n if past == "out" else k) * 2
+    assert m * row_bytes > 2 ** 31
+    y = K.linear(x, w)  # the auto choice: the persistent form (the only one past 2 GB)
+    assert torch.equal(K.linear(x, w, form="persistent"), y)
+    edge = 2 ** 31 // row_bytes
+    for lo, hi in [(0, 700), (edge - 300, edge + 300), ((edge // 256) * 256 - 5, (edge // 256) * 256 + 261),
+                   (m - 613, m)]:
+        ref_rows = K.linear(x[lo:hi].contiguous(), w, form="dma")
+        assert torch.equal(y[lo:hi], ref_rows), (lo, hi)
+        ref = x[lo:hi].float() @ w.float().t()
+        assert ((y[lo:hi].float() - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-3).all(), (lo, hi)
+    assert torch.isfinite(y[::997].float()).all()
+
+
 def test_persistent_linear_is_repeatable_at_chip_filling_rows():
     """The persistent GEMM at the C4 B=72 projection shapes (226,368 rows: ~3.5 tiles per
     workgroup run) gives the same bits launch after launch.  Its first build counted the

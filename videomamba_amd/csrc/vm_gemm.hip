@@ -484,7 +484,6 @@ static void linear_dma_launch(const LinParams& p, hipStream_t s) {
 }
 #undef VM_LDMA_K
 #undef VM_LDMA_TILE
-constexpr bool kLinearDma = true;  // vm_linear_fwd runs the pipelined form
 
 // The persistent 256-row tile kernel (vm_gemm_tile.hip): bit-identical rows, used once the
 // tile count fills every CU several times over.
@@ -497,11 +496,17 @@ void gemm_tile_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long
 // in_proj (12,544 rows, 441 tiles) 41.9 -> ~35 us, the C5 chunk 8.55 -> 8.26 ms
 constexpr int kTileMinPerCU2 = 3;
 
-// CUs of the current device, cached per device id (one query per device per process)
-static int device_cus() {
+// CUs of the device that owns `stream` (the current device for the null stream), cached per
+// device id; 0 when it cannot be queried
+static int device_cus(hipStream_t stream) {
   static int cus[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (stream) {
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return 0;
+  }
+  if (dev < 0 || dev >= 64) return 0;
   if (!cus[dev]) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -558,7 +563,12 @@ extern "C" int vm_linear_fwd_form(const void* x, long long ldx, const void* w, l
     return VM_E_INVALID;
   }
   if (form != 1 && bn) {
-    const int wgs = device_cus() / 8 * 8;
+    const int wgs = device_cus(s) / 8 * 8;  // persistent workgroups: whole XCD runs
+    if (form == 2 && wgs < 8) {
+      vmhost::set_error("vm_linear_fwd_form: the persistent form needs the launch device's CU "
+                        "count (query failed or < 8 CUs)");
+      return VM_E_INVALID;
+    }
     if (wgs >= 8 && (form == 2 || 2 * gemm_tile_count(m, n, bn) >=
                                       static_cast<long long>(kTileMinPerCU2) * wgs)) {
       gemm_tile_launch(p.x, ldx, p.w, ldw, p.out, ldo, m, n, k, bn, wgs, s);
@@ -571,29 +581,7 @@ extern "C" int vm_linear_fwd_form(const void* x, long long ldx, const void* w, l
                       "multiple of 192 or 256)");
     return VM_E_INVALID;
   }
-  if (kLinearDma) {
-    linear_dma_launch(p, s);
-    return vmhost::launch_status("vm_linear_fwd");
-  }
-  const NormTail nt{};
-  const int ntn = (n + kLinBN - 1) / kLinBN;
-  // 128-row tiles when that still gives >= 1.5 workgroups per CU (256 CUs), else 64-row
-  const bool big = (long long)((m + 127) / 128) * ntn >= 384;
-  const int bm = big ? 128 : 64;
-  const dim3 grid((m + bm - 1) / bm, ntn);
-  const size_t lds = 2 * (bm + kLinBN) * kLinPitch * sizeof(bf16_t);
-  switch (k / kLinBK) {
-#define VM_LIN(NKV)                                                                       \
-  case NKV:                                                                               \
-    if (big) hipLaunchKernelGGL((linear_kernel<128, NKV>), grid, dim3(256), lds, s, p, nt); \
-    else hipLaunchKernelGGL((linear_kernel<64, NKV>), grid, dim3(256), lds, s, p, nt);    \
-    break;
-    VM_LIN(3) VM_LIN(6) VM_LIN(9) VM_LIN(12) VM_LIN(18) VM_LIN(24)
-#undef VM_LIN
-    default:
-      vmhost::set_error("vm_linear_fwd: k = %d (supported: 192, 384, 576, 768, 1152, 1536)", k);
-      return VM_E_INVALID;
-  }
+  linear_dma_launch(p, s);
   return vmhost::launch_status("vm_linear_fwd");
 }
 

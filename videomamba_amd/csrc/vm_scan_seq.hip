@@ -1782,7 +1782,8 @@ bool seq_dtp_chunk_supported(const ScanParams& p, const DtpArgs& q, int dtype, i
   int T, nblk;
   chunk_geometry(p.seqlen, S, &T, &nblk);
   return dtype == VM_DTYPE_BF16 && seq_supported(p, dtype) && seq_sgpr_bc(p, 2) && bc1 &&
-         p.z && p.softplus && p.split == p.batch && T <= kChDtpT && workspace_bytes >= need &&
+         p.dstate == kMaxN && p.z && p.softplus && p.split == p.batch && T <= kChDtpT &&
+         workspace_bytes >= need &&
          q.dtl && q.wdt && (q.wdt_ld == 32 || q.wdt_ld == 64) && q.dt_rank >= 1 &&
          q.dt_rank <= q.wdt_ld && q.dt_rank % 4 == 0 && q.dtl_sl >= q.dt_rank &&
          (reinterpret_cast<uintptr_t>(q.dtl) & 7) == 0 && q.dtl_sl % 4 == 0 && q.dtl_sb % 4 == 0 &&
