@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 12
+#define VM_ABI_VERSION 13
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -402,10 +402,14 @@ int vm_linear_fwd_form(const void* x, long long ldx, const void* w, long long ld
  *   h = bf16(x @ w^T);  residual += h (fp32, in place);  hn = bf16(rmsnorm(residual) * nw)
  * with vm_add_norm_fwd's exact arithmetic (bit-identical to vm_linear_fwd + vm_add_norm_fwd).
  * x (m, k), w (n, k), h (m, n), hn (m, n) bf16; residual (m, n) fp32; norm_weight (n) fp32.
- * Each 16-row granule is normalised by the workgroup whose hand-off counter add comes last
- * (agent-coherent h stores / loads, no spin, no co-residency assumption).  `counters`:
- * vm_linear_add_norm_counter_bytes(m) zeroed bytes, left zeroed; one buffer must not serve
- * two launches that can run at the same time.  n % 8 == 0, n <= 1024, k as vm_linear_fwd.
+ * ONE launch when the 128 x 64-tile grid fits the stream's device at one workgroup per CU
+ * (ABI v13; B = 1 out_proj shapes): after its tile every workgroup normalises a share of the
+ * rows, waiting (bounded) on per-128-row-tile counters that the tiles' producers add to
+ * after agent-coherent h stores; a timeout sets word 0 of `counters` and makes the rows NaN.
+ * Larger grids run vm_linear_fwd + vm_add_norm_fwd (contiguous h / residual / hn rows).
+ * `counters`: vm_linear_add_norm_counter_bytes(m) zeroed bytes, left zeroed; one buffer must
+ * not serve two launches that can run at the same time.  n % 8 == 0, n <= 1024, k as
+ * vm_linear_fwd.
  */
 long long vm_linear_add_norm_counter_bytes(int m);
 int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* w, long long ldw,

@@ -15,7 +15,9 @@ if len(sys.argv) > 2:  # option overrides, e.g. small_gemm_max_n=4096
     from videomamba_amd import options
     for kv in sys.argv[2:]:
         k, v = kv.split("=")
-        options._OPTS = options.dataclasses.replace(options.get(), **{k: type(getattr(options.get(), k))(v)})
+        t = type(getattr(options.get(), k))
+        val = v.lower() in ("1", "true", "yes", "on") if t is bool else t(v)
+        options._OPTS = options.dataclasses.replace(options.get(), **{k: val})
 torch.manual_seed(0)
 model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16).cuda().to(torch.bfloat16).eval()
 x = torch.randn(1, 3, 16, 224, 224, device="cuda").to(torch.bfloat16)
@@ -45,5 +47,5 @@ with torch.no_grad():
 lat.sort()
 rep.sort()
 key.sort()
-print(f"graph replays {n}: run() p50 {lat[n // 2]:.3f} ms  min {lat[0]:.3f} ms; "
+print(f"{sys.argv[2:]} graph replays {n}: run() p50 {lat[n // 2]:.3f} ms  min {lat[0]:.3f} ms; "
       f"replay-only p50 {rep[n // 2]:.3f} ms; params-key p50 {key[n // 2]:.3f} ms")

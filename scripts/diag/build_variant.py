@@ -30,6 +30,14 @@ VARIANTS = {
                     "  for (int tg = t_beg; PASS == 2 && tg < t_end; tg += kPF) {")],
     "sc_noloop2": [("vm_scan_seq.hip", "  for (int tg = t_beg; tg < t_end; tg += kPF) {",
                     "  for (int tg = t_beg; PASS == 1 && tg < t_end; tg += kPF) {")],
+    # one-launch chunked scan pricing (results wrong): the PASS 1 (ch_noloop1) / PASS 2
+    # (ch_noloop2) step loop skipped inside the same launch
+    "ch_noloop1": [("vm_scan_seq.hip", "    for (int tg = t_beg; tg < t_end; tg += kPF) {",
+                    "    for (int tg = t_beg; EMIT && tg < t_end; tg += kPF) {")],
+    "ch_noloop2": [("vm_scan_seq.hip", "    for (int tg = t_beg; tg < t_end; tg += kPF) {",
+                    "    for (int tg = t_beg; !EMIT && tg < t_end; tg += kPF) {")],
+    # dt_proj-in-scan kernel without the d16_hi u / z loads and fp32 dt block (round 5 A/B)
+    "dtp_nod16": [("vm_scan_seq.hip", "constexpr bool kDtpD16 = true;", "constexpr bool kDtpD16 = false;")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],
@@ -207,10 +215,12 @@ VARIANTS = {
     # state composed (5), PASS 2 done and drained (6)
     # (scripts/diag/stamp_scan.py); results unchanged
     "sc_stamp": [
-        ("vm_scan_seq.hip", "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>\n__global__ __launch_bounds__(64 * kChW)",
+        ("vm_scan_seq.hip", "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>\n__global__ __launch_bounds__(64 * kChW)",
          "__device__ unsigned long long vm_dbg_stamps[4096 * 8];\n"
          "#define VM_STAMP(K) __builtin_amdgcn_sched_barrier(0); if (PASS == 3 && threadIdx.x == 0) vm_dbg_stamps[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
-         "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR>\n__global__ __launch_bounds__(64 * kChW)"),
+         "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>\n__global__ __launch_bounds__(64 * kChW)"),
+        ("vm_scan_seq.hip", "  f2 A2[kMaxN / 2], h[kMaxN / 2];\n#pragma unroll\n  for (int q = 0; q < kMaxN / 2; ++q) {\n    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};",
+         "  VM_STAMP(7)\n  f2 A2[kMaxN / 2], h[kMaxN / 2];\n#pragma unroll\n  for (int q = 0; q < kMaxN / 2; ++q) {\n    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};"),
         ("vm_scan_seq.hip", "  const int nch = min(64, p.dim - d0);  // live channels of this group\n",
          "  const int nch = min(64, p.dim - d0);  // live channels of this group\n  VM_STAMP(0)\n"),
         ("vm_scan_seq.hip", "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n",

@@ -17,18 +17,21 @@ import torch  # noqa: E402
 from bench import scan_roofline  # noqa: E402
 
 dev = torch.device("cuda", 0)
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-r = scan_roofline(B, 20, dev, "tm")  # leaves the last launch's stamps in the array
+B = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1
+r = scan_roofline(B, 20, dev, "tm", dtp="--nodtp" not in sys.argv)  # leaves the last launch's stamps in the array
 torch.cuda.synchronize()
 lib = L.load()
 lib.vm_dbg_read_stamps.argtypes = [ctypes.c_void_p]
 buf = np.zeros(4096 * 8, dtype=np.uint64)
 assert lib.vm_dbg_read_stamps(buf.ctypes.data) == 0
-st = buf.reshape(4096, 8)[:, :7].astype(np.int64)
+st8 = buf.reshape(4096, 8).astype(np.int64)
+dtb = st8[:, 7]  # DTP: the dt block written (after stamp 1)
+st = st8[:, :7]
 live = st[:, 0] > 0
 st = st[live]
 t0 = st[:, 0].min()
 rel = (st - t0) * 10e-3
+dtrel = (dtb[live] - t0) * 10e-3
 nblk = st.shape[0]
 print(json.dumps({
     "B": B, "event_us_avg": r["avg_us"], "workgroups": int(nblk),
@@ -38,4 +41,5 @@ print(json.dumps({
     "phase_max_us": [round(float(np.max(rel[:, k + 1] - rel[:, k])), 2) for k in range(6)],
     "stamp_median_us": [round(float(np.median(rel[:, k])), 2) for k in range(7)],
     "stamp_max_us": [round(float(np.max(rel[:, k])), 2) for k in range(7)],
+    "dt_block_median_us": round(float(np.median(dtrel - rel[:, 1])), 2) if (dtb[live] > 0).all() else None,
 }), flush=True)

@@ -1040,6 +1040,36 @@ def test_linear_add_norm_bitwise_equals_linear_then_add_norm(m, n, k):
     assert not cnt.any()
 
 
+@pytest.mark.parametrize("m,n,k", [(3144, 576, 1152), (1576, 192, 384), (777, 576, 1152)])
+def test_linear_add_norm_one_launch_is_repeatable(m, n, k):
+    """The one-launch form of vm_linear_add_norm_fwd (grid <= CUs: the B = 1 out_proj shapes
+    of M and Ti): every workgroup runs a share of the next block's add + RMSNorm after its
+    tile, waiting on per-row-tile counters (sc1 hand-off).  40 launches on one counter buffer
+    are bit-identical to out_proj + vm_add_norm_fwd, finite, and leave the buffer zeroed."""
+    torch.manual_seed(m + 7)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device=DEV)
+    nw = torch.rand(n, device=DEV) + 0.5
+    h_ref = K.linear(x, w)
+    res_ref = res0.clone()
+    hn_ref = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    K.add_norm_raw(h_ref, res_ref, nw, None, hn_ref, res_ref, m, n, 1e-5, True,
+                   torch.cuda.current_stream().cuda_stream)
+    res = torch.empty_like(res0)
+    hn = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    bad = 0
+    for _ in range(40):
+        res.copy_(res0)
+        h = K.linear_add_norm(x, w, res, nw, 1e-5, hn)
+        bad += int(not (torch.equal(h, h_ref) and torch.equal(res, res_ref)
+                        and torch.equal(hn, hn_ref)))
+    torch.cuda.synchronize()
+    assert bad == 0, bad
+    cnt = K.counter_buffer(x.device, torch.cuda.current_stream().cuda_stream, 0)
+    assert not cnt.any()
+
+
 @pytest.mark.parametrize("m,n,k", [(70001, 2304, 576), (70001, 576, 1152), (4097, 2304, 576),
                                    (300, 576, 1152), (9001, 768, 192), (9001, 192, 384),
                                    (5555, 1536, 384), (5555, 384, 768), (1, 2304, 576)])

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _P = c_void_p
 _LL = c_longlong

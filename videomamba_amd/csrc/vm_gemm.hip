@@ -1,16 +1,14 @@
 // Small-M projection GEMM for the streaming-chunk latency path: out = x @ w^T (+ bias),
 // bf16 operands, fp32 accumulation on v_mfma_f32_16x16x32_bf16, bf16 out.  Replaces the
-// mixer's in_proj / out_proj nn.Linear calls (mamba_simple.py:333-339, :445-446) when the
-// token count is one clip's (B = 1: M = 3144 rows).  There the library's 256x128 tiles give
-// ~1 workgroup per CU and each walks the whole K serially (14-15 us per projection);
-// 128x128 / 64x128 tiles put 2-4 workgroups on every CU.
+// mixer's in_proj / out_proj nn.Linear calls (mamba_simple.py:333-339, :445-446) below the
+// chip-filling row counts of the persistent kernel (vm_gemm_tile.hip); at B = 1 (M = 3144
+// rows) the library's 256x128 tiles give ~1 workgroup per CU and each walks the whole K
+// serially (14-15 us per projection), 128x128 / 128x64 tiles put 1-2 on every CU.
 //
 // Layout: x (m, k) and w (n, k) both K-contiguous (the nn.Linear layouts), out (m, n).
-// A workgroup (4 waves, 2 x 2) owns a BM x 128 output tile and walks K in 64-wide steps:
-// A / W pieces are fetched two steps ahead into two register slots while the current
-// step's MFMAs run from LDS (double-buffered, one barrier per step).  The tile leaves
-// through LDS as 16-byte row stores.  Each output row's dot products run in the same order
-// whatever m is, so a row's bits do not depend on the sequence length (chunked == full).
+// Each output row's dot products run in the same order whatever m is, so a row's bits do
+// not depend on the sequence length (chunked == full).  vm_linear_add_norm_fwd runs the same
+// kernel with the next block's residual add + RMSNorm as a second phase (NORM).
 
 #include "vm_common.h"
 
@@ -28,14 +26,9 @@ struct LinParams {
 };
 
 // Fused residual add + RMSNorm of the NEXT block (videomamba.py:141-166 with
-// fused_add_norm / rms_norm / residual_in_fp32): after the GEMM, out (= h, the block's
-// output rounded to bf16) is complete for a 16-row granule once every column tile of the
-// grid has stored its part; the workgroup whose counter add comes last normalises the
-// granule:  res += h (fp32, in place);  hn = bf16(res * rsqrt(mean(res^2) + eps) * w).
-// Hand-off (MI355X_MICROARCH.md cross-workgroup table, row 1): every h store is sc1, each
-// storing wave waits vmcnt(0), a workgroup barrier, then ONE lane per granule adds to the
-// granule's counter (agent-scope atomic); the last adder's waves read h with sc1 loads after
-// a barrier.  The last adder also resets the counter, so the buffer is zero after a launch.
+// fused_add_norm / rms_norm / residual_in_fp32), phase B of linear_dma_kernel<..., NORM>:
+// res += h (fp32, in place);  hn = bf16(res * rsqrt(mean(res^2) + eps) * w), h being the
+// block's output rounded to bf16.
 struct NormTail {
   float* res;         // (m, n) fp32, row stride ldr: read and updated in place
   long long ldr;
@@ -43,10 +36,9 @@ struct NormTail {
   bf16_t* hn;         // (m, n) bf16 normalised output, row stride ldh
   long long ldh;
   float eps;
-  unsigned* cnt;      // ceil(m / 16) zeroed counters
+  unsigned* cnt;      // vm_linear_add_norm_counter_bytes(m) zeroed bytes, left zeroed
 };
-constexpr int kNormGran = 16;  // rows per hand-off granule
-constexpr int kSC1 = 16;       // buffer cache-policy bit: sc1 (agent-coherent)
+constexpr int kSC1 = 16;  // buffer cache-policy bit: sc1 (agent-coherent)
 
 __device__ __forceinline__ float lin_wave_sum(float v) {
 #pragma unroll
@@ -54,244 +46,17 @@ __device__ __forceinline__ float lin_wave_sum(float v) {
   return v;
 }
 
-constexpr int kLinBN = 128;
-constexpr int kLinBK = 64;
-constexpr int kLinPitch = 72;  // bf16 per staged row: 64 + 8 pad (144 B)
-
-template <int BM, int NK, bool NORM = false>  // NK = k / 64 K-steps, fully unrolled
-__global__ __launch_bounds__(256) void linear_kernel(const LinParams p, const NormTail q) {
-  constexpr int BN = kLinBN, BK = kLinBK, PITCH = kLinPitch;
-  constexpr int WM = BM / 2, WN = BN / 2;  // wave tile
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int KQ = BK / 8;                                      // 16-B pieces per row
-  constexpr int AP = BM * KQ / 256, BP = BN * KQ / 256;           // pieces per thread
-  constexpr int kStage = (BM + BN) * PITCH;                       // bf16 per LDS stage
-  constexpr int kOutPitch = BN + 8;
-  static_assert(BM * kOutPitch <= 2 * kStage, "output tile must fit the staging buffers");
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];   // [2][kStage]
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  constexpr int nk = NK;
-
-  // Operands come in through buffer loads: rows past m (or n) fall outside the buffer's
-  // byte range and read as 0 with no branch, so every load of a step is issued back to back
-  // and waited for only where its registers go to LDS.  Two register slots: the loads for
-  // step s are issued at the top of step s - 2 and land in LDS at the end of step s - 1.
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.x), 0, static_cast<int>((long long)p.m * p.ldx * 2), 0x00020000);
-  const auto wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.w), 0, static_cast<int>((long long)p.n * p.ldw * 2), 0x00020000);
-  typedef __attribute__((__vector_size__(4 * sizeof(int)))) int i32x4_t;
-  i32x4_t ra0[AP], rb0[BP], ra1[AP], rb1[BP];
-  auto gload = [&](int kt, i32x4_t (&a)[AP], i32x4_t (&b)[BP]) {
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int i = 0; i < AP; ++i) {
-      const int pc = tid + 256 * i, row = pc / KQ, kq = pc % KQ;
-      const int off = ((m0 + row) * static_cast<int>(p.ldx) + k0 + kq * 8) * 2;
-      a[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < BP; ++i) {
-      const int pc = tid + 256 * i, row = pc / KQ, kq = pc % KQ;
-      const int off = ((n0 + row) * static_cast<int>(p.ldw) + k0 + kq * 8) * 2;
-      b[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
-    }
-  };
-  auto lstore = [&](int buf, const i32x4_t (&a)[AP], const i32x4_t (&b)[BP]) {
-    bf16_t* sA = smem + buf * kStage;
-    bf16_t* sB = sA + BM * PITCH;
-#pragma unroll
-    for (int i = 0; i < AP; ++i) {
-      const int pc = tid + 256 * i;
-      *reinterpret_cast<i32x4_t*>(&sA[(pc / KQ) * PITCH + (pc % KQ) * 8]) = a[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BP; ++i) {
-      const int pc = tid + 256 * i;
-      *reinterpret_cast<i32x4_t*>(&sB[(pc / KQ) * PITCH + (pc % KQ) * 8]) = b[i];
-    }
-  };
-  // workgroup barrier that waits only for this wave's LDS traffic: __syncthreads() also
-  // drains vmcnt, which would collapse the two-step prefetch to zero
-  auto lds_barrier = [&]() {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const bf16_t* sA = smem + buf * kStage;
-    const bf16_t* sB = sA + BM * PITCH;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8_t af[TM], bw[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8_t*>(
-            &sA[(wm * WM + i * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bw[j] = *reinterpret_cast<const bf16x8_t*>(
-            &sB[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks * 32 + (lane >> 4) * 8]);
-      __builtin_amdgcn_sched_barrier(0);  // all fragment reads in flight before the MFMAs
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  gload(0, ra0, rb0);
-  if (nk > 1) gload(1, ra1, rb1);
-  lstore(0, ra0, rb0);
-  lds_barrier();
-#pragma unroll
-  for (int kt = 0; kt < nk; ++kt) {  // fully unrolled: slots and waits are static
-    // (sched_barrier: keep the step's loads at its top — the scheduler otherwise sinks
-    // them to the end of the step, which leaves one step of prefetch instead of two)
-    if (kt & 1) {
-      if (kt + 2 < nk) gload(kt + 2, ra1, rb1);  // slot 1 held step kt, already in LDS
-      __builtin_amdgcn_sched_barrier(0);
-      compute(1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nk) lstore(0, ra0, rb0);
-    } else {
-      if (kt + 2 < nk) gload(kt + 2, ra0, rb0);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nk) lstore(1, ra1, rb1);
-    }
-    lds_barrier();
-  }
-
-  // epilogue: D[4(lane/16) + r][lane % 16] of every 16x16 tile -> LDS -> 16-B row stores
-  // (the loop's last barrier has every wave past its final LDS reads)
-  bf16_t* sO = smem;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WN + j * 16 + (lane & 15);
-      const float b = p.bias && n0 + col < p.n ? p.bias[n0 + col] : 0.0f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        sO[row * kOutPitch + col] = from_f32<bf16_t>(acc[i][j][r] + b);
-      }
-    }
-  __syncthreads();
-  constexpr int kPieces = BM * BN / 8;
-  const auto hr = __builtin_amdgcn_make_buffer_rsrc(
-      p.out, 0, static_cast<int>((long long)p.m * p.ldo * 2), 0x00020000);
-#pragma unroll
-  for (int i = 0; i < kPieces / 256; ++i) {
-    const int pc = tid + 256 * i, row = pc / (BN / 8), cq = pc % (BN / 8);
-    const int gm = m0 + row, gn = n0 + cq * 8;
-    if (gm < p.m && gn < p.n) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
-      if constexpr (NORM) {  // agent-coherent: another workgroup normalises these rows
-        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
-        __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, hr,
-                                               (gm * static_cast<int>(p.ldo) + gn) * 2, 0, kSC1);
-      } else {
-        *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) = v;
-      }
-    }
-  }
-  if constexpr (NORM) {
-    // ---- hand-off: the last column tile of a 16-row granule normalises it ----
-    __shared__ int s_last[BM / kNormGran];
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's h stores are acknowledged
-    __syncthreads();
-    const int ntn = (p.n + BN - 1) / BN;
-    if (tid < BM / kNormGran) {
-      const int g = m0 / kNormGran + tid;
-      int last = 0;
-      if (g * kNormGran < p.m) {
-        const unsigned old =
-            __hip_atomic_fetch_add(&q.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == static_cast<unsigned>(ntn - 1);
-        if (last) __hip_atomic_store(&q.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_last[tid] = last;
-    }
-    __syncthreads();
-    // per row: vm_add_norm_fwd's RMS arithmetic and lane -> chunk map (lane*4 + 256*j), so
-    // the fused result is bit-identical to out_proj followed by vm_add_norm_fwd
-    constexpr int CPL = 4;  // n <= 1024
-#pragma unroll 1
-    for (int gi = 0; gi < BM / kNormGran; ++gi) {
-      if (!s_last[gi]) continue;
-#pragma unroll 1
-      for (int rr = 0; rr < kNormGran / 4; ++rr) {
-        const int gm = m0 + gi * kNormGran + wave * (kNormGran / 4) + rr;
-        if (gm >= p.m) break;
-        float v[CPL][4];
-        float* rrow = q.res + (long long)gm * q.ldr;
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const int c = lane * 4 + 256 * j;
-          if (c < p.n) {
-            const auto hv = __builtin_amdgcn_raw_buffer_load_b64(
-                hr, (gm * static_cast<int>(p.ldo) + c) * 2, 0, kSC1);
-            const float4 r = *reinterpret_cast<const float4*>(rrow + c);
-            v[j][0] = __uint_as_float(hv[0] << 16) + r.x;
-            v[j][1] = __uint_as_float(hv[0] & 0xffff0000u) + r.y;
-            v[j][2] = __uint_as_float(hv[1] << 16) + r.z;
-            v[j][3] = __uint_as_float(hv[1] & 0xffff0000u) + r.w;
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[j][i] = 0.0f;
-          }
-        }
-        float sq = 0.0f;
-#pragma unroll
-        for (int j = 0; j < CPL; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
-        const float rstd = rsqrtf(lin_wave_sum(sq) / p.n + q.eps);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const int c = lane * 4 + 256 * j;
-          if (c < p.n) {
-            const float4 w = *reinterpret_cast<const float4*>(q.w + c);
-            const float y0 = (v[j][0] - 0.0f) * rstd * w.x, y1 = (v[j][1] - 0.0f) * rstd * w.y;
-            const float y2 = (v[j][2] - 0.0f) * rstd * w.z, y3 = (v[j][3] - 0.0f) * rstd * w.w;
-            *reinterpret_cast<uint2*>(q.hn + (long long)gm * q.ldh + c) = uint2{
-                static_cast<uint32_t>(from_f32<bf16_t>(y0)) |
-                    (static_cast<uint32_t>(from_f32<bf16_t>(y1)) << 16),
-                static_cast<uint32_t>(from_f32<bf16_t>(y2)) |
-                    (static_cast<uint32_t>(from_f32<bf16_t>(y3)) << 16)};
-            *reinterpret_cast<float4*>(rrow + c) = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
-          }
-        }
-      }
-    }
-  }
-}
+constexpr int kLinBK = 64;  // K step
 
 // ---------------------------------------------------------------- LDS-DMA pipelined form
-// The same GEMM (same per-row K order: 64-wide steps, two 16x16x32 MFMAs per step in k
-// order, so every output row is bit-identical to linear_kernel's whatever the tile shape)
-// with the operand tiles staged global -> LDS by buffer_load ... lds (no VGPR round trip,
-// no ds_write pass) into NBUF stage buffers, NBUF - 1 steps in flight across the raw
-// s_barrier (counted vmcnt, never 0 in the loop; cdna_hip_programming.md §5 "Pipelining
-// across barriers").  linear_kernel's register ring keeps one step in flight and its
-// barrier drains vmcnt, so at B = 1 (M = 3144) each of its K steps waited out an L2 round
-// trip: in_proj (N = 2304, K = 576) ran 24.7 us against ~4 us of MFMA work.
+// Per-row K order: 64-wide steps, two 16x16x32 MFMAs per step in k order (the persistent
+// kernel's too, so every output row is bit-identical whatever the tile shape), with the
+// operand tiles staged global -> LDS by buffer_load ... lds (no VGPR round trip, no
+// ds_write pass) into NBUF stage buffers, NBUF - 1 steps in flight across the raw s_barrier
+// (counted vmcnt, never 0 in the loop; cdna_hip_programming.md §5 "Pipelining across
+// barriers").  The round-2 register ring (removed in round 5) kept one step in flight and
+// its barrier drained vmcnt, so at B = 1 (M = 3144) each of its K steps waited out an L2
+// round trip: in_proj (N = 2304, K = 576) ran 24.7 us against ~4 us of MFMA work.
 // LDS image per stage: [BM rows | BN rows] x 128 B (64 bf16 of K), 16-byte chunks
 // XOR-swizzled by (row / 2) & 7 so a 16-row fragment read touches every 16-byte slot of
 // the 256-byte bank row once; the swizzle is applied to the per-lane SOURCE address (the
@@ -310,8 +75,11 @@ __device__ __forceinline__ void dma_wait_vm_lgkm0() {
 
 // NWM = wave rows (2: 4 waves in 2 x 2; 4: 8 waves in 4 x 2, two per SIMD at one workgroup
 // per CU — a wave's MFMA / LDS-read latency then has a partner to hide behind)
-template <int BM, int BN, int NK, int NBUF, int NWM = 2>
-__global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p) {
+// NORM (vm_linear_add_norm_fwd, round 5): after its tile the workgroup also runs the next
+// block's residual add + RMSNorm for a share of the rows (see the phase-B comment below);
+// the host launches it only when the whole grid is co-resident (grid <= CUs).
+template <int BM, int BN, int NK, int NBUF, int NWM = 2, bool NORM = false>
+__global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p, const NormTail q) {
   constexpr int R = kDmaRow;
   constexpr int NW = 2 * NWM;     // waves
   constexpr int NT = 64 * NW;     // threads
@@ -339,6 +107,36 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
   const int xcd = h & 7, qq = nwg >> 3, rr = nwg & 7;
   const int l = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);
   const int m0 = (l / ntn) * BM, n0 = (l % ntn) * BN;
+
+  // NORM phase-B operands that no workgroup of this launch writes — the residual rows this
+  // wave normalises and the norm weight — are loaded now and held across the GEMM
+  constexpr int kNR = NORM ? 2 : 1;  // rows per wave in phase B
+  constexpr int kNC = 4;             // 4-column chunks per lane (n <= 1024)
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float nv4f;
+  nv4f nres[kNR][kNC], nw[kNC];
+  const int rpw = NORM ? (p.m + nwg - 1) / nwg : 0;  // rows per workgroup in phase B
+  const int nrow0 = l * rpw + wave * kNR;            // this wave's first row (group 0)
+  auto ncol = [&](int j, int es) {  // byte offset of chunk j of a row (out of range past n)
+    int o = lane * 4 + 256 * j < p.n ? (lane * 4 + 256 * j) * es : 0x7ffffff0;
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  if constexpr (NORM) {
+    const auto wq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.w), 0, p.n * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < kNC; ++j)
+      nw[j] = __builtin_bit_cast(nv4f, __builtin_amdgcn_raw_buffer_load_b128(wq, ncol(j, 4), 0, 0));
+#pragma unroll
+    for (int r = 0; r < kNR; ++r) {
+      const int row = nrow0 + r;
+      const bool live = wave * kNR + r < rpw && row < p.m;  // group 0
+      const auto rq = __builtin_amdgcn_make_buffer_rsrc(
+          q.res + (long long)(live ? row : 0) * q.ldr, 0, live ? p.n * 4 : 0, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < kNC; ++j)
+        nres[r][j] = __builtin_bit_cast(nv4f, __builtin_amdgcn_raw_buffer_load_b128(rq, ncol(j, 4), 0, 0));
+    }
+  }
 
   const auto xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(p.x), 0, static_cast<int>((long long)p.m * p.ldx * 2), 0x00020000);
@@ -441,22 +239,163 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
     }
   __syncthreads();
   constexpr int kPieces = BM * BN / 8;
+  const auto hr = __builtin_amdgcn_make_buffer_rsrc(
+      p.out, 0, static_cast<int>((long long)p.m * p.ldo * 2), 0x00020000);
 #pragma unroll
   for (int i = 0; i < (kPieces + NT - 1) / NT; ++i) {
     const int pc = tid + NT * i;
     if (kPieces % NT != 0 && pc >= kPieces) break;
     const int row = pc / (BN / 8), cq = pc % (BN / 8);
     const int gm = m0 + row, gn = n0 + cq * 8;
-    if (gm < p.m && gn < p.n)
-      *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) =
-          *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+    if (gm < p.m && gn < p.n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&sO[row * kOutPitch + cq * 8]);
+      if constexpr (NORM) {  // agent-coherent: other workgroups read these rows in phase B
+        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+        __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, hr,
+                                               (gm * static_cast<int>(p.ldo) + gn) * 2, 0, kSC1);
+      } else {
+        *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) = v;
+      }
+    }
+  }
+  if constexpr (NORM) {
+    // ---- phase B: the next block's add + RMSNorm, spread over every workgroup ----
+    // Workgroup l normalises rows [l * rpw, (l + 1) * rpw) (one wave per row, kNR rows per
+    // wave), which the ntn column tiles of at most two BM-row tiles produced.  Hand-off
+    // (MI355X_MICROARCH.md cross-workgroup table, row 1): every h store above is sc1; each
+    // storing wave waits vmcnt(0), a workgroup barrier, then ONE lane adds to the row tile's
+    // counter (agent-scope atomic); a consumer's lane 0 polls the counters of the row tiles
+    // it needs with sc1 loads until each reaches ntn, a workgroup barrier, then every h load
+    // is an sc1 load.  The consumers of a row tile count themselves in a second counter; the
+    // last one resets both, so the buffer is zero again after the launch (graph replays).
+    // The whole grid is co-resident (host check), so a poll never waits on an undispatched
+    // producer; it is bounded anyway: a timeout sets the error word and makes the rows NaN.
+    unsigned* err = q.cnt;
+    unsigned* tcnt = q.cnt + 16;
+    const int nmt = (p.m + BM - 1) / BM;
+    unsigned* ccnt = tcnt + nmt;
+    // (the flag lives in the dynamic LDS, free after the stores: a second __shared__ object
+    // beside the DMA stage buffers can make hipcc drain vmcnt before every K-step's reads)
+    int& s_ok = *reinterpret_cast<int*>(dsm);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's h stores are acknowledged
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&tcnt[m0 / BM], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int r_lo = l * rpw, r_hi = min(p.m, r_lo + rpw);
+    if (r_lo >= r_hi) return;  // uniform: no rows for this workgroup
+    if (tid == 0) {
+      int ok = 1;
+      for (int mt = r_lo / BM; mt <= (r_hi - 1) / BM; ++mt) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(&tcnt[mt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               static_cast<unsigned>(ntn)) {
+          if (++spins >= (1u << 20)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      s_ok = ok;
+    }
+    __syncthreads();
+    const bool ok = s_ok != 0;
+    // per row: vm_add_norm_fwd's add_rms_bf16_kernel arithmetic and lane -> chunk map
+    // (lane * 4 + 256 j; chunks past n read 0 and add nothing), so the fused result is
+    // bit-identical to out_proj followed by vm_add_norm_fwd.  Rows go in groups of
+    // NW * kNR (one row per wave and r); the first group's residual rows came in at the
+    // kernel start, later groups' (small grids only) are loaded here.
+#pragma unroll 1
+    for (int g0 = 0; g0 < rpw; g0 += NW * kNR) {
+      if (g0 > 0) {
+#pragma unroll
+        for (int r = 0; r < kNR; ++r) {
+          const int row = nrow0 + g0 + r;
+          const bool live = g0 + wave * kNR + r < rpw && row < p.m;
+          const auto rq = __builtin_amdgcn_make_buffer_rsrc(
+              q.res + (long long)(live ? row : 0) * q.ldr, 0, live ? p.n * 4 : 0, 0x00020000);
+#pragma unroll
+          for (int j = 0; j < kNC; ++j)
+            nres[r][j] = __builtin_bit_cast(nv4f, __builtin_amdgcn_raw_buffer_load_b128(rq, ncol(j, 4), 0, 0));
+        }
+      }
+      uint32_t hq[kNR][kNC][2];
+#pragma unroll
+      for (int r = 0; r < kNR; ++r) {
+        const int row = nrow0 + g0 + r;
+        const bool live = g0 + wave * kNR + r < rpw && row < p.m;
+        const auto hq_r = __builtin_amdgcn_make_buffer_rsrc(
+            p.out + (long long)(live ? row : 0) * p.ldo, 0, live ? p.n * 2 : 0, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hq_r, ncol(j, 2), 0, kSC1);
+          hq[r][j][0] = v[0];
+          hq[r][j][1] = v[1];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every h load of the wave's rows in flight first
+#pragma unroll
+      for (int r = 0; r < kNR; ++r) {
+        const int row = nrow0 + g0 + r;
+        const bool live = g0 + wave * kNR + r < rpw && row < p.m;
+        float v[kNC][4];
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+          v[j][0] = __uint_as_float(hq[r][j][0] << 16) + nres[r][j][0];
+          v[j][1] = __uint_as_float(hq[r][j][0] & 0xffff0000u) + nres[r][j][1];
+          v[j][2] = __uint_as_float(hq[r][j][1] << 16) + nres[r][j][2];
+          v[j][3] = __uint_as_float(hq[r][j][1] & 0xffff0000u) + nres[r][j][3];
+        }
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
+        float rstd = rsqrtf(lin_wave_sum(sq) / p.n + q.eps);
+        if (!ok) rstd = __builtin_nanf("");
+        const auto hn_r = __builtin_amdgcn_make_buffer_rsrc(
+            q.hn + (long long)(live ? row : 0) * q.ldh, 0, live ? p.n * 2 : 0, 0x00020000);
+        const auto ro_r = __builtin_amdgcn_make_buffer_rsrc(
+            q.res + (long long)(live ? row : 0) * q.ldr, 0, live ? p.n * 4 : 0, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+          float y[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[i] = (v[j][i] - 0.0f) * rstd * nw[j][i];
+          typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
+          const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
+                                           (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
+                          static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
+                                           (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
+          __builtin_amdgcn_raw_buffer_store_b64(o2, hn_r, ncol(j, 2), 0, 0);
+          typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+          const v4i r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
+                          static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
+          __builtin_amdgcn_raw_buffer_store_b128(r4, ro_r, ncol(j, 4), 0, 0);
+        }
+      }
+    }
+    // count this workgroup out of the row tiles it read; the last consumer of a tile resets
+    // both of its counters (every producer has added: the poll saw ntn)
+    if (tid == 0) {
+      for (int mt = r_lo / BM; mt <= (r_hi - 1) / BM; ++mt) {
+        const int first = (mt * BM) / rpw;
+        const int last = min((min(mt * BM + BM, p.m) - 1) / rpw, nwg - 1);
+        const unsigned old =
+            __hip_atomic_fetch_add(&ccnt[mt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == static_cast<unsigned>(last - first)) {
+          __hip_atomic_store(&tcnt[mt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ccnt[mt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
   }
 }
 
 // Tile choice for the pipelined form (row bits do not depend on it), measured at the B = 1
 // chunk shapes (scripts/diag/variant_linear.py): wide outputs (in_proj, N = 2 * d_inner)
 // on 128 x 128 tiles with two stage buffers (64 KB: two workgroups per CU; 14.1 us against
-// 17.6 for linear_kernel, three buffers 16.3), eight waves each since round 4 (four per
+// 17.6 for the register ring, three buffers 16.3), eight waves each since round 4 (four per
 // SIMD with the second workgroup: 13.2 against 14.3-14.7 us, B = 2 21.9 against 22.9;
 // 256 x 128 / 128 x 256 tiles at one workgroup per CU, 8 or 16 waves, 14.2-14.3 us;
 // profiles/r04x_linear_waves.jsonl); narrow ones (out_proj, N = d_model) on 128 x 64
@@ -476,7 +415,7 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
 #define VM_LDMA_K(BMV, BNV, NBV, NWMV, NKV)                                                    \
   case NKV:                                                                                    \
     hipLaunchKernelGGL((linear_dma_kernel<BMV, BNV, NKV, NBV, NWMV>), grid, dim3(128 * NWMV), \
-                       lds, s, p);                                                             \
+                       lds, s, p, NormTail{});                                                 \
     break;
 static void linear_dma_launch(const LinParams& p, hipStream_t s) {
   if (p.n >= 1024) VM_LDMA_TILE(128, 128, 2, 4)
@@ -585,8 +524,10 @@ extern "C" int vm_linear_fwd_form(const void* x, long long ldx, const void* w, l
   return vmhost::launch_status("vm_linear_fwd");
 }
 
+// Counter buffer of vm_linear_add_norm_fwd: an error word (+ pad) and two counters per
+// 128-row tile (producers, consumers).
 extern "C" long long vm_linear_add_norm_counter_bytes(int m) {
-  return m <= 0 ? 0 : static_cast<long long>((m + kNormGran - 1) / kNormGran) * sizeof(unsigned);
+  return m <= 0 ? 0 : static_cast<long long>(16 + 2 * ((m + 127) / 128)) * sizeof(unsigned);
 }
 
 extern "C" int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* w, long long ldw,
@@ -603,36 +544,58 @@ extern "C" int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* 
       !vmhost::aligned16(x) || !vmhost::aligned16(w) || !vmhost::aligned16(h) ||
       !vmhost::aligned16(residual) || !vmhost::aligned16(norm_weight) || !vmhost::aligned16(hn) ||
       (long long)m * ldx * 2 >= (1ll << 31) || (long long)n * ldw * 2 >= (1ll << 31) ||
-      (long long)m * ldo * 2 >= (1ll << 31) ||
+      (long long)m * ldo * 2 >= (1ll << 31) || (long long)m * ldr * 4 >= (1ll << 31) ||
       counter_bytes < vm_linear_add_norm_counter_bytes(m)) {
     vmhost::set_error("vm_linear_add_norm_fwd: bf16 x / w / h / hn, fp32 residual and weight; "
                       "k a multiple of 64, n a multiple of 8 and <= 1024, 16-byte aligned "
                       "rows under 2 GB, vm_linear_add_norm_counter_bytes(m) zeroed counters");
     return VM_E_INVALID;
   }
-  if (m == 0) return VM_OK;
-  LinParams p{};
-  p.x = static_cast<const bf16_t*>(x); p.ldx = ldx;
-  p.w = static_cast<const bf16_t*>(w); p.ldw = ldw;
-  p.bias = nullptr; p.out = static_cast<bf16_t*>(h); p.ldo = ldo;
-  p.m = m; p.n = n; p.k = k;
-  NormTail q{};
-  q.res = residual; q.ldr = ldr; q.w = norm_weight; q.hn = static_cast<bf16_t*>(hn); q.ldh = ldh;
-  q.eps = eps; q.cnt = static_cast<unsigned*>(counters);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid((m + 63) / 64, (n + kLinBN - 1) / kLinBN);
-  const size_t lds = 2 * (64 + kLinBN) * kLinPitch * sizeof(bf16_t);
   switch (k / kLinBK) {
-#define VM_LIN(NKV)                                                                   \
-  case NKV:                                                                           \
-    hipLaunchKernelGGL((linear_kernel<64, NKV, true>), grid, dim3(256), lds, s, p, q); \
-    break;
-    VM_LIN(3) VM_LIN(6) VM_LIN(9) VM_LIN(12) VM_LIN(18) VM_LIN(24)
-#undef VM_LIN
+    case 3: case 6: case 9: case 12: case 18: case 24: break;
     default:
       vmhost::set_error("vm_linear_add_norm_fwd: k = %d (supported: 192, 384, 576, 768, 1152, "
                         "1536)", k);
       return VM_E_INVALID;
   }
-  return vmhost::launch_status("vm_linear_add_norm_fwd");
+  if (m == 0) return VM_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // one launch when the whole 128 x 64-tile grid is co-resident at one workgroup per CU
+  constexpr int BM = 128, BN = 64;
+  const long long nwg = static_cast<long long>((m + BM - 1) / BM) * ((n + BN - 1) / BN);
+  const int cus = device_cus(s);
+  if (cus > 0 && nwg <= cus) {
+    LinParams p{};
+    p.x = static_cast<const bf16_t*>(x); p.ldx = ldx;
+    p.w = static_cast<const bf16_t*>(w); p.ldw = ldw;
+    p.bias = nullptr; p.out = static_cast<bf16_t*>(h); p.ldo = ldo;
+    p.m = m; p.n = n; p.k = k;
+    NormTail q{};
+    q.res = residual; q.ldr = ldr; q.w = norm_weight; q.hn = static_cast<bf16_t*>(hn); q.ldh = ldh;
+    q.eps = eps; q.cnt = static_cast<unsigned*>(counters);
+    const dim3 grid((m + BM - 1) / BM, (n + BN - 1) / BN);
+    // 3 stage buffers = 72 KB; 96 KB requested so a CU holds one workgroup (the validated
+    // one-per-CU form of the hand-off)
+    const size_t lds = 96 * 1024;
+    switch (k / kLinBK) {
+#define VM_LN(NKV)                                                                               \
+  case NKV:                                                                                      \
+    hipLaunchKernelGGL((linear_dma_kernel<BM, BN, NKV, 3, 4, true>), grid, dim3(512), lds, s, p, q); \
+    break;
+      VM_LN(3) VM_LN(6) VM_LN(9) VM_LN(12) VM_LN(18) VM_LN(24)
+#undef VM_LN
+      default: break;
+    }
+    return vmhost::launch_status("vm_linear_add_norm_fwd");
+  }
+  // otherwise the two launches it replaces (the same kernels: bit-identical either way)
+  if (ldo != n || ldr != n || ldh != n) {
+    vmhost::set_error("vm_linear_add_norm_fwd: a grid past the CU count runs the separate "
+                      "kernels, which need contiguous h / residual / hn rows");
+    return VM_E_INVALID;
+  }
+  int rc = vm_linear_fwd_form(x, ldx, w, ldw, nullptr, h, ldo, m, n, k, VM_DTYPE_BF16, 0, stream);
+  if (rc != VM_OK) return rc;
+  return vm_add_norm_fwd(h, VM_DTYPE_BF16, residual, VM_DTYPE_F32, norm_weight, nullptr, hn,
+                         VM_DTYPE_BF16, residual, VM_DTYPE_F32, m, n, eps, 1, stream);
 }
