@@ -231,8 +231,8 @@ VARIANTS = {
          "    VM_STAMP(3)\n    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)"),
         ("vm_scan_seq.hip", "    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----\n    // Wave w",
          "    VM_STAMP(4)\n    // ---- walk the preceding blocks' aggregates from h0 to this block's entry ----\n    // Wave w"),
-        ("vm_scan_seq.hip", "    run_steps(BoolTag<true>{});\n    finish();\n  }\n}",
-         "    VM_STAMP(5)\n    run_steps(BoolTag<true>{});\n    finish();\n    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    VM_STAMP(6)\n  }\n}"),
+        ("vm_scan_seq.hip", "    run_steps(BoolTag<true>{});\n    finish();\n    if (tid == 0) {  // count this block out",
+         "    VM_STAMP(5)\n    run_steps(BoolTag<true>{});\n    finish();\n    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    VM_STAMP(6)\n    if (tid == 0) {  // count this block out"),
         ("vm_scan_seq.hip", "bool seq_supported(const ScanParams& p, int dtype) {",
          "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
          "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"

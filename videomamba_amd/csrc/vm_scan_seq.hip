@@ -993,14 +993,26 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // touched ~32 cache lines per wave-instruction, and with 8 waves each issuing ~80 of them
   // the address path, not the memory, set the kernel's start-up time at B = 1.
   //   A: the group's 64 x N floats are contiguous — 2 coalesced dwords per thread
+  // Every start-up load is a buffer load whose range ends where its operand does (0 bytes
+  // for an absent one), so none sits behind a branch: hipcc waits vmcnt(0) at the join of
+  // a "load or zero" branch, and round 4's form paid five dependent round trips here.
   float aval[kChSPW];
+  {
+    const auto ar = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(ps.A + static_cast<long long>(d0) * N), 0, nch * N * 4, 0x00020000);
 #pragma unroll
-  for (int k = 0; k < kChSPW; ++k) {
-    const int e = tid + k * 64 * kChW;  // element of the [64][N] tile
-    aval[k] = e < nch * N ? ps.A[static_cast<long long>(d0) * N + e] : 0.0f;
+    for (int k = 0; k < kChSPW; ++k) {
+      const int e = tid + k * 64 * kChW;  // element of the [64][N] tile
+      aval[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ar, e * 4, 0, 0));
+    }
   }
-  const float Dv = (ps.D ? ps.D[d] : 0.0f) * kLog2e;
-  const float bias = (ps.dbias ? ps.dbias[d] : 0.0f) * kLog2e;
+  auto vec_load = [&](const float* v) {  // v[d], 0 when v is null
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(v), 0, v ? p.dim * 4 : 0,
+                                                     0x00020000);
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, d * 4, 0, 0));
+  };
+  const float Dv = vec_load(ps.D) * kLog2e;
+  const float bias = vec_load(ps.dbias) * kLog2e;
   // states this wave composes across segments / blocks: kChSPW * wave (+ 1)
   const int n0 = kChSPW * wave;
 
@@ -1020,10 +1032,23 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   agv_t agH[kCW];
   float agS[kCW * 64 / (64 * kChW)];
   if constexpr (PASS == 3) {
-    if (ps.h0) {
+    // h0 (fp32 or bf16): both forms issued, the absent one over a 0-byte range
+    const bool h32 = ps.h0 && p.h0_dtype != VM_DTYPE_BF16, h16 = ps.h0 && p.h0_dtype == VM_DTYPE_BF16;
+    const long long hrow = static_cast<long long>(ps.hb) * p.h0_sb;
+    const int hspan = static_cast<int>((p.dim - 1) * p.h0_sd + N);  // elements of the row
+    const auto hr32 = __builtin_amdgcn_make_buffer_rsrc(
+        h32 ? const_cast<float*>(static_cast<const float*>(ps.h0) + hrow) : nullptr, 0,
+        h32 ? hspan * 4 : 0, 0x00020000);
+    const auto hr16 = __builtin_amdgcn_make_buffer_rsrc(
+        h16 ? const_cast<bf16_t*>(static_cast<const bf16_t*>(ps.h0) + hrow) : nullptr, 0,
+        h16 ? hspan * 2 : 0, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < kChSPW; ++i)
-        if (n0 + i < N) Hs[i] = load_dyn(ps.h0, ps.hb * p.h0_sb + d * p.h0_sd + n0 + i, p.h0_dtype);
+    for (int i = 0; i < kChSPW; ++i) {
+      int el = n0 + i < N ? static_cast<int>(d * p.h0_sd) + n0 + i : 0x1ffffff0;
+      asm volatile("" : "+v"(el));  // a select, not a branch around the loads
+      const float v32 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(hr32, el * 4, 0, 0));
+      const uint32_t v16 = __builtin_amdgcn_raw_buffer_load_b16(hr16, el * 2, 0, 0);
+      Hs[i] = __uint_as_float(v16 << 16) + v32;  // one of the two read 0 (no select to sink into)
     }
   }
   if constexpr (PASS == 2) {
@@ -1091,6 +1116,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // Warm this XCD's L2 with the block's B / C rows (one dword per 128-byte line, issued with
   // the start-up loads): the per-step scalar row loads, one step ahead, then hit L2 instead
   // of paying an infinity-cache / HBM round trip every step.
+  uint32_t warm[2] = {0u, 0u};
   {
     const int bt0 = blk * kChW * w.T;
     const int bt1 = min(L, bt0 + kChW * w.T);
@@ -1098,17 +1124,16 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       const char* base = reinterpret_cast<const char*>(Bq) + static_cast<long long>(bt0) * bsl;
       const int span = (bt1 - bt0 - 1) * static_cast<int>(bsl) + 2 * kMaxN * ES;
       const int line = static_cast<int>(threadIdx.x) * 128;
-      if (line < span) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(base + line);
-        asm volatile("" ::"v"(v));
-      }
+      // (the loads' values are consumed only after the start-up wait below: a consumer here
+      // made hipcc wait for each warm-up load on the spot)
+      const auto wr0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, span, 0x00020000);
+      warm[0] = __builtin_amdgcn_raw_buffer_load_b32(wr0, line, 0, 0);
       if constexpr (!BC1) {
         const char* cb = reinterpret_cast<const char*>(Cq) + static_cast<long long>(bt0) * csl;
         const int cspan = (bt1 - bt0 - 1) * static_cast<int>(csl) + kMaxN * ES;
-        if (PASS != 1 && line < cspan) {
-          const uint32_t v = *reinterpret_cast<const uint32_t*>(cb + line);
-          asm volatile("" ::"v"(v));
-        }
+        const auto wr1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb), 0,
+                                                           PASS != 1 ? cspan : 0, 0x00020000);
+        warm[1] = __builtin_amdgcn_raw_buffer_load_b32(wr1, line, 0, 0);
       }
     }
   }
@@ -1125,41 +1150,40 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // DTP: the group's W_dt rows into LDS (16-byte pieces; rows past dim read 0)
+  // DTP: the group's W_dt rows (64 x r_pad <= 64 x 64 bf16: one 16-byte piece per thread;
+  // rows past dim read 0), written to LDS after the start-up wait
+  typedef __attribute__((ext_vector_type(4))) unsigned wv4;
+  wv4 wdt_piece = {0u, 0u, 0u, 0u};
+  const int wdt_ppr = DTP ? q.wdt_ld >> 3 : 1;  // pieces per row (r_pad 32 or 64)
+  static_assert(64 * 8 <= 64 * kChW, "one W_dt piece per thread");
   if constexpr (DTP) {
-    const int rp = q.wdt_ld;  // r_pad: 32 or 64
-    const int ppr = rp >> 3;  // pieces per row
+    const int rp = q.wdt_ld;
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(q.wdt + static_cast<long long>(d0) * rp), 0, nch * rp * 2, 0x00020000);
-    for (int i = tid; i < 64 * ppr; i += 64 * kChW) {
-      const int row = i / ppr, pc = i - row * ppr;
-      typedef __attribute__((ext_vector_type(4))) unsigned wv4;
-      const wv4 v = __builtin_bit_cast(
-          wv4, __builtin_amdgcn_raw_buffer_load_b128(wr, (row * rp + pc * 8) * 2, 0, 0));
-      *reinterpret_cast<wv4*>(&sWd[row * kChDtpWPitch + pc * 8]) = v;
-    }
+    const int row = tid / wdt_ppr, pc = tid - row * wdt_ppr;
+    int off = tid < 64 * wdt_ppr ? (row * rp + pc * 8) * 2 : 0x7ffffff0;
+    asm volatile("" : "+v"(off));
+    wdt_piece = __builtin_bit_cast(wv4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
   }
-  // one wait for every start-up load (parameters, entry operands, prologue): left pending
-  // they would merge into the step loop's header waits
+  // This launch's hand-off tag (PASS 3): the buffer's epoch + 1 (never 0, the zeroed
+  // buffer's value).  Every block reads the epoch here, with the start-up loads, and adds
+  // itself to `done` at its very end; the block that completes the count (so every block
+  // has read the epoch) resets the count and advances the epoch for the next launch.  Tags
+  // only grow over a buffer's launches, so granules left by an earlier launch — of any
+  // shape — never match (until 2^32 - 1 launches wrap).  (Round 4 counted itself in here,
+  // before PASS 1: two dependent agent-scope round trips on every block's start-up path.)
+  unsigned ep = 0;
+  if constexpr (PASS == 3)  // (every thread: a tid == 0 branch would wait at its join)
+    ep = __hip_atomic_load(w.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // one wait for every start-up load (parameters, entry operands, prologue, the epoch): left
+  // pending they would merge into the step loop's header waits
   __builtin_amdgcn_s_waitcnt(0);
-  if constexpr (PASS == 3) {
-    // This launch's hand-off tag: the buffer's epoch + 1 (never 0, the zeroed buffer's
-    // value).  Every block reads the epoch before adding itself to `done`; the block that
-    // completes the count (so every block has read it) resets the count and advances the
-    // epoch for the next launch.  Tags only grow over a buffer's launches, so granules left
-    // by an earlier launch — of any shape — never match (until 2^32 - 1 launches wrap).
-    if (tid == 0) {
-      const unsigned ep = __hip_atomic_load(w.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned tag = ep + 1u == 0u ? 1u : ep + 1u;
-      s_tag = tag;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the read completes before the count
-      const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
-      if (__hip_atomic_fetch_add(w.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
-        __hip_atomic_store(w.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(w.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+  asm volatile("" ::"v"(warm[0]), "v"(warm[1]));  // the L2 warm-up loads are not dead
+  if constexpr (DTP) {
+    const int row = tid / wdt_ppr, pc = tid - row * wdt_ppr;
+    if (tid < 64 * wdt_ppr) *reinterpret_cast<wv4*>(&sWd[row * kChDtpWPitch + pc * 8]) = wdt_piece;
   }
+  if (PASS == 3 && tid == 0) s_tag = ep + 1u == 0u ? 1u : ep + 1u;
   // A transposed into LDS: sA[n][c] (zero for n >= N and for channels past dim)
 #pragma unroll
   for (int k = 0; k < kChSPW; ++k) {
@@ -1531,6 +1555,13 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     }
     run_steps(BoolTag<true>{});
     finish();
+    if (tid == 0) {  // count this block out (its epoch read completed at the start-up wait)
+      const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+      if (__hip_atomic_fetch_add(w.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
+        __hip_atomic_store(w.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w.epoch, s_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
