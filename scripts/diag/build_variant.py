@@ -238,6 +238,26 @@ VARIANTS = {
          "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
          "namespace vm {\nbool seq_supported(const ScanParams& p, int dtype) {"),
     ],
+    # per-WAVE timestamps of the one-launch chunked scan (lane 0 of each wave, s_memrealtime):
+    # 0 start-up wait passed, 1 dt block + A2 ready, 2 PASS 1 loop done, 3 after the
+    # compose barrier + granule stores (scripts/diag/stamp_scan_waves.py); results unchanged
+    "sc_stampw": [
+        ("vm_scan_seq.hip", "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>\n__global__ __launch_bounds__(64 * kChW)",
+         "__device__ unsigned long long vm_dbg_stamps[4096 * 8 * 4];\n"
+         "#define VM_STAMPW(K) __builtin_amdgcn_sched_barrier(0); if (PASS == 3 && (threadIdx.x & 63) == 0) vm_dbg_stamps[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + (threadIdx.x >> 6)) * 4 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0);\n"
+         "template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>\n__global__ __launch_bounds__(64 * kChW)"),
+        ("vm_scan_seq.hip", '  asm volatile("" ::"v"(warm[0]), "v"(warm[1]));  // the L2 warm-up loads are not dead',
+         '  asm volatile("" ::"v"(warm[0]), "v"(warm[1]));  // the L2 warm-up loads are not dead\n  VM_STAMPW(0)'),
+        ("vm_scan_seq.hip", "  f2 A2[kMaxN / 2], h[kMaxN / 2];\n#pragma unroll\n  for (int q = 0; q < kMaxN / 2; ++q) {\n    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};",
+         "  VM_STAMPW(1)\n  f2 A2[kMaxN / 2], h[kMaxN / 2];\n#pragma unroll\n  for (int q = 0; q < kMaxN / 2; ++q) {\n    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};"),
+        ("vm_scan_seq.hip", "  run_steps(BoolTag<false>{});\n", "  run_steps(BoolTag<false>{});\n  VM_STAMPW(2)\n"),
+        ("vm_scan_seq.hip", "    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)",
+         "    VM_STAMPW(3)\n    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)"),
+        ("vm_scan_seq.hip", "bool seq_supported(const ScanParams& p, int dtype) {",
+         "}  // namespace vm\nextern \"C\" int vm_dbg_read_stamps(void* dst) {\n"
+         "  return static_cast<int>(hipMemcpyFromSymbol(dst, HIP_SYMBOL(vm::vm_dbg_stamps), sizeof(vm::vm_dbg_stamps)));\n}\n"
+         "namespace vm {\nbool seq_supported(const ScanParams& p, int dtype) {"),
+    ],
     # per-wave phase timestamps of the fused small-batch conv_proj (lane 0 of every wave):
     # entry (0), conv done (1), W_x 2-3 issued (2), u LDS tile written (3), x_proj MFMAs
     # retired (4), u rows stored (5), W_dt issued (6), barrier passed (7)
@@ -271,11 +291,17 @@ VARIANTS = {
 }
 
 
-def build(name):
+def build(name, rev=None):
     src = os.path.join(ROOT, "videomamba_amd", "csrc")
     work = os.path.join(ROOT, "build", "var", name, "src", "csrc")  # ../../include resolves
     shutil.rmtree(work, ignore_errors=True)
     shutil.copytree(src, work)
+    if rev:  # the csrc sources of a git revision (e.g. HEAD: the committed baseline)
+        for f in os.listdir(work):
+            blob = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:videomamba_amd/csrc/{f}"],
+                                  capture_output=True)
+            if blob.returncode == 0:
+                open(os.path.join(work, f), "wb").write(blob.stdout)
     inc = os.path.join(ROOT, "build", "var", name, "include")
     shutil.rmtree(inc, ignore_errors=True)
     shutil.copytree(os.path.join(ROOT, "include"), inc)
@@ -291,5 +317,12 @@ def build(name):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:]:
-        build(n)
+    # python build_variant.py name...            variants of the working-tree sources
+    # python build_variant.py --rev REV name     the sources of git revision REV (as "name")
+    args = sys.argv[1:]
+    if args and args[0] == "--rev":
+        VARIANTS.setdefault(args[2], [])
+        build(args[2], rev=args[1])
+    else:
+        for n in args:
+            build(n)

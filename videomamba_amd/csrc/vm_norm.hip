@@ -57,17 +57,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base
   void* ub = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(ub, 0, bytes, 0x00020000);
 }
+// (no early exit for the rows past the end: their buffers have 0-byte ranges, so every
+// access is a no-op, and the kernel-argument loads are not split by a branch into two
+// dependent rounds before the first global load)
 template <int CPL, bool RES, bool RO>
 __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= p.rows) return;
+  const long long row0 = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool live = row0 < p.rows;
+  const long long row = live ? row0 : 0;
   const int lane = threadIdx.x & 63;
   const long long base = row * p.cols;
-  const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, p.cols * 2);
-  const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, p.cols * 4);
+  const int cb2 = live ? p.cols * 2 : 0, cb4 = live ? p.cols * 4 : 0;
+  const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, cb2);
+  const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, cb4);
   const auto wr = norm_row_rsrc(p.w, p.cols * 4);
-  const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, p.cols * 2);
-  const auto ror = norm_row_rsrc(RO ? static_cast<float*>(p.res_out) + base : p.w, p.cols * 4);
+  const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, cb2);
+  const auto ror = norm_row_rsrc(RO ? static_cast<float*>(p.res_out) + base : p.w, cb4);
   typedef __attribute__((__vector_size__(4 * sizeof(float)))) float v4f;
   auto off = [&](int j, int es) {
     int o = lane * 4 + 256 * j < p.cols ? (lane * 4 + 256 * j) * es : kNormOut;
