@@ -64,6 +64,14 @@ VARIANTS = {
                    "    if (i < 72 * 16 && tok >= 0 && tok < q.ntok && qd * 8 < nch && tok0 < 0)")],
     # persistent GEMM: s_setprio around each MFMA quadrant (tg_prio1) / waves 4-7 at
     # priority 1 throughout (tg_prio2)
+    # persistent out_proj + add + RMSNorm (vm_gemm_tile.hip NORM) pricing: no norm rows
+    # (polls / barriers / hand-off kept; results wrong), 4 rows in flight per wave, h read
+    # back without sc1 (timing only)
+    "tn_nonorm": [("vm_gemm_tile.hip", "    for (int g = 0; g < RPW; g += kTileNormRows) {",
+                   "    for (int g = 0; g < 0; g += kTileNormRows) {")],
+    "tn_rows4": [("vm_gemm_tile.hip", "constexpr int kTileNormRows = 8;", "constexpr int kTileNormRows = 4;")],
+    "tn_plainh": [("vm_gemm_tile.hip", "          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hr, c2[j] + oh, 0, kTileSC1);",
+                   "          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hr, c2[j] + oh, 0, 0);")],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",

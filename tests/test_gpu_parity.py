@@ -1070,6 +1070,43 @@ def test_linear_add_norm_one_launch_is_repeatable(m, n, k):
     assert not cnt.any()
 
 
+@pytest.mark.parametrize("m,n,k,reps", [(40000, 576, 1152, 20), (100001, 192, 384, 5),
+                                        (50003, 384, 768, 5), (1408512, 576, 1152, 4)])
+def test_persistent_linear_add_norm_bitwise_and_repeatable(m, n, k, reps):
+    """vm_linear_add_norm_fwd at chip-filling row counts: the persistent tile GEMM with the
+    next block's add + RMSNorm run per 256-row block by the workgroup of its last column tile
+    after the other column tiles' producers count in (vm_gemm_tile.hip NORM).  Every launch
+    is bit-identical to the persistent out_proj followed by vm_add_norm_fwd (h, the fp32
+    residual updated in place, the normalised rows) and leaves the counters zeroed.  Shapes:
+    ragged row blocks for VideoMamba-M / Ti / S out_proj, and the bench's B = 448 out_proj
+    (1,408,512 rows: x and the residual past 2 GB)."""
+    torch.manual_seed(m + n)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device=DEV)
+    nw = torch.rand(n, device=DEV) + 0.5
+    h_ref = K.linear(x, w)
+    res_ref = res0.clone()
+    hn_ref = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    K.add_norm_raw(h_ref, res_ref, nw, None, hn_ref, res_ref, m, n, 1e-5, True,
+                   torch.cuda.current_stream().cuda_stream)
+    res = torch.empty_like(res0)
+    hn = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    h = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+    bad = 0
+    for _ in range(reps):
+        res.copy_(res0)
+        hn.fill_(0)
+        K.linear_add_norm(x, w, res, nw, 1e-5, hn, h=h)
+        bad += int(not (torch.equal(h, h_ref) and torch.equal(res, res_ref)
+                        and torch.equal(hn, hn_ref)))
+    torch.cuda.synchronize()
+    assert bad == 0, bad
+    assert torch.isfinite(hn[-1].float()).all()
+    cnt = K.counter_buffer(x.device, torch.cuda.current_stream().cuda_stream, 0)
+    assert not cnt.any()
+
+
 @pytest.mark.parametrize("m,n,k", [(70001, 2304, 576), (70001, 576, 1152), (4097, 2304, 576),
                                    (300, 576, 1152), (9001, 768, 192), (9001, 192, 384),
                                    (5555, 1536, 384), (5555, 384, 768), (1, 2304, 576)])

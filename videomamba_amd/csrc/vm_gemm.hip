@@ -431,6 +431,11 @@ long long gemm_tile_count(int m, int n, int bn);
 void gemm_tile_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long ldw,
                       bf16_t* out, long long ldo, int m, int n, int k, int bn, int workgroups,
                       hipStream_t s);
+bool gemm_tile_norm_ok(int n, int k, int bn);
+void gemm_tile_norm_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long ldw,
+                           bf16_t* out, long long ldo, float* res, long long ldr, const float* nw,
+                           float eps, bf16_t* hn, long long ldh, unsigned* cnt, int m, int n,
+                           int k, int workgroups, hipStream_t s);
 // the persistent kernel runs from 1.5 tiles per CU (twice the tile count >= 3 x CUs): C5's
 // in_proj (12,544 rows, 441 tiles) 41.9 -> ~35 us, the C5 chunk 8.55 -> 8.26 ms
 constexpr int kTileMinPerCU2 = 3;
@@ -543,12 +548,10 @@ extern "C" int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* 
       ldo < n || ldr < n || ldh < n || ldx % 8 || ldw % 8 || ldo % 8 || ldr % 4 || ldh % 4 ||
       !vmhost::aligned16(x) || !vmhost::aligned16(w) || !vmhost::aligned16(h) ||
       !vmhost::aligned16(residual) || !vmhost::aligned16(norm_weight) || !vmhost::aligned16(hn) ||
-      (long long)m * ldx * 2 >= (1ll << 31) || (long long)n * ldw * 2 >= (1ll << 31) ||
-      (long long)m * ldo * 2 >= (1ll << 31) || (long long)m * ldr * 4 >= (1ll << 31) ||
-      counter_bytes < vm_linear_add_norm_counter_bytes(m)) {
+      (long long)n * ldw * 2 >= (1ll << 31) || counter_bytes < vm_linear_add_norm_counter_bytes(m)) {
     vmhost::set_error("vm_linear_add_norm_fwd: bf16 x / w / h / hn, fp32 residual and weight; "
                       "k a multiple of 64, n a multiple of 8 and <= 1024, 16-byte aligned "
-                      "rows under 2 GB, vm_linear_add_norm_counter_bytes(m) zeroed counters");
+                      "rows, w under 2 GB, vm_linear_add_norm_counter_bytes(m) zeroed counters");
     return VM_E_INVALID;
   }
   switch (k / kLinBK) {
@@ -587,6 +590,20 @@ extern "C" int vm_linear_add_norm_fwd(const void* x, long long ldx, const void* 
       default: break;
     }
     return vmhost::launch_status("vm_linear_add_norm_fwd");
+  }
+  // chip-filling row counts: the persistent tile GEMM with the norm pass per 256-row block
+  // (vm_gemm_tile.hip, NORM), where vm_linear_fwd_form would pick the persistent form
+  {
+    const int bn = gemm_tile_bn(m, n, k, ldx, ldw, ldo);
+    const int wgs = cus / 8 * 8;
+    if (bn && gemm_tile_norm_ok(n, k, bn) && wgs >= 8 &&
+        2 * gemm_tile_count(m, n, bn) >= static_cast<long long>(kTileMinPerCU2) * wgs) {
+      gemm_tile_norm_launch(static_cast<const bf16_t*>(x), ldx, static_cast<const bf16_t*>(w), ldw,
+                            static_cast<bf16_t*>(h), ldo, residual, ldr, norm_weight, eps,
+                            static_cast<bf16_t*>(hn), ldh, static_cast<unsigned*>(counters), m, n,
+                            k, wgs, s);
+      return vmhost::launch_status("vm_linear_add_norm_fwd");
+    }
   }
   // otherwise the two launches it replaces (the same kernels: bit-identical either way)
   if (ldo != n || ldr != n || ldh != n) {

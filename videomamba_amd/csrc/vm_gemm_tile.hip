@@ -95,8 +95,19 @@ struct TileGemmParams {
   int m, n, k;
   int ntn;    // n / BN
   int tiles;  // ceil(m / BM) * ntn
-  int tpx;    // ceil(tiles / 8): the contiguous tile range of one XCD's workgroups
+  int tpx;    // ceil(tiles / 8) (NORM: rounded up to whole row blocks of ntn tiles): the
+              // contiguous tile range of one XCD's workgroups
+  // NORM (vm_linear_add_norm_fwd at chip-filling row counts): the next block's residual
+  // add + RMSNorm, res += out (fp32, in place), hn = bf16(res * rsqrt(mean(res^2) + eps) * nw)
+  float* res; long long ldr;
+  const float* nw;
+  bf16_t* hn; long long ldh;
+  float eps;
+  unsigned* cnt;  // [0] error word, [16 + row block] producer counts; left zeroed
 };
+constexpr int kTileSC1 = 16;  // buffer cache-policy bit sc1: agent-coherent (cross-workgroup)
+// rows of the NORM pass each wave has in flight at once (18 VGPRs per row at n = 576)
+constexpr int kTileNormRows = 8;
 
 struct TileRes {  // one output tile: its x rows' buffer, its w rows' offset, its index
   __amdgpu_buffer_rsrc_t x;
@@ -132,7 +143,7 @@ constexpr bool kTileStamps = false;
 
 __device__ void tg_stamp_sink(int idx, unsigned long long t);
 
-template <int WGM, int TMH, int TNH, int NK>
+template <int WGM, int TMH, int TNH, int NK, bool NORM = false, int NC = 1>
 __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) {
   constexpr int WGN = 8 / WGM;
   constexpr int BM = 2 * WGM * TMH * 16, BN = 2 * WGN * TNH * 16;
@@ -146,6 +157,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   static_assert(WGM * WGN == 8 && HA == 128 && (HB == 128 || HB == 96), "tile geometry");
   static_assert(NK >= 3, "the prefetch reaches two K-tiles ahead inside one tile");
   static_assert(S <= 16, "output stores per wave per tile");
+  static_assert(!NORM || (TPI == 1 && NC >= 1 && NC <= 4), "NORM: even NK, n <= 1024");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
   const int tid = threadIdx.x;
@@ -305,10 +317,124 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
           const tg_i32x4 v{static_cast<int>(s0[0]), static_cast<int>(s1[0]),
                            static_cast<int>(s0[1]), static_cast<int>(s1[1])};
           const int col = (fq & 1) ? col_b : col_a;
-          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, 0);
+          // NORM: sc1, so the row block's norm pass on another workgroup reads them
+          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);
         }
       }
   };
+
+  // ---- NORM: the next block's add + RMSNorm of a finished 256-row block (NORM only).
+  // The ntn tiles of a row block are consecutive tile indices in one XCD's range (tpx is a
+  // whole number of row blocks), run by neighbouring workgroups at the same or an earlier
+  // step.  A producer (column tile < ntn - 1) makes its sc1 stores complete (vmcnt(0)) and,
+  // once every wave has (the barrier after), adds 1 to the block's counter; the last column
+  // tile's workgroup (the poller) completes its own stores, lines up its waves, polls the
+  // counter to ntn - 1 (sc1 / agent-scope, bounded: a timeout sets the error word and
+  // poisons the rows with NaN), then normalises the block: one wave per row, each lane the
+  // 4-column chunks lane * 4 + 256 j — add_rms_bf16_kernel's arithmetic and order
+  // (vm_norm.hip), so the result is bit-identical to out_proj then vm_add_norm_fwd — and
+  // resets the counter.  (MI355X_MICROARCH.md cross-workgroup hand-off; the grid is one
+  // workgroup per CU, every producer runs.)
+  typedef __attribute__((__vector_size__(4 * sizeof(float)))) float nv4f;
+  auto ncol = [&](int j, int es) __attribute__((always_inline)) {  // chunk j (out of range past n)
+    uint32_t o = lane * 4 + 256 * j < p.n ? (lane * 4 + 256 * j) * es : 0x7ffffff0u;
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  auto norm_pass = [&](int mt) __attribute__((always_inline)) {
+    const long long r0 = static_cast<long long>(mt) * BM;
+    const int rows = static_cast<int>(min(static_cast<long long>(p.m) - r0, static_cast<long long>(BM)));
+    int ok = 1;
+    if (lane == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(&p.cnt[16 + mt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             static_cast<unsigned>(p.ntn - 1)) {
+        if (++spins >= (1u << 20)) {
+          __hip_atomic_store(p.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    nv4f nwv[NC];
+    {
+      const auto wq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.nw), 0, p.n * 4, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        nwv[j] = __builtin_bit_cast(nv4f, __builtin_amdgcn_raw_buffer_load_b128(wq, ncol(j, 4), 0, 0));
+    }
+    constexpr int RPW = BM / 8;  // rows per wave
+    // one buffer per operand over the block's rows (range: the live rows; a dead row's or a
+    // column past n's offset falls outside), row offsets in the lane offset
+    const auto hr = __builtin_amdgcn_make_buffer_rsrc(p.out + r0 * p.ldo, 0, static_cast<int>(rows * p.ldo * 2), 0x00020000);
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(p.res + r0 * p.ldr, 0, static_cast<int>(rows * p.ldr * 4), 0x00020000);
+    const auto hnr = __builtin_amdgcn_make_buffer_rsrc(p.hn + r0 * p.ldh, 0, static_cast<int>(rows * p.ldh * 2), 0x00020000);
+    uint32_t c2[NC], c4[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      c2[j] = ncol(j, 2);
+      c4[j] = ncol(j, 4);
+    }
+#pragma unroll 1
+    for (int g = 0; g < RPW; g += kTileNormRows) {
+      uint32_t hq[kTileNormRows][NC][2];
+      nv4f rq[kTileNormRows][NC];
+#pragma unroll
+      for (int r = 0; r < kTileNormRows; ++r) {
+        const uint32_t lr = wave * RPW + g + r;
+        const uint32_t oh = lr * static_cast<uint32_t>(p.ldo) * 2, orr = lr * static_cast<uint32_t>(p.ldr) * 4;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hr, c2[j] + oh, 0, kTileSC1);
+          hq[r][j][0] = v[0];
+          hq[r][j][1] = v[1];
+          rq[r][j] = __builtin_bit_cast(nv4f, __builtin_amdgcn_raw_buffer_load_b128(rr, c4[j] + orr, 0, 0));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every load of the group in flight first
+#pragma unroll
+      for (int r = 0; r < kTileNormRows; ++r) {
+        const uint32_t lr = wave * RPW + g + r;
+        const uint32_t ohn = lr * static_cast<uint32_t>(p.ldh) * 2, orr = lr * static_cast<uint32_t>(p.ldr) * 4;
+        float v[NC][4];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          v[j][0] = __uint_as_float(hq[r][j][0] << 16) + rq[r][j][0];
+          v[j][1] = __uint_as_float(hq[r][j][0] & 0xffff0000u) + rq[r][j][1];
+          v[j][2] = __uint_as_float(hq[r][j][1] << 16) + rq[r][j][2];
+          v[j][3] = __uint_as_float(hq[r][j][1] & 0xffff0000u) + rq[r][j][3];
+        }
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+        float rstd = rsqrtf(sq / p.n + p.eps);
+        if (!ok) rstd = __builtin_nanf("");
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          float y[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[i] = (v[j][i] - 0.0f) * rstd * nwv[j][i];
+          typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
+          const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
+                                           (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
+                          static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
+                                           (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
+          __builtin_amdgcn_raw_buffer_store_b64(o2, hnr, c2[j] + ohn, 0, 0);
+          const tg_i32x4 r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
+                               static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
+          __builtin_amdgcn_raw_buffer_store_b128(r4, rr, c4[j] + orr, 0, 0);
+        }
+      }
+    }
+  };
+  int sig_mt = -1;   // NORM: the producer row block wave 4 counts in after its next barrier
+  int pend_mt = -1;  // NORM: the polled row block normalised at the end of the next tile
 
   // the iteration's tiles and the next iteration's first (scalars, not an array: an array
   // of descriptors captured by the lambdas below stays in memory and loses uniformity)
@@ -366,6 +492,13 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       stamp(1);
       tg_barrier();
       stamp(2);
+      if constexpr (NORM && P == 0 && kt == 0) {
+        // every wave's stores of the previous tile completed before this barrier (waves 0-3
+        // run one barrier ahead of wave 4): count the producer tile in
+        if (sig_mt >= 0 && wave == 4 && lane == 0)
+          __hip_atomic_fetch_add(&p.cnt[16 + sig_mt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sig_mt = -1;
+      }
       if constexpr (kTileLgkmLate) {
         tg_wait_lgkm0();
         __builtin_amdgcn_sched_barrier(0);
@@ -384,6 +517,33 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       if constexpr (P == 3 && kt == NK - 1) {
         if constexpr (tp == 0) store_tile(cur0);
         else store_tile(cur1);
+        if constexpr (NORM) {
+          __builtin_amdgcn_s_waitcnt(0);  // this wave's sc1 stores are acknowledged
+          const int mt = cur0.t / p.ntn;
+          const bool poller = cur0.t - mt * p.ntn == p.ntn - 1;  // uniform
+          if (pend_mt >= 0) {
+            // the row block this workgroup polled for one tile ago: line the waves up (waves
+            // 0-3 skip the stagger's barrier; every wave's stores are then acknowledged),
+            // count this tile in, normalise, re-stagger
+            if (wave < 4) tg_barrier();
+            tg_barrier();
+            if (!poller && wave == 0 && lane == 0)
+              __hip_atomic_fetch_add(&p.cnt[16 + mt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            norm_pass(pend_mt);
+            if (wave >= 4) {
+              tg_barrier();  // waves 0-3 have finished their polls and rows
+              if (wave == 4 && lane == 0)
+                __hip_atomic_store(&p.cnt[16 + pend_mt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            pend_mt = -1;
+          } else if (!poller) {
+            sig_mt = mt;  // wave 4 counts it in after its next barrier
+          }
+          // the poller normalises its block after its NEXT tile: its producers (the
+          // neighbouring workgroups' same-step tiles) have then long finished, so a norm pass
+          // never waits on another workgroup's norm pass (no chain across the XCD's runs)
+          if (poller) pend_mt = mt;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -401,6 +561,17 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   // the last prefetches (out of range) still write LDS: drain before the workgroup ends
   __builtin_amdgcn_s_waitcnt(0);
   if (wave < 4) tg_barrier();  // balance the stagger's extra barrier
+  if constexpr (NORM) {
+    tg_barrier();  // every wave's stores of the last tile are acknowledged
+    if (sig_mt >= 0 && wave == 0 && lane == 0)
+      __hip_atomic_fetch_add(&p.cnt[16 + sig_mt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pend_mt >= 0) {
+      norm_pass(pend_mt);
+      tg_barrier();
+      if (wave == 0 && lane == 0)
+        __hip_atomic_store(&p.cnt[16 + pend_mt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Configurations: (WGM, TMH, TNH) -> BM x BN
@@ -463,5 +634,37 @@ void gemm_tile_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long
 }
 #undef VM_TG_CFG
 #undef VM_TG_K
+
+// The NORM form (out_proj + the next block's residual add + RMSNorm): 256 x 192 tiles,
+// K = 384 / 768 / 1152 with n = 192 / 384 / 576 (VideoMamba Ti / S / M out_proj).
+bool gemm_tile_norm_ok(int n, int k, int bn) {
+  return bn == 192 && ((n == 192 && k == 384) || (n == 384 && k == 768) || (n == 576 && k == 1152));
+}
+
+void gemm_tile_norm_launch(const bf16_t* x, long long ldx, const bf16_t* w, long long ldw,
+                           bf16_t* out, long long ldo, float* res, long long ldr, const float* nw,
+                           float eps, bf16_t* hn, long long ldh, unsigned* cnt, int m, int n,
+                           int k, int workgroups, hipStream_t s) {
+  TileGemmParams p{};
+  p.x = x; p.ldx = ldx; p.w = w; p.ldw = ldw; p.out = out; p.ldo = ldo;
+  p.m = m; p.n = n; p.k = k;
+  p.ntn = n / 192;
+  p.tiles = static_cast<int>(gemm_tile_count(m, n, 192));
+  p.tpx = ((p.tiles + 7) / 8 + p.ntn - 1) / p.ntn * p.ntn;  // whole row blocks per XCD range
+  p.res = res; p.ldr = ldr; p.nw = nw; p.hn = hn; p.ldh = ldh; p.eps = eps; p.cnt = cnt;
+  const dim3 grid(workgroups);
+  switch (k / 64) {
+    case 6:
+      hipLaunchKernelGGL((gemm_tile_kernel<4, 2, 3, 6, true, 1>), grid, dim3(512), kTileLdsNarrow, s, p);
+      break;
+    case 12:
+      hipLaunchKernelGGL((gemm_tile_kernel<4, 2, 3, 12, true, 2>), grid, dim3(512), kTileLdsNarrow, s, p);
+      break;
+    case 18:
+      hipLaunchKernelGGL((gemm_tile_kernel<4, 2, 3, 18, true, 3>), grid, dim3(512), kTileLdsNarrow, s, p);
+      break;
+    default: break;
+  }
+}
 
 }  // namespace vm

@@ -41,10 +41,12 @@ documented options object; tests and sweeps change them with :func:`override`.
                      forward bit for bit; 0: only the small_gemm_* rule below.
     fuse_out_norm    False (default): True makes a mixer whose out_proj runs on the HIP GEMM
                      (bf16 fused RMSNorm blocks) also run the next block's residual add +
-                     RMSNorm (vm_linear_add_norm_fwd; bit-identical to the separate kernels).
-                     Measured slower at B = 1 (48 vs 10.9 + 6.9 us per layer: the granule's
-                     last workgroup reads the other tiles' rows back from beyond L2), so it
-                     is off by default (DESIGN §7).
+                     RMSNorm (vm_linear_add_norm_fwd; bit-identical to the separate kernels:
+                     the one-launch LDS-DMA form at small row counts, the persistent tile
+                     GEMM's per-row-block norm pass at chip-filling ones).  Measured slower
+                     at both ends: B = 1 16.5-17.3 vs 13.1-13.8 us per layer,
+                     B = 448 4.14 vs 3.37-3.55 ms per layer (the step 492 vs 441 ms), so it
+                     is off by default.
     small_gemm_rows  ("library" mode) in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
