@@ -72,6 +72,11 @@ VARIANTS = {
     "tn_rows4": [("vm_gemm_tile.hip", "constexpr int kTileNormRows = 8;", "constexpr int kTileNormRows = 4;")],
     "tn_plainh": [("vm_gemm_tile.hip", "          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hr, c2[j] + oh, 0, kTileSC1);",
                    "          const auto v = __builtin_amdgcn_raw_buffer_load_b64(hr, c2[j] + oh, 0, 0);")],
+    # persistent GEMM: the tile's stores in two halves (A-top after phase 1, A-bottom after
+    # phase 3 of the last K-tile)
+    "tg_split": [("vm_gemm_tile.hip", "constexpr bool kTileSplitStore = false;", "constexpr bool kTileSplitStore = true;")],
+    # chunked scan: B|C rows one step ahead with a wait every step (the round-4 form)
+    "ch_bc1": [("vm_scan_seq.hip", "constexpr bool kChBcPairs = true;", "constexpr bool kChBcPairs = false;")],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",

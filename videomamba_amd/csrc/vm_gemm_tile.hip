@@ -138,6 +138,10 @@ constexpr bool kTileLgkmLate = true;
 // five points of every phase of one steady-state iteration, waves 0 and 4 of workgroup 0.
 // Off in the product (the calls are discarded; the sink is defined only by the probe build).
 constexpr bool kTileStamps = false;
+// store the A-top half of a finished tile after phase 1 of its last K-tile (its quadrants
+// (top, left) and (top, right) are final there) and the A-bottom half after phase 3, instead
+// of all 2 x TMH x TNH stores after phase 3 (the burst is split across the stagger)
+constexpr bool kTileSplitStore = false;
 
 }  // namespace
 
@@ -297,9 +301,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
   // consecutive columns: lane row r16 = lane / 16 takes tile 2c + (r16 & 1), columns
   // 8 (r16 >> 1) .. +7
   const int st_lane = fr * static_cast<int>(p.ldo) * 2 + (8 * (fq >> 1)) * 2;
-  auto store_tile = [&](const TileRes& tr) __attribute__((always_inline)) {
+  auto store_tile = [&](const TileRes& tr, int h0 = 0, int h1 = 2) __attribute__((always_inline)) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = h0; h < h1; ++h)
 #pragma unroll
       for (int i = 0; i < TMH; ++i) {
         const auto o = out_res(tr.t, h * HA + arow0 + i * 16);
@@ -514,9 +518,20 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       tg_barrier();
       stamp(4);
       // 5. the tile is done after its last quadrant: store it, restart the accumulators
+      if constexpr (kTileSplitStore && !NORM && P == 1 && kt == NK - 1) {
+        if constexpr (tp == 0) store_tile(cur0, 0, 1);
+        else store_tile(cur1, 0, 1);
+#pragma unroll
+        for (int i = 0; i < TMH; ++i)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int j = 0; j < TNH; ++j) acc[0][i][g][j] = tg_f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       if constexpr (P == 3 && kt == NK - 1) {
-        if constexpr (tp == 0) store_tile(cur0);
-        else store_tile(cur1);
+        constexpr int h0 = (kTileSplitStore && !NORM) ? 1 : 0;
+        if constexpr (tp == 0) store_tile(cur0, h0, 2);
+        else store_tile(cur1, h0, 2);
         if constexpr (NORM) {
           __builtin_amdgcn_s_waitcnt(0);  // this wave's sc1 stores are acknowledged
           const int mt = cur0.t / p.ntn;

@@ -917,6 +917,11 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
 // Compared with the summary / carry / final form it replaces for SGPR-eligible operands,
 // the carry never leaves the chip's LDS except for one aggregate per block.
 constexpr int kChW = 8;  // segments (waves) per workgroup
+// chunked scan, PASS 1 step loop: B|C rows fetched in pairs of steps, two steps ahead (a
+// 4-slot SGPR ring, one lgkmcnt(0) per pair): scalar loads return out of order, so a ring
+// deeper than one step needs the wait to cover whole groups.  PASS 2 keeps one row one step
+// ahead (its C rows double the ring: SGPR spills in its loop cost more than the wait saves)
+constexpr bool kChBcPairs = true;
 constexpr int kChSPW = kMaxN / kChW;  // states a wave composes / publishes / walks
 constexpr int kChPoll = kChSPW == 2 ? 8 : 4;  // preceding blocks polled per round (one-launch)
 static_assert(kMaxN % kChW == 0 && (kChSPW == 1 || kChSPW == 2), "1 or 2 states per wave");
@@ -1097,7 +1102,8 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const T* Cq = static_cast<const T*>(p.C) + b * p.c_sb;
   const uint32_t bsl = static_cast<uint32_t>(p.b_sl * ES);
   const uint32_t csl = static_cast<uint32_t>(p.c_sl * ES);
-  uint32_t bcw[2][2 * NWD];
+  constexpr int kBcSlots = kChBcPairs ? 4 : 2;
+  uint32_t bcw[kBcSlots][2 * NWD];
   auto bc_load = [&](int t, uint32_t (&dst)[2 * NWD]) {
     const cptr bp = (cptr)(reinterpret_cast<const char*>(Bq) + static_cast<uint32_t>(t) * bsl);
     if constexpr (BC1) {
@@ -1141,6 +1147,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   float sdel = 0.0f;
   if (t_beg < t_end) {
     bc_load(t_beg, bcw[0]);
+    if constexpr (kChBcPairs) bc_load(min(t_beg + 1, tlast), bcw[1]);
 #pragma unroll
     for (int j = 0; j < kPF; ++j) {
       const int t = min(t_beg + j, tlast);
@@ -1336,8 +1343,16 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         ru[j] = bload<T>(ur, voff, tn * us);
         if constexpr (!DTP) rd[j] = bload<T>(dr_, voff, tn * ds);
         if (HZ && EMIT) rz[j] = bload<T>(zr, voff, tn * zs);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
-        bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+        if constexpr (kChBcPairs && !EMIT) {
+          if ((j & 1) == 0) {  // a pair starts: its two rows have landed; fetch the next pair's
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            bc_load(min(t + 2, tlast), bcw[(j + 2) & 3]);
+            bc_load(min(t + 3, tlast), bcw[(j + 3) & 3]);
+          }
+        } else {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B/C rows have landed
+          bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);
+        }
         // DTP: the LDS read goes after that wait, so the next step's wait is its first
         if constexpr (DTP) rd[j] = dt_lds(tn);
         __builtin_amdgcn_sched_barrier(0);  // (without: 10-40 % slower, scripts/diag)
@@ -1350,7 +1365,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
           g_nx = gate_of(rz[(j + 1) & (kPF - 1)]);
         }
         const float du = dl * uu;
-        const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
+        const uint32_t (&cw)[2 * NWD] = bcw[j & ((kChBcPairs && !EMIT) ? 3 : 1)];
         const f2 dl2 = {dl, dl}, du2 = {du, du};
         f2 ya = {Dv * uu, 0.0f}, yb = {0.0f, 0.0f};
 #pragma unroll
