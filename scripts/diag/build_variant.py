@@ -77,6 +77,29 @@ VARIANTS = {
     "tg_split": [("vm_gemm_tile.hip", "constexpr bool kTileSplitStore = false;", "constexpr bool kTileSplitStore = true;")],
     # chunked scan: B|C rows one step ahead with a wait every step (the round-4 form)
     "ch_bc1": [("vm_scan_seq.hip", "constexpr bool kChBcPairs = true;", "constexpr bool kChBcPairs = false;")],
+    # persistent GEMM pricing (results wrong): no output stores
+    "tg_nostore": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);",
+                    "          if (v[0] == 0x12345 && v[3] == 0x777) __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);")],
+    # persistent GEMM output stores with another cache policy: nt (aux 2) / sc0 (aux 1) / sc0 nt (3)
+    "tg_st_nt": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 2);")],
+    "tg_st_sc0": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 1);")],
+    "tg_st_sc0nt": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 3);")],
+    # persistent GEMM pricing (results may be wrong): the first K-tile's waits after a tile's
+    # stores allow the stores as younger ops (no drain of the stores at the tile boundary)
+    "tg_st_nodrain": [("vm_gemm_tile.hip", "        if constexpr (P != 2) tg_wait_vm<VM>();",
+                       "        if constexpr (P != 2) { if constexpr (kt == 0) tg_wait_vm<VM + S>(); else tg_wait_vm<VM>(); }")],
+    # persistent GEMM output stores sc1 (write-through, the line leaves L2) / sc0 sc1
+    "tg_st_sc1": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 16);")],
+    "tg_st_sc01": [("vm_gemm_tile.hip", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 0);", "          __builtin_amdgcn_raw_buffer_store_b128(v, o, st_lane + col * 2, 0, NORM ? kTileSC1 : 17);")],
+    # persistent GEMM pricing (results wrong): every tile stages the first N-panel of W
+    # (w_fixed: W L2-resident) / the first row block of x (x_fixed)
+    "tg_w_fixed": [("vm_gemm_tile.hip", "    r.wsoff = nt * BN * wbytes;", "    r.wsoff = 0 * nt * BN * wbytes;")],
+    "tg_x_fixed": [("vm_gemm_tile.hip", "    r.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.x + m0 * p.ldx), 0,",
+                    "    r.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.x + 0 * m0 * p.ldx), 0,")],
+    # persistent GEMM: the A-bottom half of a tile stored after the next tile's phase 1
+    "tg_defer": [("vm_gemm_tile.hip", "constexpr bool kTileDeferStore = false;", "constexpr bool kTileDeferStore = true;")],
+    # persistent GEMM: every wave stores a finished tile at the same time (no MFMA beside it)
+    "tg_sync": [("vm_gemm_tile.hip", "constexpr bool kTileSyncStore = false;", "constexpr bool kTileSyncStore = true;")],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",

@@ -142,6 +142,12 @@ constexpr bool kTileStamps = false;
 // (top, left) and (top, right) are final there) and the A-bottom half after phase 3, instead
 // of all 2 x TMH x TNH stores after phase 3 (the burst is split across the stagger)
 constexpr bool kTileSplitStore = false;
+// store the A-bottom half of a finished tile one phase into the next tile (after its phase-1
+// MFMAs; those accumulators are next used in its phase 2) instead of with the A-top half
+constexpr bool kTileDeferStore = false;
+// all eight waves store a finished tile together (waves 0-3 wait for 4-7's last MFMAs, 4-7
+// re-stagger after their stores) instead of each half beside the other half's MFMAs
+constexpr bool kTileSyncStore = false;
 
 }  // namespace
 
@@ -437,6 +443,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       }
     }
   };
+  int prev_t = -1;   // kTileDeferStore: the tile whose A-bottom half is still to be stored
   int sig_mt = -1;   // NORM: the producer row block wave 4 counts in after its next barrier
   int pend_mt = -1;  // NORM: the polled row block normalised at the end of the next tile
 
@@ -528,10 +535,31 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
 #pragma unroll
             for (int j = 0; j < TNH; ++j) acc[0][i][g][j] = tg_f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (kTileDeferStore && !NORM && P == 1 && kt == 0) {
+        if (prev_t >= 0) {  // the previous tile's A-bottom half
+          TileRes pr;
+          pr.t = prev_t;
+          store_tile(pr, 1, 2);
+#pragma unroll
+          for (int i = 0; i < TMH; ++i)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+              for (int j = 0; j < TNH; ++j) acc[1][i][g][j] = tg_f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      if constexpr (kTileSyncStore && !NORM && P == 3 && kt == NK - 1) {
+        if (wave < 4) tg_barrier();
+      }
       if constexpr (P == 3 && kt == NK - 1) {
         constexpr int h0 = (kTileSplitStore && !NORM) ? 1 : 0;
-        if constexpr (tp == 0) store_tile(cur0, h0, 2);
-        else store_tile(cur1, h0, 2);
+        constexpr int h1 = (kTileDeferStore && !NORM) ? 1 : 2;
+        if constexpr (tp == 0) store_tile(cur0, h0, h1);
+        else store_tile(cur1, h0, h1);
+        if constexpr (kTileDeferStore && !NORM) prev_t = tp == 0 ? cur0.t : cur1.t;
+        if constexpr (kTileSyncStore && !NORM) {
+          if (wave >= 4) tg_barrier();
+        }
         if constexpr (NORM) {
           __builtin_amdgcn_s_waitcnt(0);  // this wave's sc1 stores are acknowledged
           const int mt = cur0.t / p.ntn;
@@ -560,7 +588,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
           if (poller) pend_mt = mt;
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < ((kTileDeferStore && !NORM) ? 1 : 2); ++h)
 #pragma unroll
           for (int i = 0; i < TMH; ++i)
 #pragma unroll
@@ -572,6 +600,13 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
     cur0 = nxt;
     if (TPI == 2) cur1 = tile_res(TPI * it + TPI + 1);
     nxt = tile_res(TPI * it + 2 * TPI);
+  }
+  if constexpr (kTileDeferStore && !NORM) {
+    if (prev_t >= 0) {
+      TileRes pr;
+      pr.t = prev_t;
+      store_tile(pr, 1, 2);
+    }
   }
   // the last prefetches (out of range) still write LDS: drain before the workgroup ends
   __builtin_amdgcn_s_waitcnt(0);
