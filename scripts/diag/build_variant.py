@@ -100,6 +100,9 @@ VARIANTS = {
     "tg_defer": [("vm_gemm_tile.hip", "constexpr bool kTileDeferStore = false;", "constexpr bool kTileDeferStore = true;")],
     # persistent GEMM: every wave stores a finished tile at the same time (no MFMA beside it)
     "tg_sync": [("vm_gemm_tile.hip", "constexpr bool kTileSyncStore = false;", "constexpr bool kTileSyncStore = true;")],
+    # persistent GEMM pricing (results wrong): every tile's stores go to tile 0's rows (an
+    # L2-resident 128 KB target: same instructions, no HBM write stream)
+    "tg_st_l2": [("vm_gemm_tile.hip", "      m0 = static_cast<long long>(mt) * BM + r0;", "      m0 = 0 * static_cast<long long>(mt) * BM + r0;")],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",
