@@ -406,7 +406,14 @@ int vm_linear_fwd_form(const void* x, long long ldx, const void* w, long long ld
  * (ABI v13; B = 1 out_proj shapes): after its tile every workgroup normalises a share of the
  * rows, waiting (bounded) on per-128-row-tile counters that the tiles' producers add to
  * after agent-coherent h stores; a timeout sets word 0 of `counters` and makes the rows NaN.
- * Larger grids run vm_linear_fwd + vm_add_norm_fwd (contiguous h / residual / hn rows).
+ * Chip-filling row counts (where vm_linear_fwd picks the persistent tile kernel) with
+ * (n, k) = (192, 384), (384, 768) or (576, 1152) — the Ti / S / M out_proj — run the
+ * persistent kernel's NORM form: the workgroup of a 256-row block's last column tile, after
+ * the other column tiles' producers count in, normalises the block (any row count, operands
+ * past 2 GB).  Other larger grids run vm_linear_fwd + vm_add_norm_fwd (contiguous h /
+ * residual / hn rows).  Every form gives the bits of the two separate calls; both fused
+ * forms measured slower than the separate calls on MI355X, so the model
+ * uses this entry point only when options.fuse_out_norm is set.
  * `counters`: vm_linear_add_norm_counter_bytes(m) zeroed bytes, left zeroed; one buffer must
  * not serve two launches that can run at the same time.  n % 8 == 0, n <= 1024, k as
  * vm_linear_fwd.
