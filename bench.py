@@ -481,9 +481,21 @@ def _base_line(args, cfg, world, global_batch, per_rank, elapsed, strong):
                        "one stateful streaming chunk (chunk_size 32) per step"),
                    "model": cfg["name"], "global_batch": global_batch,
                    "per_gpu_batch": per_rank, "frames": T, "seq_len": 1 + T * 196,
-                   "parallelism": f"batch-sharded x{world}, no data-path collectives"},
+                   "parallelism": f"batch-sharded x{world}, no data-path collectives",
+                   "sub_batch_streams": _sub_batch_streams(per_rank)},
         "per_gpu_value": round(value / world, 1),
     }
+
+
+def _sub_batch_streams(batch):
+    """How many HIP streams the model's forward splits this per-GPU batch over
+    (options.batch_streams; bit-identical to one stream)."""
+    try:
+        from videomamba_amd import options
+    except Exception:  # the CPU stub run
+        return 1
+    o = options.get()
+    return int(o.batch_streams) if batch >= max(int(o.batch_stream_min_clips), 2) else 1
 
 
 def main_stub_cpu(args):

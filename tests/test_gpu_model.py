@@ -11,6 +11,7 @@ from types import SimpleNamespace
 
 import pytest
 import torch
+from torch import Tensor
 import torch.nn.functional as F
 
 import video_mamba
@@ -1126,3 +1127,90 @@ def test_conv_proj_cm_chunk_invariant_bitwise(Bsz, L, cut):
     rdt = torch.einsum("dr,rbl->dbl", m.dt_proj.weight.float().cpu(),
                        xd[:R].float().cpu()).to(torch.bfloat16)
     torch.testing.assert_close(dt.float().cpu(), rdt.float(), rtol=2e-2, atol=2e-2)
+
+
+def _clone_state(st):
+    if st is None:
+        return None
+    if isinstance(st, dict):
+        return {k: _clone_state(v) for k, v in st.items()}
+    if isinstance(st, Tensor):
+        return st.clone()
+    items = [_clone_state(v) for v in st]
+    return tuple(items) if isinstance(st, tuple) else items
+
+
+def _flat(st):
+    if st is None:
+        return []
+    if isinstance(st, Tensor):
+        return [st]
+    vals = st.values() if isinstance(st, dict) else st
+    return [t for v in vals for t in _flat(v)]
+
+
+@pytest.mark.parametrize("kind", ["none", "list", "tuple", "dict", "ssm_only", "mask", "keep_temporal"])
+@pytest.mark.parametrize("parts", [2, 3])
+def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
+    """options.batch_streams: a forward over enough clips runs as sub-batches, each on its own
+    HIP stream (the bench's B = 448 step: two halves, one's scan overlapping the other's
+    projections).  Every kernel's rows are batch-independent, so x_vis, x_pool and every
+    returned state are bit-equal to the one-stream forward — over two stateful chunks (the
+    ssm states advanced in place in the caller's tensors, new conv states), for list / tuple
+    / dict / legacy ssm-only state containers, masks and keep_temporal pooling; uneven part
+    sizes (7 clips in 2 or 3 parts)."""
+    torch.manual_seed(5)
+    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=64, channels=3,
+                               kernel_size=1, num_frames=4, pool_type="avg",
+                               fused_add_norm=True, rms_norm=True, residual_in_fp32=True)
+    model = model.to(DEV).to(torch.bfloat16).eval()
+    B = 7
+    x = torch.randn(B, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
+    mask = None
+    if kind == "mask":  # a 2-frame chunk: 4 patch tokens per frame x 2 (+ CLS); keep 6
+        g = torch.Generator(device="cpu").manual_seed(3)
+        mask = torch.ones(B, 9, dtype=torch.bool)
+        for b in range(B):
+            mask[b, 0] = False
+            keep = torch.randperm(8, generator=g)[:5] + 1
+            mask[b, keep] = False
+        mask = mask.to(DEV)
+
+    def make_state():
+        if kind in ("none", "mask", "keep_temporal"):
+            return None
+        if kind == "ssm_only":
+            return model.init_ssm_state(B, dtype=torch.float32, device=DEV)
+        st = model.allocate_state(B, dtype=torch.bfloat16, device=DEV, as_dict=kind == "dict")
+        return tuple(st) if kind == "tuple" else st
+
+    def run(n):
+        st = make_state()
+        outs = []
+        with options.override(batch_streams=n, batch_stream_min_clips=2), torch.no_grad():
+            for off in (0, 2):
+                kw = dict(keep_temporal=kind == "keep_temporal", mask=mask if off == 0 else None)
+                if st is None:
+                    res = model(x[:, :, off:off + 2], **kw)
+                    outs.append([t.clone() for t in res])
+                    continue
+                held = _flat(st)
+                res = model(x[:, :, off:off + 2], ssm_state=st, temporal_pos_offset=off, **kw)
+                new = res[-1]
+                if kind == "ssm_only":
+                    assert new is st
+                else:  # ssm states advanced in the caller's tensors, conv states new
+                    for (c_new, s_new), s_old in zip(new.values() if isinstance(new, dict) else new,
+                                                     held[1::2]):
+                        assert s_new is s_old
+                    assert type(new) is type(st)
+                outs.append([t.clone() for t in res[:-1]] + [t.clone() for t in _flat(new)])
+                st = new
+        torch.cuda.synchronize()
+        return outs
+
+    one, many = run(1), run(parts)
+    for a_step, b_step in zip(one, many):
+        assert len(a_step) == len(b_step)
+        for a, b in zip(a_step, b_step):
+            assert a.shape == b.shape and torch.equal(a, b), (a.float() - b.float()).abs().max().item()

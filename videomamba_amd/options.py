@@ -47,6 +47,17 @@ documented options object; tests and sweeps change them with :func:`override`.
                      at both ends: B = 1 16.5-17.3 vs 13.1-13.8 us per layer,
                      B = 448 4.14 vs 3.37-3.55 ms per layer (the step 492 vs 441 ms), so it
                      is off by default.
+    batch_streams    2 (default): a forward over at least ``batch_stream_min_clips`` clips runs
+                     as this many sub-batches, each on its own HIP stream, so one part's
+                     VALU-bound scan overlaps another part's MFMA / HBM-bound kernels; every
+                     kernel's rows are independent of the batch, so the outputs and states
+                     are bit-identical to the one-stream forward.  1 = one stream.
+                     Measured on M-16f (scripts/diag/batch_streams_sweep.py): B = 448 in two
+                     parts 424-425 vs 432-436 ms per step; three or four parts, or two parts
+                     of B = 224 / 112, are slower than one stream.
+    batch_stream_min_clips
+                     the smallest batch that is split (default 448: parts of >= 224 clips,
+                     a whole round of the dt_proj-in-scan grid each).
     small_gemm_rows  ("library" mode) in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -80,6 +91,8 @@ class Options:
     projection_gemm: str = "hip"
     row_invariant_gemm_clips: int = 8
     fuse_out_norm: bool = False
+    batch_streams: int = 2
+    batch_stream_min_clips: int = 448
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
 
@@ -88,6 +101,8 @@ class Options:
             raise ValueError(f"mixer_layout must be one of {_LAYOUTS}, got {self.mixer_layout!r}")
         if int(self.scan_segments) < 0:
             raise ValueError("scan_segments must be >= 0")
+        if int(self.batch_streams) < 1:
+            raise ValueError("batch_streams must be >= 1")
         if int(self.small_gemm_rows) < 0:
             raise ValueError("small_gemm_rows must be >= 0")
         if self.scan_dt_proj not in ("auto", "on", "off"):

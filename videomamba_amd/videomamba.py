@@ -241,6 +241,18 @@ class PatchEmbed(nn.Module):
 
 
 # ----------------------------------------------------------------------------- encoder
+_SIDE_STREAMS: Dict[Any, List[torch.cuda.Stream]] = {}
+
+
+def _side_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
+    """n persistent HIP streams of ``device`` for sub-batch forwards (created once)."""
+    key = (device.type, device.index)
+    have = _SIDE_STREAMS.setdefault(key, [])
+    while len(have) < n:
+        have.append(torch.cuda.Stream(device))
+    return have[:n]
+
+
 class PretrainVideoMamba(nn.Module):
     streaming_contract_version: str = STREAMING_CONTRACT_VERSION
 
@@ -596,6 +608,9 @@ class PretrainVideoMamba(nn.Module):
     def _encode(self, x, mask, ssm_state, temporal_pos_offset, tpos=None, pool=None,
                 conv_out=None):
         """(features (B, N_vis, C), x_pool | None, state result | None)."""
+        parts = self._stream_parts(x, ssm_state, tpos, conv_out)
+        if parts > 1:
+            return self._encode_streams(x, mask, ssm_state, temporal_pos_offset, pool, parts)
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
         h, L, _, _ = self._embed(x, has_cls, temporal_pos_offset, tpos=tpos)
         Bsz = x.shape[0]
@@ -620,6 +635,112 @@ class PretrainVideoMamba(nn.Module):
             st = new_states
         else:
             st = ssm_state
+        return feats, x_pool, st
+
+    # ------------------------------------------------------------------ batch streams
+    def _stream_parts(self, x, ssm_state, tpos, conv_out) -> int:
+        """How many sub-batches (one HIP stream each) this forward runs as:
+        ``options.batch_streams`` from ``batch_stream_min_clips`` clips up, outside graph
+        capture and the graph runner's buffers, when every layer's state (if any) is one kind
+        (full (conv, ssm) pairs of one conv dtype, or legacy ssm-only tensors)."""
+        o = options.get()
+        n = int(o.batch_streams)
+        B = x.shape[0]
+        if (n <= 1 or B < max(int(o.batch_stream_min_clips), 2) or tpos is not None
+                or conv_out is not None or torch.cuda.is_current_stream_capturing()):
+            return 1
+        if ssm_state is not None:
+            kinds = set()
+            for idx in range(len(self.layers)):
+                st = self._get_layer_state(ssm_state, idx)
+                if isinstance(st, (list, tuple)) and len(st) == 2:
+                    kinds.add(("full", st[0].dtype))
+                elif isinstance(st, Tensor):
+                    kinds.add(("ssm", None))
+                else:
+                    return 1
+            if len(kinds) != 1:
+                return 1
+        return min(n, B)
+
+    def _prepare_param_caches(self) -> None:
+        """Materialise every parameter-derived cache (fp32 copies, padded projection
+        weights) on the current stream before a forward forks into sub-batch streams: a
+        cache first built inside one sub-batch's stream would be read by the others
+        unordered."""
+        for layer in self.layers:
+            layer.mixer._fp32_params()
+            layer.mixer._padded_proj_weights()
+            K.f32_cached(layer.norm, layer.norm.weight, "w")
+            K.f32_cached(layer.norm, getattr(layer.norm, "bias", None), "b")
+        K.f32_cached(self.norm, self.norm.weight, "w")
+        K.f32_cached(self.norm, getattr(self.norm, "bias", None), "b")
+        pn = getattr(self, "pool_norm", None)
+        if isinstance(pn, nn.LayerNorm):
+            K.f32_cached(pn, pn.weight, "w")
+            K.f32_cached(pn, pn.bias, "b")
+        K.f32_cached(self.patch_embed, self.patch_embed.proj.bias, "b")
+
+    def _encode_streams(self, x, mask, ssm_state, temporal_pos_offset, pool, parts):
+        """_encode as ``parts`` sub-batches on their own streams, joined before returning.
+        Sub-batch states are views of the caller's tensors (ssm states advance in place as
+        in the one-stream forward); new conv states land in slices of one fresh buffer."""
+        dev = x.device
+        B = x.shape[0]
+        cut = [B * i // parts for i in range(parts + 1)]
+        cur = torch.cuda.current_stream(dev)
+        streams = _side_streams(dev, parts)
+        self._prepare_param_caches()
+        depth = len(self.layers)
+        full = False
+        conv_new = None
+        if ssm_state is not None:
+            st0 = self._get_layer_state(ssm_state, 0)
+            full = isinstance(st0, (list, tuple))
+            if full:
+                m0 = self.layers[0].mixer
+                conv_new = torch.empty((depth, B, m0.d_inner, m0.d_conv), dtype=st0[0].dtype,
+                                       device=dev)
+
+        def part_state(a, b):
+            if ssm_state is None:
+                return None
+            def sl(st):
+                if isinstance(st, Tensor):
+                    return st[a:b]
+                return type(st)(t[a:b] for t in st) if isinstance(st, tuple) else [t[a:b] for t in st]
+            if isinstance(ssm_state, dict):
+                return {k: sl(v) for k, v in ssm_state.items()}
+            items = [sl(v) for v in ssm_state]
+            return tuple(items) if isinstance(ssm_state, tuple) else items
+
+        outs = []
+        for i in range(parts):
+            a, b = cut[i], cut[i + 1]
+            s = streams[i]
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                outs.append(self._encode(
+                    x[a:b], None if mask is None else mask[a:b], part_state(a, b),
+                    temporal_pos_offset, pool=pool,
+                    conv_out=None if conv_new is None else conv_new[:, a:b]))
+        for s in streams[:parts]:
+            cur.wait_stream(s)
+        feats = torch.cat([o[0] for o in outs], 0)
+        x_pool = None if outs[0][1] is None else torch.cat([o[1] for o in outs], 0)
+        if ssm_state is None:
+            st = None
+        elif full:
+            def layer(idx):
+                old = self._get_layer_state(ssm_state, idx)
+                return (conv_new[idx], old[1])  # the ssm state advanced in place
+            if isinstance(ssm_state, dict):
+                st = {k: layer(k) for k in ssm_state}
+            else:
+                items = [layer(idx) for idx in range(depth)]
+                st = tuple(items) if isinstance(ssm_state, tuple) else items
+        else:
+            st = ssm_state  # legacy ssm-only tensors, advanced in place
         return feats, x_pool, st
 
     def forward(self, x: Tensor, mask: Optional[Tensor] = None, use_image: bool = False,
