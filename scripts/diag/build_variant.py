@@ -103,6 +103,10 @@ VARIANTS = {
     # persistent GEMM pricing (results wrong): every tile's stores go to tile 0's rows (an
     # L2-resident 128 KB target: same instructions, no HBM write stream)
     "tg_st_l2": [("vm_gemm_tile.hip", "      m0 = static_cast<long long>(mt) * BM + r0;", "      m0 = 0 * static_cast<long long>(mt) * BM + r0;")],
+    # B = 448 scan capped at 6 workgroups (3 waves per SIMD) per CU by 5 KB of padding LDS,
+    # leaving a wave slot per SIMD for another stream's kernel
+    "dtp_occ3": [("vm_scan_seq.hip", "    case 3: hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;",
+                  "    case 3: hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 5120, s, p, q); break;")],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",
