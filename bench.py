@@ -55,7 +55,10 @@ CYC_EXP, CYC_FMA, SIMDS, CLOCK_HZ = 8.2, 2.8, 1024, 2.4e9
 LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
-    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M"),  # C3 (default)
+    # C3 (default): 896 clips per GPU = two 448-clip sub-batch streams (options.batch_streams;
+    # each launch keeps the 448-clip shape whose scan grid runs ~2 whole rounds), 921-934 vs
+    # 949 us per clip at 448 (profiles/r05zd_batch_sweep.jsonl, r05ze_batch_sweep.jsonl)
+    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M", batch=896),
     "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M"),  # C4
     "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti",  # C1 / C2 shape
                 batch=512),
@@ -87,9 +90,10 @@ def _args():
     a = ap.parse_args()
     a.batch_default = a.batch is None
     if a.batch is None:
-        # 448 clips per GPU: the single-pass scan grid (9 workgroups per clip, 8 resident per
-        # CU) runs ~2 full rounds; at 336 (1.5 rounds) the dt_proj-in-scan kernel loses 15 %
-        # in the partial second round (profiles/r03c_batch_sweep.txt)
+        # 448 clips per launch: the single-pass scan grid (9 workgroups per clip, 8 resident
+        # per CU) runs ~2 full rounds; at 336 (1.5 rounds) the dt_proj-in-scan kernel loses
+        # 15 % in the partial second round (profiles/r03c_batch_sweep.txt).  M-16f runs two
+        # such launches side by side (CONFIGS)
         a.batch = CONFIGS[a.config].get("batch", 448)
     return a
 
@@ -611,11 +615,13 @@ def main():
                 "non-finite B=1 chunk output"
         from videomamba_amd.mamba_simple import mixer_layout
         mx0 = model.layers[0].mixer
+        # the scan as the step launches it: one sub-batch stream's clips per launch
+        rb = max(B // _sub_batch_streams(B), 1)
         hn0 = torch.empty((1, 1, cfg["embed_dim"]), device=device,
-                          dtype=torch.bfloat16).expand(max(B, 1), 3144, cfg["embed_dim"])
+                          dtype=torch.bfloat16).expand(rb, 3144, cfg["embed_dim"])
         _progress("scan roofline leg")
-        roof = scan_roofline(max(B, 1), args.scan_reps, device,
-                             mixer_layout(max(B, 1), cfg["embed_dim"] * 2, device),
+        roof = scan_roofline(rb, args.scan_reps, device,
+                             mixer_layout(rb, cfg["embed_dim"] * 2, device),
                              dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))
         b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 and not args.no_b1 else None
 

@@ -858,16 +858,18 @@ def test_c3_m_16f_bf16_bench_kernels_match_oracle():
     torch.testing.assert_close(xv[:1].float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
 
 
-def test_c3_bench_batch_448_clips_bitwise_equal_small_batch_and_oracle():
+def test_c3_bench_batch_896_clips_bitwise_equal_small_batch_and_oracle():
     """Correctness at the benched batch: the bench's exact C3 call —
-    VideoMamba-M 16x224^2 bf16, bf16 zero state, offset 0, cls+avg — at B = 448, where xz is
+    VideoMamba-M 16x224^2 bf16, bf16 zero state, offset 0, cls+avg — at B = 896, which the
+    forward runs as two 448-clip sub-batch streams (options.batch_streams): per launch xz is
     6.5 GB and u / y 3.2 GB (past every 31-bit buffer offset; the persistent projection GEMM,
     the wide conv_proj without dt rows and the dt_proj-in-scan single-pass scan).  Clips
-    {0, 1, 223, 446, 447} of x_vis, x_pool and every layer's returned (conv, ssm) state are
-    bit-equal to the same clips run in a B = 9 batch with scan_segments = 1 (the same kernel
-    forms at small extents: every form is row-invariant by design), and clip 447 matches
-    orc.encoder_forward at the C3 tolerances (relative L2 <= 1e-2; reference
-    videomamba.py:943-1067, mamba_simple.py:331-339, :443-446)."""
+    {0, 1, 447, 448, 894, 895} (both sides of the sub-batch boundary) of x_vis, x_pool and
+    every layer's returned (conv, ssm) state are bit-equal to the same clips run in a B = 9
+    batch with scan_segments = 1 (the same kernel forms at small extents: every form is
+    row-invariant by design), and clip 895 matches orc.encoder_forward at the C3 tolerances
+    (relative L2 <= 1e-2; reference videomamba.py:943-1067, mamba_simple.py:331-339,
+    :443-446)."""
     torch.manual_seed(0)
     model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
     with torch.no_grad():
@@ -875,15 +877,17 @@ def test_c3_bench_batch_448_clips_bitwise_equal_small_batch_and_oracle():
     model = model.to(torch.bfloat16).eval()
     p = {k: v.detach().clone() for k, v in model.state_dict().items()}
     model = model.to(DEV)
-    B, picks = 448, [0, 1, 223, 446, 447]
+    B, picks = 896, [0, 1, 447, 448, 894, 895]
+    half = B // options.get().batch_streams
+    assert options.get().batch_streams == 2 and B >= options.get().batch_stream_min_clips
     g = torch.Generator(device=DEV).manual_seed(448)
     x = torch.empty(B, 3, 16, 224, 224, device=DEV, dtype=torch.bfloat16)
     for i in range(0, B, 64):
         x[i:i + 64] = torch.randn(min(64, B - i), 3, 16, 224, 224, device=DEV, generator=g)
     mx = model.layers[0].mixer
-    hn = torch.empty(1, 1, 576, device=DEV, dtype=torch.bfloat16).expand(B, 3144, 576)
+    hn = torch.empty(1, 1, 576, device=DEV, dtype=torch.bfloat16).expand(half, 3144, 576)
     assert mx._dtp_ok(hn, 3137)  # the bench's scan: dt_proj inside the single-pass scan
-    assert B * 3144 * 2304 * 2 > 2 ** 31 and B * 3144 * 1152 * 2 > 2 ** 31  # xz, u / y
+    assert half * 3144 * 2304 * 2 > 2 ** 31 and half * 3144 * 1152 * 2 > 2 ** 31  # xz, u / y
     with torch.no_grad():
         st = model.allocate_state(B, dtype=torch.bfloat16, device=DEV)
         xv, xp, st = model(x, ssm_state=st, temporal_pos_offset=0)
@@ -892,8 +896,8 @@ def test_c3_bench_batch_448_clips_bitwise_equal_small_batch_and_oracle():
         big_v = xv[picks].clone()
         big_p = xp[picks].clone()
         big_s = [(c[picks].clone(), s[picks].clone()) for c, s in st]
-        x9 = torch.cat([x[picks], x[2:6]]).contiguous()  # 9 clips, the picks first
-        x447 = x[447:448].cpu()
+        x9 = torch.cat([x[picks], x[2:5]]).contiguous()  # 9 clips, the picks first
+        xlast = x[B - 1:B].cpu()
         del xv, xp, st, x
         torch.cuda.empty_cache()
         st9 = model.allocate_state(9, dtype=torch.bfloat16, device=DEV)
@@ -910,10 +914,10 @@ def test_c3_bench_batch_448_clips_bitwise_equal_small_batch_and_oracle():
     ost = [(torch.zeros(1, 1152, 4, dtype=torch.bfloat16),
             torch.zeros(1, 1152, 16, dtype=torch.bfloat16)) for _ in range(32)]
     torch.set_num_threads(16)
-    ref_v, ref_p, ref_st = orc.encoder_forward(p, cfg, x447, state=ost, temporal_pos_offset=0)
+    ref_v, ref_p, ref_st = orc.encoder_forward(p, cfg, xlast, state=ost, temporal_pos_offset=0)
     rv, rp = _rel(big_v[-1:].cpu(), ref_v), _rel(big_p[-1:].cpu(), ref_p)
     rs = max(_rel(big_s[i][1][-1:].cpu(), ref_st[i][1]) for i in range(32))
-    print(f"C3 B=448 clip 447 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e}")
+    print(f"C3 B=896 clip 895 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e}")
     assert rv <= 1e-2 and rp <= 1e-2 and rs <= 1e-2, (rv, rp, rs)
 
 
