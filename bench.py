@@ -11,8 +11,9 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
-Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 448 clips per rank by default, so
-the 1/2/4/8-GPU curve keeps every GPU at the batch where the scan holds its occupancy —
+Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 896 clips per rank by default, two
+448-clip sub-batch streams as in C3, so the 1/2/4/8-GPU curve keeps every GPU at the batch
+where the scan holds its occupancy —
 weak scaling; --global-batch G instead splits G clips across ranks with
 sharding.shard_range — strong scaling; run under torchrun for the 8-GPU case), --config ti8
 --full-sequence (C2).  The metric name follows the config ("<model> <T>f 224").  The
@@ -59,7 +60,9 @@ CONFIGS = {
     # each launch keeps the 448-clip shape whose scan grid runs ~2 whole rounds), 921-934 vs
     # 949 us per clip at 448 (profiles/r05zd_batch_sweep.jsonl, r05ze_batch_sweep.jsonl)
     "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M", batch=896),
-    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M"),  # C4
+    # C4: the same 896 clips per GPU (profiles/r05zg_*: 3.373 M at 896 with two streams,
+    # 3.316 M at 448 on one stream, 3.263 M at 448 as two 224-clip streams)
+    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M", batch=896),
     "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti",  # C1 / C2 shape
                 batch=512),
 }
@@ -85,6 +88,8 @@ def _args():
                     help="oracle threads (0: every CPU this process may use, see _cpu_share)")
     ap.add_argument("--scan-dt-proj", default="auto", choices=("auto", "on", "off"),
                     help="options.scan_dt_proj: dt_proj inside the scan at chip-filling batches")
+    ap.add_argument("--batch-streams", type=int, default=0,
+                    help="options.batch_streams (sub-batch HIP streams per forward; 0: default)")
     ap.add_argument("--full-sequence", action="store_true",
                     help="stateless full-sequence forward (C2) instead of a stateful chunk")
     a = ap.parse_args()
@@ -551,6 +556,8 @@ def main():
     from videomamba_amd.videomamba import PretrainVideoMamba
 
     options.get().scan_dt_proj = args.scan_dt_proj
+    if args.batch_streams > 0:
+        options.get().batch_streams = args.batch_streams
     cfg = CONFIGS[args.config]
     torch.manual_seed(0)
     model = PretrainVideoMamba(depth=cfg["depth"], embed_dim=cfg["embed_dim"],

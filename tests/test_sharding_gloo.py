@@ -94,14 +94,15 @@ def test_bench_control_flow_world2_weak_scaling():
     assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
 
 
-def test_bench_control_flow_world2_m32_default_is_weak_448_per_rank():
-    """C4 (--config m32) without --global-batch keeps 448 clips per rank (the batch where
+def test_bench_control_flow_world2_m32_default_is_weak_896_per_rank():
+    """C4 (--config m32) without --global-batch keeps 896 clips per rank (two 448-clip
+    sub-batch streams, as C3; 448 per launch is the batch where
     the scan holds its occupancy; 84 per GPU at N = 8 from a fixed 672 would have measured
-    the batch choice, not the sharding): weak scaling, global batch = world x 448, and the
+    the batch choice, not the sharding): weak scaling, global batch = world x 896, and the
     metric names the workload actually run."""
     line = _bench_stub(["--config", "m32"])
     assert line["scaling"] == "weak"
-    assert line["config"]["per_gpu_batch"] == 448 and line["config"]["global_batch"] == 896
+    assert line["config"]["per_gpu_batch"] == 896 and line["config"]["global_batch"] == 1792
     assert line["metric"].endswith("VideoMamba-M 32f 224")
     assert _bench_stub(["--config", "ti8"])["metric"].endswith("VideoMamba-Ti 8f 224")
 
