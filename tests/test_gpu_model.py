@@ -1218,3 +1218,34 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
         assert len(a_step) == len(b_step)
         for a, b in zip(a_step, b_step):
             assert a.shape == b.shape and torch.equal(a, b), (a.float() - b.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("bsz", [1, 2])
+def test_in_proj_z_stream_is_bitwise_the_one_launch_in_proj(bsz):
+    """options.in_proj_z_stream: at streaming batches in_proj runs as its x half on the
+    current stream and its z half on a side stream beside conv_proj.  VideoMamba-M 16x224^2
+    bf16 stateful chunks (two, so the carried states are compared too): x_vis, x_pool and
+    every layer's states bit-equal to the one-launch in_proj, eagerly and through the
+    captured hipGraph (the side stream is a graph branch)."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    model = _m_model(16, add_pool_norm=True)
+    model.pool_type = "cls+avg"
+    g = torch.Generator(device=DEV).manual_seed(21)
+    x = torch.randn(bsz, 3, 16, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+    res = {}
+    for split in (False, True):
+        st = model.allocate_state(bsz, dtype=torch.bfloat16, device=DEV)
+        outs = []
+        with options.override(in_proj_z_stream=split), torch.no_grad():
+            for _ in range(2):
+                xv, xp, st = model(x, ssm_state=st, temporal_pos_offset=0)
+                outs += [xv.clone(), xp.clone()] + [t.clone() for c in st for t in c]
+        torch.cuda.synchronize()
+        res[split] = outs
+    assert all(torch.equal(a, b) for a, b in zip(res[False], res[True]))
+    if bsz == 1:
+        with options.override(in_proj_z_stream=True), torch.no_grad():
+            runner = StreamingChunkGraph(model, batch=1, frames=16)
+            gv, gp = runner.run(x, temporal_pos_offset=0)
+            torch.cuda.synchronize()
+        assert torch.equal(gv, res[True][0]) and torch.equal(gp, res[True][1])

@@ -104,6 +104,18 @@ def _linear_into(x: Tensor, w: Tensor, b: Optional[Tensor], out: Tensor,
         return torch.addmm(b.to(out.dtype), x, w.t(), out=out)
 
 
+_Z_STREAMS = {}
+
+
+def _z_stream(device: torch.device) -> torch.cuda.Stream:
+    """The side stream the small-batch mixer runs in_proj's z half on (one per device)."""
+    key = (device.type, device.index)
+    s = _Z_STREAMS.get(key)
+    if s is None:
+        s = _Z_STREAMS[key] = torch.cuda.Stream(device)
+    return s
+
+
 def _matmul(a: Tensor, b: Tensor) -> Tensor:
     with tuned():
         return torch.matmul(a, b)
@@ -339,7 +351,24 @@ class Mamba(nn.Module):
         stream = torch.cuda.current_stream(hn.device).cuda_stream
         _, _, _, cw, cb = self._fp32_params()
         s_u, s_xz = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm)
-        if bufs is None:
+        z_side = None
+        if bufs is None and self._split_in_proj_ok(hn, Bsz):
+            # in_proj as two launches: x (what conv_proj needs) here, z (what only the scan's
+            # gate reads) on a side stream, so it runs beside conv_proj; the current stream
+            # waits for it before returning.  Every row of either half is the same MFMA
+            # chain as in the one-launch GEMM (the HIP GEMM's rows do not depend on n).
+            h2 = hn.view(n, C)
+            w = self.in_proj.weight
+            xz = torch.empty((n, 2 * Dm), dtype=hn.dtype, device=hn.device)
+            K.linear(h2, w[:Dm], out=xz[:, :Dm])
+            cur = torch.cuda.current_stream(hn.device)
+            z_side = _z_stream(hn.device)
+            z_side.wait_stream(cur)
+            with torch.cuda.stream(z_side):
+                K.linear(h2, w[Dm:], out=xz[:, Dm:])
+            u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            x_dbl = dt = None
+        elif bufs is None:
             xz = _linear(hn.view(n, C), self.in_proj.weight, self.in_proj.bias,
                          clips=Bsz)  # (n, 2D)
             u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
@@ -373,7 +402,22 @@ class Mamba(nn.Module):
             else:
                 _linear_into(u, self.x_proj.weight, None, x_dbl)
                 _linear_into(x_dbl[:, :R], self.dt_proj.weight, None, dt)
+        if z_side is not None:  # the z half is complete before anything after this reads xz
+            torch.cuda.current_stream(hn.device).wait_stream(z_side)
         return xz, u, x_dbl, dt
+
+    def _split_in_proj_ok(self, hn: Tensor, clips: int) -> bool:
+        """in_proj runs as x / z halves on two streams (``options.in_proj_z_stream``) at
+        streaming batches (``clips <= options.in_proj_split_clips``), where every kernel of
+        the layer is latency-bound and conv_proj can share the CUs with the z half; the HIP
+        GEMM must take both halves (bf16, no bias; n = d_inner per half)."""
+        o = options.get()
+        if not o.in_proj_z_stream or clips > o.in_proj_split_clips or self.in_proj.bias is not None:
+            return False
+        n = hn.shape[0] * hn.shape[1]
+        w = self.in_proj.weight
+        return (_small_gemm_ok(hn.view(n, hn.shape[2]), w[:self.d_inner], None, clips=clips)
+                and (self.d_inner * w.stride(0) * w.element_size()) % 16 == 0)
 
     def _forward_padded_tm(self, hn, seqlen, conv_state_in, conv_state_out, h0, h_last,
                            next_norm=None):

@@ -58,6 +58,13 @@ documented options object; tests and sweeps change them with :func:`override`.
     batch_stream_min_clips
                      the smallest batch that is split (default 448: parts of >= 224 clips,
                      a whole round of the dt_proj-in-scan grid each).
+    in_proj_z_stream False (default): True makes the mixer at streaming batches (at most
+                     ``in_proj_split_clips`` clips, default 8) run in_proj as two launches,
+                     the x half on the current stream and the z half (read only by the scan's
+                     gate) on a side stream beside conv_proj; bit-identical (the HIP GEMM's
+                     rows do not depend on the column count).  Measured slower: the B = 1
+                     graph replay 2.97-2.99 vs 2.56-2.58 ms (each cross-stream edge of the
+                     replayed graph costs more than the z half's ~6 us), so it is off.
     small_gemm_rows  ("library" mode) in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -92,6 +99,8 @@ class Options:
     row_invariant_gemm_clips: int = 8
     fuse_out_norm: bool = False
     batch_streams: int = 2
+    in_proj_z_stream: bool = False
+    in_proj_split_clips: int = 8
     batch_stream_min_clips: int = 448
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
