@@ -107,6 +107,11 @@ VARIANTS = {
     # leaving a wave slot per SIMD for another stream's kernel
     "dtp_occ3": [("vm_scan_seq.hip", "    case 3: hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 0, s, p, q); break;",
                   "    case 3: hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 5120, s, p, q); break;")],
+    # add_rms_bf16_kernel with non-temporal (nt) loads / stores
+    "an_ld_nt": [("vm_norm.hip", '    const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);\n    xq[j][0] = q[0];', '    const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 2);\n    xq[j][0] = q[0];'),
+                 ("vm_norm.hip", '    if constexpr (RES) rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));', '    if constexpr (RES) rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 2));')],
+    "an_st_nt": [("vm_norm.hip", '    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);\n    if constexpr (RO) {', '    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 2);\n    if constexpr (RO) {'),
+                 ("vm_norm.hip", '      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);\n    }\n  }\n}', '      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 2);\n    }\n  }\n}')],
     "tg_prio1": [("vm_gemm_tile.hip", "constexpr int kTilePrio = 0;", "constexpr int kTilePrio = 1;")],
     # persistent GEMM phase timestamps (scripts/diag/gemm_stamps.py)
     "tg_stamp": [("vm_gemm_tile.hip", "constexpr bool kTileStamps = false;\n\n}  // namespace\n\n__device__ void tg_stamp_sink(int idx, unsigned long long t);",
