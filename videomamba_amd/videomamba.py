@@ -734,8 +734,8 @@ class PretrainVideoMamba(nn.Module):
             def layer(idx):
                 old = self._get_layer_state(ssm_state, idx)
                 return (conv_new[idx], old[1])  # the ssm state advanced in place
-            if isinstance(ssm_state, dict):
-                st = {k: layer(k) for k in ssm_state}
+            if isinstance(ssm_state, dict):  # as the one-stream path: one entry per layer
+                st = {idx: layer(idx) for idx in range(depth)}
             else:
                 items = [layer(idx) for idx in range(depth)]
                 st = tuple(items) if isinstance(ssm_state, tuple) else items
