@@ -1161,8 +1161,9 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
     projections).  Every kernel's rows are batch-independent, so x_vis, x_pool and every
     returned state are bit-equal to the one-stream forward — over two stateful chunks (the
     ssm states advanced in place in the caller's tensors, new conv states), for list / tuple
-    / dict / legacy ssm-only state containers, masks and keep_temporal pooling; uneven part
-    sizes (7 clips in 2 or 3 parts)."""
+    / dict / legacy ssm-only state containers and keep_temporal pooling; uneven part sizes
+    (7 clips in 2 or 3 parts).  A masked forward stays on one stream (its equal-visible-count
+    check spans the whole batch)."""
     torch.manual_seed(5)
     model = PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=64, channels=3,
                                kernel_size=1, num_frames=4, pool_type="avg",

@@ -516,7 +516,7 @@ class PretrainVideoMamba(nn.Module):
                 return False
         return True
 
-    def _final_norm_pool(self, h, residual, L, has_cls, visible, pool):
+    def _final_norm_pool(self, h, residual, L, has_cls, visible, pool, out=None):
         """Final add + norm of the padded buffer straight into contiguous (B, L, C)
         features, fused with the pooling sums (``vm_norm_pool_fwd``), then the pool tail
         (``vm_pool_finish_fwd``): (features, x_pool | None).  ``pool`` is None (no pooling)
@@ -551,7 +551,7 @@ class PretrainVideoMamba(nn.Module):
                     groups, group_rows = tt, 0
         feats, ws = K.norm_pool(h, residual, L, w32, b32, eps, is_rms, head=head,
                                 groups=groups, group_rows=group_rows, bounds=bounds,
-                                max_group_rows=max_rows, sums=sums)
+                                max_group_rows=max_rows, sums=sums, out=out)
         if pool is None:
             return feats, None
         pn = self.pool_norm
@@ -606,9 +606,12 @@ class PretrainVideoMamba(nn.Module):
         return feats if ssm_state is None else (feats, st)
 
     def _encode(self, x, mask, ssm_state, temporal_pos_offset, tpos=None, pool=None,
-                conv_out=None):
-        """(features (B, N_vis, C), x_pool | None, state result | None)."""
-        parts = self._stream_parts(x, ssm_state, tpos, conv_out)
+                conv_out=None, feats_out=None, split=True):
+        """(features (B, N_vis, C), x_pool | None, state result | None).  ``feats_out``: a
+        (B, N_vis, C) buffer with contiguous rows the features are written into; ``split``
+        False keeps this call on the current stream (a sub-batch never splits again)."""
+        parts = (self._stream_parts(x, ssm_state, tpos, conv_out)
+                 if split and mask is None and feats_out is None else 1)
         if parts > 1:
             return self._encode_streams(x, mask, ssm_state, temporal_pos_offset, pool, parts)
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
@@ -623,7 +626,8 @@ class PretrainVideoMamba(nn.Module):
             h[:, :L] = gathered
 
         h, residual, new_states, tuple_out = self._run_layers(h, None, L, ssm_state, conv_out)
-        feats, x_pool = self._final_norm_pool(h, residual, L, has_cls, visible, pool)
+        feats, x_pool = self._final_norm_pool(h, residual, L, has_cls, visible, pool,
+                                              out=feats_out)
 
         if new_states is not None and isinstance(new_states, list):
             if any(s is None for s in new_states):
@@ -714,6 +718,12 @@ class PretrainVideoMamba(nn.Module):
             items = [sl(v) for v in ssm_state]
             return tuple(items) if isinstance(ssm_state, tuple) else items
 
+        # every part writes its rows of one features buffer (no concatenation pass)
+        has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
+        gh, gw = self._spatial_token_grid(x.shape[-2], x.shape[-1])
+        L = self._validate_temporal_length(x.shape[2]) * gh * gw + (1 if has_cls else 0)
+        feats = torch.empty((B, L, self.embed_dim), dtype=self.patch_embed.proj.weight.dtype,
+                            device=dev)
         outs = []
         for i in range(parts):
             a, b = cut[i], cut[i + 1]
@@ -721,12 +731,11 @@ class PretrainVideoMamba(nn.Module):
             s.wait_stream(cur)
             with torch.cuda.stream(s):
                 outs.append(self._encode(
-                    x[a:b], None if mask is None else mask[a:b], part_state(a, b),
-                    temporal_pos_offset, pool=pool,
-                    conv_out=None if conv_new is None else conv_new[:, a:b]))
+                    x[a:b], None, part_state(a, b), temporal_pos_offset, pool=pool,
+                    conv_out=None if conv_new is None else conv_new[:, a:b],
+                    feats_out=feats[a:b], split=False))
         for s in streams[:parts]:
             cur.wait_stream(s)
-        feats = torch.cat([o[0] for o in outs], 0)
         x_pool = None if outs[0][1] is None else torch.cat([o[1] for o in outs], 0)
         if ssm_state is None:
             st = None
