@@ -245,11 +245,14 @@ _SIDE_STREAMS: Dict[Any, List[torch.cuda.Stream]] = {}
 
 
 def _side_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
-    """n persistent HIP streams of ``device`` for sub-batch forwards (created once)."""
+    """n persistent HIP streams of ``device`` for sub-batch forwards (created once).  The
+    first runs at high priority: its kernels dispatch first, so the halves drift apart and
+    one's scan meets the other's memory-bound kernels more often (B = 896: 825-831 vs
+    838-843 ms per step, profiles/r05zn_stream_priority.jsonl)."""
     key = (device.type, device.index)
     have = _SIDE_STREAMS.setdefault(key, [])
     while len(have) < n:
-        have.append(torch.cuda.Stream(device))
+        have.append(torch.cuda.Stream(device, priority=-1 if not have else 0))
     return have[:n]
 
 
