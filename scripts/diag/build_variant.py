@@ -336,6 +336,28 @@ VARIANTS = {
     "bc_fixed": [("vm_scan_seq.hip",
                   "      bc_load(min(t + 1, tlast), bcw[(j + 1) & 1]);",
                   "      bc_load(t_beg, bcw[(j + 1) & 1]);")],
+    # B = 1 patch kernel (patch_mfma16_kernel) cost split: two k-steps only / no
+    # positional loads in the epilogue / no head+pad rows (results wrong)
+    "pt_k2": [("vm_patch.hip", "  for (int kk = 0; kk < p.K; kk += 64) {\n    load(kk + 32, a1, b1);",
+               "  for (int kk = 0; kk < 64; kk += 64) {\n    load(kk + 32, a1, b1);")],
+    "pt_noepi": [("vm_patch.hip",
+                  "    svs[it] = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);\n"
+                  "    tvs[it] = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);\n"
+                  "    orow[it] = ok ? b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n : -1;\n"
+                  "    soff[it] = ml * (kPN + 8) + c8;",
+                  "    svs[it] = make_uint4(sp, 0, 0, 0);\n    tvs[it] = make_uint4(t, 0, 0, 0);\n"
+                  "    orow[it] = ok ? b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n : -1;\n"
+                  "    soff[it] = ml * (kPN + 8) + c8;")],
+
+    # the B = 1 patch kernel returning at once (the launch + event floor) / two k-steps and
+    # no output stores (results wrong)
+    "pt_empty": [("vm_patch.hip", "  __shared__ __attribute__((aligned(16))) bf16_t stile[kPT * (kPN + 8)];\n  const int tid = threadIdx.x;",
+                  "  __shared__ __attribute__((aligned(16))) bf16_t stile[kPT * (kPN + 8)];\n  if (p.M > 0) return;\n  const int tid = threadIdx.x;")],
+    "pt_k2_nost": [("vm_patch.hip", "  for (int kk = 0; kk < p.K; kk += 64) {\n    load(kk + 32, a1, b1);",
+                    "  for (int kk = 0; kk < 64; kk += 64) {\n    load(kk + 32, a1, b1);"),
+                   ("vm_patch.hip", "    *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);\n  }\n  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);",
+                    "    if (ow[0] == 0x12345678u) *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);\n  }\n  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);")],
+
 }
 
 

@@ -33,18 +33,18 @@ struct PatchParams {
 };
 
 // The rows of the padded token buffer around the patch tokens, written by the launch's
-// blockIdx.y == 0 workgroups after their tiles (the scalar fallback: before) (grid-stride over batch x rows x channels):
+// channel-tile-0 workgroups (block bx of nbx along the tokens, channel tile by) after their tiles (the scalar fallback: before) (grid-stride over batch x rows x channels):
 // the CLS rows [0, row0) = e(cls + cls_pos) — the reference's cls_token + pos_embed[:, :1]
 // in the model dtype (videomamba.py:806-815) — and pad_rows zero rows after the last token.
 // Folded in here they cost no launches of their own (three small torch kernels before).
 template <typename T>
-__device__ __forceinline__ void patch_frame_rows(const PatchParams& p) {
+__device__ __forceinline__ void patch_frame_rows(const PatchParams& p, int bx, int nbx, int by) {
   const int head = p.cls ? p.row0 : 0;
   const int per_b = head + p.pad_rows;
-  if (blockIdx.y != 0 || per_b == 0) return;
+  if (by != 0 || per_b == 0) return;
   const int ntok = p.tt * p.gh * p.gw;
   const int total = p.batch * per_b * p.embed;  // < 2^31 (checked on the host)
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+  for (int i = bx * blockDim.x + threadIdx.x; i < total; i += nbx * blockDim.x) {
     const int br = i / p.embed;
     const int c = i - br * p.embed;
     const int b = br / per_b;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void patch_mfma_kernel(const PatchParams p) {
         const int n = n0 + j * 16 + r;
         if (m < p.M && n < p.embed) patch_store<bf16_t>(p, m, n, acc[i][j][e]);
       }
-  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
+  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);  // after the tile: the head / padding rows never delay it
 }
 
 // 16x16 patches, bf16, embed % 192 == 0 (the VideoMamba shapes): workgroup tile
@@ -176,13 +176,11 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
   // lane's k within a 32-wide k-step: patch row 2*step + (kg >> 1), columns (kg & 1) * 8
   const long long lane_k = (long long)(kg >> 1) * p.width + (kg & 1) * 8;
 
-  long long abase[2];
-  bool mval[2];
+  long long abase[2];  // rows past the last token read token 0 (their outputs are never stored)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + i * 16 + r;
-    mval[i] = m < p.M;
-    abase[i] = token_base(p, mval[i] ? m : 0) + lane_k;
+    abase[i] = token_base(p, m < p.M ? m : 0) + lane_k;
   }
   const bf16_t* wrow[kPJ];
 #pragma unroll
@@ -193,26 +191,39 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
 #pragma unroll
     for (int j = 0; j < kPJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bf16x8 zero = {};
   const int steps_per_c = 8 * p.kt;  // 256 * kt k per input channel, 32 per step
-  for (int kk = 0; kk < p.K; kk += 32) {
+  // two register sets of operands, ping-ponged: one k-step's loads are in flight while
+  // the other's 12 MFMAs run.  16x16 patches make K = 256 * cin * kt, a whole number of
+  // step pairs, so every load and MFMA is unconditional (the last pair's look-ahead load is
+  // clamped to the last step): no register copies close the loop and nothing is sunk into a
+  // branch, so the waits stay counted instead of draining every load each step.
+  auto load = [&](int kk, bf16x8 (&ra)[2], bf16x8 (&rb)[kPJ]) {
     const int step = kk >> 5;
     const int ci = step / steps_per_c;
     const int sr = step - ci * steps_per_c;  // (kz, row pair) within the channel
     const int kz = sr >> 3;
     const long long koff = ci * plane + (long long)kz * p.height * p.width +
                            (long long)(2 * (sr & 7)) * p.width;
-    bf16x8 a[2], b[kPJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      a[i] = mval[i] ? *reinterpret_cast<const bf16x8*>(vid + abase[i] + koff) : zero;
+    for (int i = 0; i < 2; ++i) ra[i] = *reinterpret_cast<const bf16x8*>(vid + abase[i] + koff);
 #pragma unroll
-    for (int j = 0; j < kPJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kk);
+    for (int j = 0; j < kPJ; ++j) rb[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kk);
+  };
+  auto mma = [&](const bf16x8 (&ra)[2], const bf16x8 (&rb)[kPJ]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < kPJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[i], rb[j], acc[i][j], 0, 0, 0);
+  };
+  const int klast = p.K - 32;
+  bf16x8 a0[2], b0[kPJ], a1[2], b1[kPJ];
+  load(0, a0, b0);
+  for (int kk = 0; kk < p.K; kk += 64) {
+    load(kk + 32, a1, b1);
+    mma(a0, b0);
+    load(min(kk + 64, klast), a0, b0);
+    mma(a1, b1);
   }
   // stage round(acc + bias) (the conv output's rounding point) as bf16 [token][channel]
 #pragma unroll
@@ -234,21 +245,36 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
   const bf16_t* spos = static_cast<const bf16_t*>(p.spos);
   const bf16_t* tpos = static_cast<const bf16_t*>(p.tpos);
   bf16_t* out = static_cast<bf16_t*>(p.out);
-  for (int idx = tid; idx < kPT * (kPN / 8); idx += 256) {
+  // the positional loads of all 6 chunks first, then the adds and stores: one L2 round
+  // trip per tile instead of one per chunk (each store would otherwise order the next loads)
+  constexpr int kEpi = kPT * (kPN / 8) / 256;
+  uint4 svs[kEpi], tvs[kEpi];
+  long long orow[kEpi];
+  int soff[kEpi];
+#pragma unroll
+  for (int it = 0; it < kEpi; ++it) {
+    const int idx = tid + it * 256;
     const int ml = idx / (kPN / 8);
     const int c8 = (idx - ml * (kPN / 8)) * 8;
     const int m = mt0 + ml;
-    if (m >= p.M) continue;
-    const int b = m / per_b;
-    const int rem = m - b * per_b;
+    const bool ok = m < p.M;
+    const int b = ok ? m / per_b : 0;
+    const int rem = ok ? m - b * per_b : 0;
     const int t = rem / hw;
     const int sp = rem - t * hw;
     const int n = blockIdx.y * kPN + c8;
-    const uint4 cv = *reinterpret_cast<const uint4*>(&stile[ml * (kPN + 8) + c8]);
-    const uint4 sv = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
-    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
-    const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w},
-                   tw[4] = {tv.x, tv.y, tv.z, tv.w};
+    svs[it] = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
+    tvs[it] = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
+    orow[it] = ok ? b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n : -1;
+    soff[it] = ml * (kPN + 8) + c8;
+  }
+#pragma unroll
+  for (int it = 0; it < kEpi; ++it) {
+    if (orow[it] < 0) continue;
+    const uint4 cv = *reinterpret_cast<const uint4*>(&stile[soff[it]]);
+    const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w},
+                   sw[4] = {svs[it].x, svs[it].y, svs[it].z, svs[it].w},
+                   tw[4] = {tvs[it].x, tvs[it].y, tvs[it].z, tvs[it].w};
     uint32_t ow[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -263,10 +289,9 @@ __global__ __launch_bounds__(256) void patch_mfma16_kernel(const PatchParams p) 
       ow[q] = static_cast<uint32_t>(from_f32<bf16_t>(o[0])) |
               (static_cast<uint32_t>(from_f32<bf16_t>(o[1])) << 16);
     }
-    *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
-        make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
-  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
+  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);  // after the tile: the head / padding rows never delay it
 }
 
 // 16x16 patches, bf16, embed % 192 == 0, an LDS-staged GEMM: workgroup tile 128 tokens x
@@ -281,8 +306,15 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[kGT * (kGN + 8)];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int mt0 = blockIdx.x * kGT;
-  const int nt0 = blockIdx.y * kGN;
+  // XCD-grouped tile order (one linear grid): ids g * 8 * nn + ni * 8 + x hold token tile
+  // g * 8 + x, channel tile ni, so the nn channel tiles of one token tile share the id's
+  // residue mod 8 — the same XCD — and read their video patches through one L2.
+  const int nn = p.embed / kGN, nm = (p.M + kGT - 1) / kGT;
+  const int grp = blockIdx.x / (8 * nn), rg = blockIdx.x - grp * 8 * nn;
+  const int mti = grp * 8 + (rg & 7), nti = rg >> 3;
+  if (mti >= nm) return;  // the last group's missing token tiles (before any barrier)
+  const int mt0 = mti * kGT;
+  const int nt0 = nti * kGN;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 96;
   const int r16 = lane & 15, kg = lane >> 4;
   const bf16_t* vid = static_cast<const bf16_t*>(p.video);
@@ -293,14 +325,12 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
   // staging roles: A: 512 16-byte chunks (row = idx >> 2, c = idx & 3) -> 2 per thread;
   //                B: 768 chunks -> 3 per thread
   long long abase[2];
-  bool aval[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int idx = tid + q * 256;
     const int row = idx >> 2, c = idx & 3;
     const int m = mt0 + row;
-    aval[q] = m < p.M;
-    abase[q] = token_base(p, aval[q] ? m : 0) + (long long)(c >> 1) * p.width + (c & 1) * 8;
+    abase[q] = token_base(p, m < p.M ? m : 0) + (long long)(c >> 1) * p.width + (c & 1) * 8;
   }
   auto koff_of = [&](int kk) {
     const int step = kk >> 5;
@@ -310,32 +340,29 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
     return ci * plane + (long long)(sr >> 3) * p.height * p.width +
            (long long)(2 * (sr & 7)) * p.width;
   };
-  uint4 ra[2], rb[3];
+  // the staged chunks in named registers: as arrays the compiler kept the weight chunks in
+  // scratch, and each k-step waited for their loads before its MFMAs
+  uint4 ra0, ra1, rb0, rb1, rb2;
+  const int brow = tid >> 2, bc = (tid & 3) * 8;  // B chunk q: row brow + 64 q, column bc
   auto fetch = [&](int kk) {
     const long long ko = koff_of(kk);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      ra[q] = aval[q] ? *reinterpret_cast<const uint4*>(vid + abase[q] + ko) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int idx = tid + q * 256;
-      const int row = idx >> 2, c = idx & 3;
-      rb[q] = *reinterpret_cast<const uint4*>(wt + (long long)(nt0 + row) * p.K + kk + c * 8);
-    }
+    // rows past the last token read token 0's pixels (abase): their outputs are never
+    // stored, and no branch here lets the loads stay in flight across the MFMAs
+    ra0 = *reinterpret_cast<const uint4*>(vid + abase[0] + ko);
+    ra1 = *reinterpret_cast<const uint4*>(vid + abase[1] + ko);
+    const bf16_t* wb = wt + (long long)(nt0 + brow) * p.K + kk + bc;
+    rb0 = *reinterpret_cast<const uint4*>(wb);
+    rb1 = *reinterpret_cast<const uint4*>(wb + 64LL * p.K);
+    rb2 = *reinterpret_cast<const uint4*>(wb + 128LL * p.K);
   };
   auto put = [&](int buf) {
-    bf16_t* sa = smem + buf * kBuf;
-    bf16_t* sb = sa + kA;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int idx = tid + q * 256;
-      *reinterpret_cast<uint4*>(sa + (idx >> 2) * kGP + (idx & 3) * 8) = ra[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int idx = tid + q * 256;
-      *reinterpret_cast<uint4*>(sb + (idx >> 2) * kGP + (idx & 3) * 8) = rb[q];
-    }
+    bf16_t* sa = smem + buf * kBuf + brow * kGP + bc;  // A chunk q: row brow + 64 q
+    bf16_t* sb = smem + buf * kBuf + kA + brow * kGP + bc;
+    *reinterpret_cast<uint4*>(sa) = ra0;
+    *reinterpret_cast<uint4*>(sa + 64 * kGP) = ra1;
+    *reinterpret_cast<uint4*>(sb) = rb0;
+    *reinterpret_cast<uint4*>(sb + 64 * kGP) = rb1;
+    *reinterpret_cast<uint4*>(sb + 128 * kGP) = rb2;
   };
 
   f32x4 acc[4][6];
@@ -386,44 +413,61 @@ __global__ __launch_bounds__(256) void patch_gemm_kernel(const PatchParams p) {
   const bf16_t* spos = static_cast<const bf16_t*>(p.spos);
   const bf16_t* tpos = static_cast<const bf16_t*>(p.tpos);
   bf16_t* out = static_cast<bf16_t*>(p.out);
-  for (int idx = tid; idx < kGT * (kGN / 8); idx += 256) {
-    const int ml = idx / (kGN / 8);
-    const int c8 = (idx - ml * (kGN / 8)) * 8;
-    const int m = mt0 + ml;
-    if (m >= p.M) continue;
-    const int b = m / per_b;
-    const int rem = m - b * per_b;
-    const int t = rem / hw;
-    const int sp = rem - t * hw;
-    const int n = nt0 + c8;
-    const uint4 cv = *reinterpret_cast<const uint4*>(&stile[ml * (kGN + 8) + c8]);
-    const uint4 sv = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
-    const uint4 tv = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
-    const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w},
-                   tw[4] = {tv.x, tv.y, tv.z, tv.w};
-    uint32_t ow[4];
+  // the positional loads of 6 chunks first, then their adds and stores: one L2 round trip
+  // per half tile instead of one per chunk (each store would otherwise order the next loads)
+  constexpr int kEpi = kGT * (kGN / 8) / 256, kEpiH = kEpi / 2;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float o[2];
+  for (int half = 0; half < 2; ++half) {
+    uint4 svs[kEpiH], tvs[kEpiH];
+    long long orow[kEpiH];
+    int soff[kEpiH];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float c = __uint_as_float(h ? (cw[q] & 0xffff0000u) : (cw[q] << 16));
-        const float sp_ = __uint_as_float(h ? (sw[q] & 0xffff0000u) : (sw[q] << 16));
-        const float tp = __uint_as_float(h ? (tw[q] & 0xffff0000u) : (tw[q] << 16));
-        o[h] = round_to<bf16_t>(c + sp_) + tp;
-      }
-      ow[q] = static_cast<uint32_t>(from_f32<bf16_t>(o[0])) |
-              (static_cast<uint32_t>(from_f32<bf16_t>(o[1])) << 16);
+    for (int it = 0; it < kEpiH; ++it) {
+      const int idx = tid + (half * kEpiH + it) * 256;
+      const int ml = idx / (kGN / 8);
+      const int c8 = (idx - ml * (kGN / 8)) * 8;
+      const int m = mt0 + ml;
+      const bool ok = m < p.M;
+      const int b = ok ? m / per_b : 0;
+      const int rem = ok ? m - b * per_b : 0;
+      const int t = rem / hw;
+      const int sp = rem - t * hw;
+      const int n = nt0 + c8;
+      svs[it] = *reinterpret_cast<const uint4*>(spos + (long long)sp * p.embed + n);
+      tvs[it] = *reinterpret_cast<const uint4*>(tpos + (long long)t * p.embed + n);
+      orow[it] = ok ? b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n : -1;
+      soff[it] = ml * (kGN + 8) + c8;
     }
-    *reinterpret_cast<uint4*>(out + b * p.out_sb + (long long)(p.row0 + rem) * p.embed + n) =
-        make_uint4(ow[0], ow[1], ow[2], ow[3]);
+#pragma unroll
+    for (int it = 0; it < kEpiH; ++it) {
+      if (orow[it] < 0) continue;
+      const uint4 cv = *reinterpret_cast<const uint4*>(&stile[soff[it]]);
+      const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w},
+                     sw[4] = {svs[it].x, svs[it].y, svs[it].z, svs[it].w},
+                     tw[4] = {tvs[it].x, tvs[it].y, tvs[it].z, tvs[it].w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float c = __uint_as_float(h ? (cw[q] & 0xffff0000u) : (cw[q] << 16));
+          const float sp_ = __uint_as_float(h ? (sw[q] & 0xffff0000u) : (sw[q] << 16));
+          const float tp = __uint_as_float(h ? (tw[q] & 0xffff0000u) : (tw[q] << 16));
+          o[h] = round_to<bf16_t>(c + sp_) + tp;
+        }
+        ow[q] = static_cast<uint32_t>(from_f32<bf16_t>(o[0])) |
+                (static_cast<uint32_t>(from_f32<bf16_t>(o[1])) << 16);
+      }
+      *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
   }
-  patch_frame_rows<bf16_t>(p);  // after the tile: the head / padding rows never delay it
+  patch_frame_rows<bf16_t>(p, mti, nm, nti);  // after the tile: the head / padding rows never delay it
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void patch_generic_kernel(const PatchParams p) {
-  patch_frame_rows<T>(p);
+  patch_frame_rows<T>(p, blockIdx.x, gridDim.x, blockIdx.y);
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (long long)p.M * p.embed) return;
   const int m = static_cast<int>(gid / p.embed);
@@ -474,14 +518,14 @@ extern "C" int vm_patch_embed_fwd(const void* video, const void* weight, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool mfma_ok = dtype == VM_DTYPE_BF16 && patch_w % 8 == 0 && width % 8 == 0 &&
                        p.K % 8 == 0 && vmhost::aligned16(video) && vmhost::aligned16(weight);
-  const bool wide_ok = mfma_ok && patch_h == 16 && patch_w == 16 && embed % kPN == 0 && p.K % 32 == 0 &&
+  const bool wide_ok = mfma_ok && patch_h == 16 && patch_w == 16 && embed % kPN == 0 && p.K % 64 == 0 &&
                        out_sb % 8 == 0 && vmhost::aligned16(out) && vmhost::aligned16(spos) &&
                        vmhost::aligned16(tpos);
   // the 128-token LDS-staged tiles pay off on chip-filling batches; small ones keep more,
   // smaller workgroups (B = 1: 147 of 64 x 192 against 75 of 128 x 192).  All three MFMA
   // kernels accumulate in the same k order and round at the same points (bit-identical).
   if (wide_ok && p.M >= 32768) {
-    dim3 grid((p.M + kGT - 1) / kGT, embed / kGN);
+    dim3 grid(static_cast<unsigned>((p.M + 8 * kGT - 1) / (8 * kGT) * 8 * (embed / kGN)));
     hipLaunchKernelGGL(patch_gemm_kernel, grid, dim3(256), 0, s, p);
   } else if (wide_ok) {  // the 64x192 register-fragment kernel
     dim3 grid((p.M + kPT - 1) / kPT, embed / kPN);
