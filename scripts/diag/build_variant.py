@@ -358,6 +358,14 @@ VARIANTS = {
                    ("vm_patch.hip", "    *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);\n  }\n  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);",
                     "    if (ow[0] == 0x12345678u) *reinterpret_cast<uint4*>(out + orow[it]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);\n  }\n  patch_frame_rows<bf16_t>(p, blockIdx.x, gridDim.x, blockIdx.y);")],
 
+    # the token-major dtp scan's waves at raised issue priority (s_setprio), so that beside
+    # another sub-batch stream's memory-bound kernels on the same SIMD its instructions
+    # issue first
+    "dtp_prio2": [("vm_scan_seq.hip", "  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);",
+                   "  __builtin_amdgcn_s_setprio(2);\n  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);")],
+    "dtp_prio3": [("vm_scan_seq.hip", "  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);",
+                   "  __builtin_amdgcn_s_setprio(3);\n  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);")],
+
 }
 
 
