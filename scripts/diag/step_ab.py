@@ -1,6 +1,6 @@
 """One library's B-clip M-16f stateful-chunk step time (the bench's forward, default
 sub-batch streams), for A/B across probe builds run in alternating processes:
-    python scripts/diag/step_ab.py [--lib=VARIANT] [--batch=896] [--reps=3]
+    python scripts/diag/step_ab.py [--lib=VARIANT] [--batch=896] [--reps=3] [--lock=0|1]
 Prints ms per step and a fingerprint of the pooled features (equal = same bits)."""
 import hashlib
 import json
@@ -15,6 +15,7 @@ if LIB:  # a probe variant (scripts/diag/build_variant.py)
     import videomamba_amd._lib as L
     L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", LIB[0], "libvideomamba_hip.so")
 import torch  # noqa: E402
+from videomamba_amd import options  # noqa: E402
 from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
 
 
@@ -23,7 +24,10 @@ def arg(name, default):
     return int(v[0]) if v else default
 
 
-B, reps = arg("batch", 896), arg("reps", 3)
+B, reps, lock = arg("batch", 896), arg("reps", 3), arg("lock", -1)
+_ctx = options.override(batch_stream_lock=bool(lock)) if lock >= 0 else None
+if _ctx is not None:
+    _ctx.__enter__()  # (held in _ctx: a collected generator would restore the options)
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
@@ -40,5 +44,6 @@ with torch.no_grad():
         model(x, ssm_state=st, temporal_pos_offset=0)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / reps * 1e3
-print(json.dumps({"lib": LIB[0] if LIB else "product", "batch": B, "ms_per_step": round(ms, 2),
+print(json.dumps({"lib": LIB[0] if LIB else "product", "batch": B,
+                  "batch_stream_lock": options.get().batch_stream_lock, "ms_per_step": round(ms, 2),
                   "fingerprint": fp}), flush=True)

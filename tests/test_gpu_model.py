@@ -1153,9 +1153,10 @@ def _flat(st):
     return [t for v in vals for t in _flat(v)]
 
 
+@pytest.mark.parametrize("lock", [True, False])
 @pytest.mark.parametrize("kind", ["none", "list", "tuple", "dict", "ssm_only", "mask", "keep_temporal"])
 @pytest.mark.parametrize("parts", [2, 3])
-def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
+def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts, lock):
     """options.batch_streams: a forward over enough clips runs as sub-batches, each on its own
     HIP stream (the bench's B = 448 step: two halves, one's scan overlapping the other's
     projections).  Every kernel's rows are batch-independent, so x_vis, x_pool and every
@@ -1163,7 +1164,9 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
     ssm states advanced in place in the caller's tensors, new conv states), for list / tuple
     / dict / legacy ssm-only state containers and keep_temporal pooling; uneven part sizes
     (7 clips in 2 or 3 parts).  A masked forward stays on one stream (its equal-visible-count
-    check spans the whole batch)."""
+    check spans the whole batch).  ``lock``: options.batch_stream_lock, the parts' layers
+    issued from one host thread each with their pre phases ordered in a ring (phase_lock.py),
+    or free-running streams issued from the caller's thread."""
     torch.manual_seed(5)
     model = PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=64, channels=3,
                                kernel_size=1, num_frames=4, pool_type="avg",
@@ -1192,7 +1195,8 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts):
     def run(n):
         st = make_state()
         outs = []
-        with options.override(batch_streams=n, batch_stream_min_clips=2), torch.no_grad():
+        with options.override(batch_streams=n, batch_stream_min_clips=2,
+                              batch_stream_lock=lock), torch.no_grad():
             for off in (0, 2):
                 kw = dict(keep_temporal=kind == "keep_temporal", mask=mask if off == 0 else None)
                 if st is None:

@@ -696,12 +696,14 @@ def test_patch_embed_matches_oracle(dt, Bz, T, H, W, P, kt, C):
     assert not out[:, -1].float().abs().any()
 
 
-@pytest.mark.parametrize("T,kt,C", [(32, 1, 576), (16, 2, 192), (32, 1, 192)])
+@pytest.mark.parametrize("T,kt,C", [(32, 1, 576), (16, 2, 192), (32, 1, 192), (16, 1, 384)])
 def test_patch_embed_kernels_agree_bitwise(T, kt, C):
     """The library picks the patch-embed kernel by token count: the LDS-staged 128x192
     tiles at >= 32768 tokens, the 64x192 register-fragment tiles below.  Both accumulate
     in the same k order and round at the same points, so a clip embedded inside a large
-    batch equals the same clip embedded alone, bit for bit."""
+    batch equals the same clip embedded alone, bit for bit.  The large kernel walks its
+    tiles in XCD groups of 8 token tiles x C / 192 channel tiles: C = 192, 384, 576 cover
+    one to three channel tiles per group, and every batch here ends in a partial group."""
     g = torch.Generator().manual_seed(7 + C)
     bf = torch.bfloat16
     Bz = -(-32768 // ((T // kt) * 196)) + 1  # enough clips for the wide-tile kernel

@@ -45,6 +45,7 @@ from torch import Tensor
 
 from . import kernels as K
 from . import options
+from . import phase_lock as _phase
 from .gemm_tuning import tuned
 from .layers import round_up, warn_if_grad
 
@@ -432,6 +433,7 @@ class Mamba(nn.Module):
         dtp = self._dtp_ok(hn, seqlen, conv_state_in)
         xz, u, x_dbl, dt = self._tm_front(hn, seqlen, conv_state_in, conv_state_out,
                                           want_dt=not dtp)
+        _phase.pre_done(self.layer_idx)  # sub-batch streams: the next part's pre phase may go
         y = torch.empty_like(u)
         h0_s = (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0)
         hl_s = (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0)

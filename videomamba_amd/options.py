@@ -55,6 +55,14 @@ documented options object; tests and sweeps change them with :func:`override`.
                      Measured on M-16f (scripts/diag/batch_streams_sweep.py): B = 448 in two
                      parts 424-425 vs 432-436 ms per step; three or four parts, or two parts
                      of B = 224 / 112, are slower than one stream.
+    batch_stream_lock
+                     True (default) orders the parts' layer "pre" phases in a ring (add +
+                     norm, in_proj, conv_proj; phase_lock.py).  Each part's layers are issued
+                     from its own host thread, with cross-stream event waits, so one part's
+                     scan runs beside another part's pre phase and no two pre phases overlap.
+                     B = 896: 0.3-1.1 % faster per step, same bits (809.8-810.2 vs
+                     817.8-818.7 ms in one process; 820.6-823.3 vs 823.4-830.7 ms across
+                     processes).  False lets the streams run free.
     batch_stream_min_clips
                      the smallest batch that is split (default 448: parts of >= 224 clips,
                      a whole round of the dt_proj-in-scan grid each).
@@ -71,7 +79,8 @@ documented options object; tests and sweeps change them with :func:`override`.
     small_gemm_max_n ... and at most this many output columns (default 1024: out_proj;
                      in_proj's N = 2 * d_inner stays on the library GEMM).
 
-Options are process-global (not thread-local): the model is driven from one host thread.
+Options are process-global (not thread-local): the model is driven from one host thread,
+and the sub-batch issue threads of ``batch_stream_lock`` read the caller's options.
 """
 
 from __future__ import annotations
@@ -99,6 +108,7 @@ class Options:
     row_invariant_gemm_clips: int = 8
     fuse_out_norm: bool = False
     batch_streams: int = 2
+    batch_stream_lock: bool = True
     in_proj_z_stream: bool = False
     in_proj_split_clips: int = 8
     batch_stream_min_clips: int = 448

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import logging
 import math
+import threading
 from functools import partial
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union, cast
 
@@ -30,6 +31,7 @@ from torch import Tensor
 
 from . import kernels as K
 from . import options
+from . import phase_lock as _phase
 from .layers import DropPath, RMSNorm, round_up, to_2tuple, trunc_normal_, warn_if_grad
 from .mamba_simple import InferenceParamsLike, Mamba
 from .streaming import (STREAMING_CONTRACT_VERSION, ForwardReturnSemantics, StateShape,
@@ -141,6 +143,8 @@ class Block(nn.Module):
         previous block's out_proj already ran this block's add + norm (``pre.done``): use its
         normalised rows and updated residual.  ``next_norm``: offer the NEXT block's norm to
         this block's out_proj (vm_linear_add_norm_fwd)."""
+        idx = getattr(self, "layer_idx", None)
+        _phase.pre_start(idx)  # sub-batch streams: after the previous part's pre phase
         if pre is not None and pre.done:
             hn, residual = pre.hn, pre.residual
         else:
@@ -151,6 +155,7 @@ class Block(nn.Module):
         res = self.mixer.forward_padded(hn, seqlen, ssm_state=ssm_state, state=state,
                                         return_state=return_state, conv_out=conv_out,
                                         next_norm=next_norm)
+        _phase.pre_done(idx)  # (the token-major mixer marked it after conv_proj already)
         if return_state:
             return res[0], residual, res[1]
         return res, residual, None
@@ -254,6 +259,38 @@ def _side_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
     while len(have) < n:
         have.append(torch.cuda.Stream(device, priority=-1 if not have else 0))
     return have[:n]
+
+
+def _issue_phase_locked(issue: Callable[[int], None], lock: "_phase.PhaseLock", parts: int,
+                        device: torch.device) -> None:
+    """Issue sub-batch ``i`` by ``issue(i)`` under ``lock`` (phase_lock.py): part 0 from the
+    calling thread, the others from one host thread each, with the caller's device, grad
+    and inference modes (thread-local in torch).  A failing part releases its phase events
+    so the others drain; the first error is raised after every part returned."""
+    grad, infer = torch.is_grad_enabled(), torch.is_inference_mode_enabled()
+    errors: List[Optional[BaseException]] = [None] * parts
+
+    def work(i: int) -> None:
+        _phase.bind(lock, i)
+        try:
+            with torch.cuda.device(device), torch.inference_mode(infer), \
+                    torch.set_grad_enabled(grad):
+                issue(i)
+        except BaseException as e:  # noqa: BLE001 - re-raised below, on the caller's thread
+            errors[i] = e
+            lock.release(i)
+        finally:
+            _phase.bind(None, 0)
+
+    threads = [threading.Thread(target=work, args=(i,), daemon=True) for i in range(1, parts)]
+    for t in threads:
+        t.start()
+    work(0)
+    for t in threads:
+        t.join()
+    for e in errors:
+        if e is not None:
+            raise e
 
 
 class PretrainVideoMamba(nn.Module):
@@ -727,16 +764,23 @@ class PretrainVideoMamba(nn.Module):
         L = self._validate_temporal_length(x.shape[2]) * gh * gw + (1 if has_cls else 0)
         feats = torch.empty((B, L, self.embed_dim), dtype=self.patch_embed.proj.weight.dtype,
                             device=dev)
-        outs = []
-        for i in range(parts):
+        outs: List[Any] = [None] * parts
+
+        def issue(i: int) -> None:
             a, b = cut[i], cut[i + 1]
-            s = streams[i]
-            s.wait_stream(cur)
-            with torch.cuda.stream(s):
-                outs.append(self._encode(
+            with torch.cuda.stream(streams[i]):
+                outs[i] = self._encode(
                     x[a:b], None, part_state(a, b), temporal_pos_offset, pool=pool,
                     conv_out=None if conv_new is None else conv_new[:, a:b],
-                    feats_out=feats[a:b], split=False))
+                    feats_out=feats[a:b], split=False)
+
+        for s in streams[:parts]:
+            s.wait_stream(cur)
+        if parts > 1 and options.get().batch_stream_lock:
+            _issue_phase_locked(issue, _phase.PhaseLock(parts, depth), parts, dev)
+        else:
+            for i in range(parts):
+                issue(i)
         for s in streams[:parts]:
             cur.wait_stream(s)
         x_pool = None if outs[0][1] is None else torch.cat([o[1] for o in outs], 0)
