@@ -7,7 +7,9 @@ add + norm, in_proj and conv_proj; the scan and out_proj follow it.
   - alternate: oneway, and half A's pre(l + 1) also waits for half B's pre(l), so the two
                halves' pre phases never overlap and each scan meets the other's pre;
   - alternate_post: alternate with the previous layer's out_proj inside the locked phase
-               (out_proj(l - 1) + pre(l)), so no two GEMMs of the halves overlap.
+               (out_proj(l - 1) + pre(l)), so no two GEMMs of the halves overlap;
+  - alt_inproj: alternate with the locked phase ending after in_proj (conv_proj outside).
+"product" is the model's own forward (since round 5 with options.batch_stream_lock).
     python scripts/diag/phase_lock_streams.py"""
 import json
 import os
@@ -43,7 +45,10 @@ def hook(kind, idx):
         return
     ev, rec = state["ev"], state["rec"]
     cur = torch.cuda.current_stream(dev)
-    if kind == "pre_done":
+    if kind in ("pre_done", "pre_done_early"):
+        # alt_inproj: the locked phase ends after in_proj (conv_proj outside it)
+        if (kind == "pre_done_early") != (mode == "alt_inproj"):
+            return
         ev[part][idx].record(cur)
         rec[part][idx].set()
     elif kind == "pre_start" or kind == "post_start":
@@ -61,7 +66,7 @@ def hook(kind, idx):
         if part == 1:
             rec[0][idx].wait()
             cur.wait_event(ev[0][idx])
-        elif mode in ("alternate", "alternate_post") and idx >= 1:
+        elif mode in ("alternate", "alternate_post", "alt_inproj") and idx >= 1:
             rec[1][idx - 1].wait()
             cur.wait_event(ev[1][idx - 1])
 
@@ -87,10 +92,20 @@ def scan_dtproj_raw(*a, **k):
 
 
 MS.K.scan_dtproj_raw = scan_dtproj_raw
+_cp = MS.K.conv_proj_raw
+
+
+def conv_proj_raw(*a, **k):
+    hook("pre_done_early", tls.layer)
+    return _cp(*a, **k)
+
+
+MS.K.conv_proj_raw = conv_proj_raw
 _fp = V.Block.forward_padded
 
 
 def block_fp(self, *a, **k):
+    tls.layer = self.mixer._phase_idx
     hook("pre_start", self.mixer._phase_idx)
     return _fp(self, *a, **k)
 
@@ -138,7 +153,7 @@ def threaded(st, mode):
 with torch.no_grad():
     ref_state = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     ref = model(x, ssm_state=ref_state, temporal_pos_offset=0)[1].float()
-    for mode in ("free", "alternate", "alternate_post"):
+    for mode in ("alternate", "alt_inproj"):
         fresh = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
         out = threaded(fresh, mode).float()
         print(json.dumps({"mode": mode, "pool_bitwise_equal_product": bool(torch.equal(out, ref))}),
@@ -146,7 +161,7 @@ with torch.no_grad():
         del fresh
     st = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     for r in range(3):
-        for mode in ("product", "alternate", "alternate_post"):
+        for mode in ("product", "alternate", "alt_inproj"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(3):
