@@ -366,6 +366,17 @@ VARIANTS = {
     "dtp_prio3": [("vm_scan_seq.hip", "  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);",
                    "  __builtin_amdgcn_s_setprio(3);\n  int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;\n  xcd_order(gx, gy, gz);")],
 
+    # add + RMSNorm (the B = 448 form) / the wide conv_proj at raised wave priority, so that
+    # beside the other sub-batch's VALU-bound scan their memory requests issue first
+    "an_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
+                  "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n")],
+    "cp_prio3": [("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
+                  "void conv_proj_kernel(const ConvProjParams p) {\n  __builtin_amdgcn_s_setprio(3);\n")],
+    "ancp_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
+                    "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n"),
+                   ("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
+                    "void conv_proj_kernel(const ConvProjParams p) {\n  __builtin_amdgcn_s_setprio(3);\n")],
+
 }
 
 
