@@ -8,7 +8,9 @@ add + norm, in_proj and conv_proj; the scan and out_proj follow it.
                halves' pre phases never overlap and each scan meets the other's pre;
   - alternate_post: alternate with the previous layer's out_proj inside the locked phase
                (out_proj(l - 1) + pre(l)), so no two GEMMs of the halves overlap;
-  - alt_inproj: alternate with the locked phase ending after in_proj (conv_proj outside).
+  - alt_inproj: alternate with the locked phase ending after in_proj (conv_proj outside);
+  - alt_op:    alternate, and each half's out_proj(l) waits for the other half's next
+               in_proj, so out_proj meets conv_proj rather than in_proj.
 "product" is the model's own forward (since round 5 with options.batch_stream_lock).
     python scripts/diag/phase_lock_streams.py"""
 import json
@@ -45,6 +47,16 @@ def hook(kind, idx):
         return
     ev, rec = state["ev"], state["rec"]
     cur = torch.cuda.current_stream(dev)
+    if kind == "pre_done_early" and mode == "alt_op":  # in_proj(idx) issued
+        state["ev2"][part][idx].record(cur)
+        state["rec2"][part][idx].set()
+        return
+    if kind == "post_start" and mode == "alt_op":  # out_proj(idx) waits the other's in_proj
+        o, j = (1, idx) if part == 0 else (0, idx + 1)
+        if j < depth:
+            state["rec2"][o][j].wait()
+            cur.wait_event(state["ev2"][o][j])
+        return
     if kind in ("pre_done", "pre_done_early"):
         # alt_inproj: the locked phase ends after in_proj (conv_proj outside it)
         if (kind == "pre_done_early") != (mode == "alt_inproj"):
@@ -66,7 +78,7 @@ def hook(kind, idx):
         if part == 1:
             rec[0][idx].wait()
             cur.wait_event(ev[0][idx])
-        elif mode in ("alternate", "alternate_post", "alt_inproj") and idx >= 1:
+        elif mode in ("alternate", "alternate_post", "alt_inproj", "alt_op") and idx >= 1:
             rec[1][idx - 1].wait()
             cur.wait_event(ev[1][idx - 1])
 
@@ -118,6 +130,8 @@ def threaded(st, mode):
     state["mode"] = mode
     state["ev"] = [[torch.cuda.Event() for _ in range(depth)] for _ in range(2)]
     state["rec"] = [[threading.Event() for _ in range(depth)] for _ in range(2)]
+    state["ev2"] = [[torch.cuda.Event() for _ in range(depth)] for _ in range(2)]
+    state["rec2"] = [[threading.Event() for _ in range(depth)] for _ in range(2)]
     cut = [0, B // 2, B]
     cur = torch.cuda.current_stream(dev)
     streams = V._side_streams(dev, 2)
@@ -153,7 +167,7 @@ def threaded(st, mode):
 with torch.no_grad():
     ref_state = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     ref = model(x, ssm_state=ref_state, temporal_pos_offset=0)[1].float()
-    for mode in ("alternate", "alt_inproj"):
+    for mode in ("alternate", "alt_op"):
         fresh = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
         out = threaded(fresh, mode).float()
         print(json.dumps({"mode": mode, "pool_bitwise_equal_product": bool(torch.equal(out, ref))}),
@@ -161,7 +175,7 @@ with torch.no_grad():
         del fresh
     st = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     for r in range(3):
-        for mode in ("product", "alternate", "alt_inproj"):
+        for mode in ("product", "alt_op"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(3):
