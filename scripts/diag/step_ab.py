@@ -1,6 +1,6 @@
 """One library's B-clip M-16f stateful-chunk step time (the bench's forward, default
 sub-batch streams), for A/B across probe builds run in alternating processes:
-    python scripts/diag/step_ab.py [--lib=VARIANT] [--batch=896] [--reps=3] [--lock=0|1]
+    python scripts/diag/step_ab.py [--lib=VARIANT] [--batch=896] [--reps=3] [--lock=0|1] [--opt=name=value]
 Prints ms per step and a fingerprint of the pooled features (equal = same bits)."""
 import hashlib
 import json
@@ -25,7 +25,12 @@ def arg(name, default):
 
 
 B, reps, lock = arg("batch", 896), arg("reps", 3), arg("lock", -1)
-_ctx = options.override(batch_stream_lock=bool(lock)) if lock >= 0 else None
+_kw = {} if lock < 0 else {"batch_stream_lock": bool(lock)}
+for a in sys.argv:  # --opt=name=value (bool / int options)
+    if a.startswith("--opt="):
+        k, v = a[6:].split("=", 1)
+        _kw[k] = v.lower() in ("1", "true", "on") if v.lower() in ("0", "1", "true", "false", "on", "off") else int(v)
+_ctx = options.override(**_kw) if _kw else None
 if _ctx is not None:
     _ctx.__enter__()  # (held in _ctx: a collected generator would restore the options)
 dev = torch.device("cuda", 0)
@@ -45,5 +50,6 @@ with torch.no_grad():
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / reps * 1e3
 print(json.dumps({"lib": LIB[0] if LIB else "product", "batch": B,
-                  "batch_stream_lock": options.get().batch_stream_lock, "ms_per_step": round(ms, 2),
+                  "batch_stream_lock": options.get().batch_stream_lock,
+                  "fuse_out_norm": options.get().fuse_out_norm, "ms_per_step": round(ms, 2),
                   "fingerprint": fp}), flush=True)
