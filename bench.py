@@ -56,10 +56,12 @@ CYC_EXP, CYC_FMA, SIMDS, CLOCK_HZ = 8.2, 2.8, 1024, 2.4e9
 LAB_NO_MEMORY_US_PER_CLIP_LAYER = 9.67
 
 CONFIGS = {
-    # C3 (default): 896 clips per GPU = two 448-clip sub-batch streams (options.batch_streams;
-    # each launch keeps the 448-clip shape whose scan grid runs ~2 whole rounds), 921-934 vs
-    # 949 us per clip at 448 (profiles/r05zd_batch_sweep.jsonl, r05ze_batch_sweep.jsonl)
-    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M", batch=896),
+    # C3 (default): 1344 clips per GPU = two 672-clip sub-batch streams with their layer
+    # phases locked (options.batch_streams / batch_stream_lock; each launch's scan grid runs
+    # ~3 whole rounds): 909.6-910.0 vs 920.1-923.3 us per clip at 896 (2 x 448), 908.3-908.8
+    # at 1792, same box alternating (profiles/r05zzn_batch_lock_sweep.jsonl); before the lock
+    # 896 and 1344 ran alike (921-934 / 925 us, r05zd_batch_sweep.jsonl, r05ze_*)
+    "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M", batch=1344),
     # C4: the same 896 clips per GPU (profiles/r05zg_*: 3.373 M at 896 with two streams,
     # 3.316 M at 448 on one stream, 3.263 M at 448 as two 224-clip streams)
     "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M", batch=896),

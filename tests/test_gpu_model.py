@@ -858,18 +858,20 @@ def test_c3_m_16f_bf16_bench_kernels_match_oracle():
     torch.testing.assert_close(xv[:1].float().cpu(), ref_v.float(), rtol=5e-2, atol=5e-2)
 
 
-def test_c3_bench_batch_896_clips_bitwise_equal_small_batch_and_oracle():
+@pytest.mark.parametrize("B", [896, 1344])
+def test_c3_bench_batch_clips_bitwise_equal_small_batch_and_oracle(B):
     """Correctness at the benched batch: the bench's exact C3 call —
-    VideoMamba-M 16x224^2 bf16, bf16 zero state, offset 0, cls+avg — at B = 896, which the
-    forward runs as two 448-clip sub-batch streams (options.batch_streams): per launch xz is
-    6.5 GB and u / y 3.2 GB (past every 31-bit buffer offset; the persistent projection GEMM,
-    the wide conv_proj without dt rows and the dt_proj-in-scan single-pass scan).  Clips
-    {0, 1, 447, 448, 894, 895} (both sides of the sub-batch boundary) of x_vis, x_pool and
-    every layer's returned (conv, ssm) state are bit-equal to the same clips run in a B = 9
-    batch with scan_segments = 1 (the same kernel forms at small extents: every form is
-    row-invariant by design), and clip 895 matches orc.encoder_forward at the C3 tolerances
-    (relative L2 <= 1e-2; reference videomamba.py:943-1067, mamba_simple.py:331-339,
-    :443-446)."""
+    VideoMamba-M 16x224^2 bf16, bf16 zero state, offset 0, cls+avg — at B = 1344 (the bench's
+    batch since the phase lock) and 896 (before it).  The forward runs them as two 672- or
+    448-clip sub-batch streams (options.batch_streams, with options.batch_stream_lock): per
+    launch xz is 9.7 / 6.5 GB and u / y 4.9 / 3.2 GB (past every 31-bit buffer offset; the
+    persistent projection GEMM, the wide conv_proj without dt rows and the dt_proj-in-scan
+    single-pass scan).  Clips {0, 1, B/2 - 1, B/2, B - 2, B - 1} (both sides of the
+    sub-batch boundary) of x_vis, x_pool and every layer's returned (conv, ssm) state are
+    bit-equal to the same clips run in a B = 9 batch with scan_segments = 1 (the same kernel
+    forms at small extents: every form is row-invariant by design), and clip B - 1 matches
+    orc.encoder_forward at the C3 tolerances (relative L2 <= 1e-2; reference
+    videomamba.py:943-1067, mamba_simple.py:331-339, :443-446)."""
     torch.manual_seed(0)
     model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
     with torch.no_grad():
@@ -877,8 +879,8 @@ def test_c3_bench_batch_896_clips_bitwise_equal_small_batch_and_oracle():
     model = model.to(torch.bfloat16).eval()
     p = {k: v.detach().clone() for k, v in model.state_dict().items()}
     model = model.to(DEV)
-    B, picks = 896, [0, 1, 447, 448, 894, 895]
     half = B // options.get().batch_streams
+    picks = [0, 1, half - 1, half, B - 2, B - 1]
     assert options.get().batch_streams == 2 and B >= options.get().batch_stream_min_clips
     g = torch.Generator(device=DEV).manual_seed(448)
     x = torch.empty(B, 3, 16, 224, 224, device=DEV, dtype=torch.bfloat16)
@@ -917,7 +919,7 @@ def test_c3_bench_batch_896_clips_bitwise_equal_small_batch_and_oracle():
     ref_v, ref_p, ref_st = orc.encoder_forward(p, cfg, xlast, state=ost, temporal_pos_offset=0)
     rv, rp = _rel(big_v[-1:].cpu(), ref_v), _rel(big_p[-1:].cpu(), ref_p)
     rs = max(_rel(big_s[i][1][-1:].cpu(), ref_st[i][1]) for i in range(32))
-    print(f"C3 B=896 clip 895 vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e}")
+    print(f"C3 B={B} clip {B - 1} vs oracle: x_vis {rv:.3e} x_pool {rp:.3e} ssm {rs:.3e}")
     assert rv <= 1e-2 and rp <= 1e-2 and rs <= 1e-2, (rv, rp, rs)
 
 

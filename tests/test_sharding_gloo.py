@@ -86,10 +86,10 @@ def test_bench_control_flow_world2_weak_scaling():
     slowest rank's (rank 1 sleeps 4 ms per step), one JSON line from rank 0."""
     line = _bench_stub([])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    # C3 default: 896 clips per rank (two 448-clip sub-batch streams on a GPU)
-    assert line["config"]["per_gpu_batch"] == 896 and line["config"]["global_batch"] == 1792
+    # C3 default: 1344 clips per rank (two 672-clip sub-batch streams on a GPU)
+    assert line["config"]["per_gpu_batch"] == 1344 and line["config"]["global_batch"] == 2688
     assert line["ms_per_step"] >= 4.0  # the slower rank sets the step time
-    want = 1792 * 16 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
+    want = 2688 * 16 * 196 * 4 / (line["ms_per_step"] * 4 / 1e3)
     assert abs(line["value"] - want) / want < 1e-3
     assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
 
