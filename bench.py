@@ -11,8 +11,8 @@ clips.  A step = one forward of B clips per GPU; clips shard by batch across ran
 no collective on the data path (weak scaling).  value = video tokens (B*T*196, CLS
 excluded) per second summed over all ranks, timed as the max over ranks.
 
-Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 896 clips per rank by default, two
-448-clip sub-batch streams as in C3, so the 1/2/4/8-GPU curve keeps every GPU at the batch
+Other configs: --config m32 (VideoMamba-M 32x224^2, C4: 1344 clips per rank by default, two
+672-clip sub-batch streams as in C3, so the 1/2/4/8-GPU curve keeps every GPU at the batch
 where the scan holds its occupancy —
 weak scaling; --global-batch G instead splits G clips across ranks with
 sharding.shard_range — strong scaling; run under torchrun for the 8-GPU case), --config ti8
@@ -62,9 +62,10 @@ CONFIGS = {
     # at 1792, same box alternating (profiles/r05zzn_batch_lock_sweep.jsonl); before the lock
     # 896 and 1344 ran alike (921-934 / 925 us, r05zd_batch_sweep.jsonl, r05ze_*)
     "m16": dict(depth=32, embed_dim=576, frames=16, name="VideoMamba-M", batch=1344),
-    # C4: the same 896 clips per GPU (profiles/r05zg_*: 3.373 M at 896 with two streams,
-    # 3.316 M at 448 on one stream, 3.263 M at 448 as two 224-clip streams)
-    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M", batch=896),
+    # C4: the same 1344 clips per GPU (two locked 672-clip streams): 3.516-3.535 M vs
+    # 3.488-3.508 M at 896, alternating on one box (profiles/r05zzq_m32_batch_ab.jsonl;
+    # before the lock r05zg_*: 3.373 M at 896 with two streams, 3.316 M at 448 on one)
+    "m32": dict(depth=32, embed_dim=576, frames=32, name="VideoMamba-M", batch=1344),
     "ti8": dict(depth=24, embed_dim=192, frames=8, name="VideoMamba-Ti",  # C1 / C2 shape
                 batch=512),
 }

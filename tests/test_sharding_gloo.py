@@ -94,15 +94,14 @@ def test_bench_control_flow_world2_weak_scaling():
     assert line["per_gpu_value"] * 2 == pytest.approx(line["value"], rel=1e-6)
 
 
-def test_bench_control_flow_world2_m32_default_is_weak_896_per_rank():
-    """C4 (--config m32) without --global-batch keeps 896 clips per rank (two 448-clip
-    sub-batch streams, as C3; 448 per launch is the batch where
-    the scan holds its occupancy; 84 per GPU at N = 8 from a fixed 672 would have measured
-    the batch choice, not the sharding): weak scaling, global batch = world x 896, and the
-    metric names the workload actually run."""
+def test_bench_control_flow_world2_m32_default_is_weak_1344_per_rank():
+    """C4 (--config m32) without --global-batch keeps 1344 clips per rank (two 672-clip
+    sub-batch streams, as C3; a launch of whole scan-grid rounds; 84 per GPU at N = 8 from a
+    fixed 672 would have measured the batch choice, not the sharding): weak scaling, global
+    batch = world x 1344, and the metric names the workload actually run."""
     line = _bench_stub(["--config", "m32"])
     assert line["scaling"] == "weak"
-    assert line["config"]["per_gpu_batch"] == 896 and line["config"]["global_batch"] == 1792
+    assert line["config"]["per_gpu_batch"] == 1344 and line["config"]["global_batch"] == 2688
     assert line["metric"].endswith("VideoMamba-M 32f 224")
     assert _bench_stub(["--config", "ti8"])["metric"].endswith("VideoMamba-Ti 8f 224")
 
