@@ -10,7 +10,9 @@ add + norm, in_proj and conv_proj; the scan and out_proj follow it.
                (out_proj(l - 1) + pre(l)), so no two GEMMs of the halves overlap;
   - alt_inproj: alternate with the locked phase ending after in_proj (conv_proj outside);
   - alt_op:    alternate, and each half's out_proj(l) waits for the other half's next
-               in_proj, so out_proj meets conv_proj rather than in_proj.
+               in_proj, so out_proj meets conv_proj rather than in_proj;
+  - alt_nonorm: alternate with the add + norm outside the locked phase (it runs when its
+               own half gets there; the lock starts at in_proj).
 "product" is the model's own forward (since round 5 with options.batch_stream_lock).
     python scripts/diag/phase_lock_streams.py"""
 import json
@@ -30,7 +32,7 @@ torch.manual_seed(0)
 model = V.PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16, pool_type="cls+avg")
 model = model.to(device=dev, dtype=torch.bfloat16).eval()
 depth = len(model.layers)
-B = 896
+B = int(([a.split('=', 1)[1] for a in sys.argv if a.startswith('--batch=')] or ['896'])[0])
 g = torch.Generator(device=dev).manual_seed(1000)
 x = torch.randn(B, 3, 16, 224, 224, device=dev, generator=g).to(torch.bfloat16)
 for i, layer in enumerate(model.layers):
@@ -63,7 +65,9 @@ def hook(kind, idx):
             return
         ev[part][idx].record(cur)
         rec[part][idx].set()
-    elif kind == "pre_start" or kind == "post_start":
+    elif kind in ("pre_start", "mixer_start") and (kind == "mixer_start") != (mode == "alt_nonorm"):
+        return  # alt_nonorm: the locked phase starts after the add + norm, at the mixer
+    if kind in ("pre_start", "mixer_start", "post_start"):
         # alternate_post: a layer's locked phase starts at the previous layer's out_proj
         # (post_start of idx - 1 is the phase start of idx); layer 0's at its add + norm
         if mode == "alternate_post":
@@ -78,7 +82,7 @@ def hook(kind, idx):
         if part == 1:
             rec[0][idx].wait()
             cur.wait_event(ev[0][idx])
-        elif mode in ("alternate", "alternate_post", "alt_inproj", "alt_op") and idx >= 1:
+        elif mode in ("alternate", "alternate_post", "alt_inproj", "alt_op", "alt_nonorm") and idx >= 1:
             rec[1][idx - 1].wait()
             cur.wait_event(ev[1][idx - 1])
 
@@ -123,6 +127,15 @@ def block_fp(self, *a, **k):
 
 
 V.Block.forward_padded = block_fp
+_mfp = MS.Mamba.forward_padded
+
+
+def mixer_fp(self, *a, **k):
+    hook("mixer_start", self._phase_idx)
+    return _mfp(self, *a, **k)
+
+
+MS.Mamba.forward_padded = mixer_fp
 
 
 def threaded(st, mode):
@@ -167,7 +180,7 @@ def threaded(st, mode):
 with torch.no_grad():
     ref_state = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     ref = model(x, ssm_state=ref_state, temporal_pos_offset=0)[1].float()
-    for mode in ("alternate", "alt_op"):
+    for mode in ("alternate", "alt_nonorm"):
         fresh = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
         out = threaded(fresh, mode).float()
         print(json.dumps({"mode": mode, "pool_bitwise_equal_product": bool(torch.equal(out, ref))}),
@@ -175,7 +188,7 @@ with torch.no_grad():
         del fresh
     st = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
     for r in range(3):
-        for mode in ("product", "alt_op"):
+        for mode in ("product", "alt_nonorm"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(3):
