@@ -29,7 +29,7 @@ _kw = {} if lock < 0 else {"batch_stream_lock": bool(lock)}
 for a in sys.argv:  # --opt=name=value (bool / int options)
     if a.startswith("--opt="):
         k, v = a[6:].split("=", 1)
-        _kw[k] = v.lower() in ("1", "true", "on") if v.lower() in ("0", "1", "true", "false", "on", "off") else int(v)
+        _kw[k] = v.lower() in ("true", "on") if v.lower() in ("true", "false", "on", "off") else int(v)
 _ctx = options.override(**_kw) if _kw else None
 if _ctx is not None:
     _ctx.__enter__()  # (held in _ctx: a collected generator would restore the options)
@@ -51,5 +51,6 @@ with torch.no_grad():
     ms = (time.perf_counter() - t0) / reps * 1e3
 print(json.dumps({"lib": LIB[0] if LIB else "product", "batch": B,
                   "batch_stream_lock": options.get().batch_stream_lock,
-                  "fuse_out_norm": options.get().fuse_out_norm, "ms_per_step": round(ms, 2),
+                  "fuse_out_norm": options.get().fuse_out_norm,
+                  "batch_streams": options.get().batch_streams, "ms_per_step": round(ms, 2),
                   "fingerprint": fp}), flush=True)
