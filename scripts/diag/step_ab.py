@@ -52,5 +52,6 @@ with torch.no_grad():
 print(json.dumps({"lib": LIB[0] if LIB else "product", "batch": B,
                   "batch_stream_lock": options.get().batch_stream_lock,
                   "fuse_out_norm": options.get().fuse_out_norm,
-                  "batch_streams": options.get().batch_streams, "ms_per_step": round(ms, 2),
+                  "batch_streams": options.get().batch_streams,
+                  "min_clips": options.get().batch_stream_min_clips, "ms_per_step": round(ms, 2),
                   "fingerprint": fp}), flush=True)

@@ -64,8 +64,11 @@ documented options object; tests and sweeps change them with :func:`override`.
                      817.8-818.7 ms in one process; 820.6-823.3 vs 823.4-830.7 ms across
                      processes).  False lets the streams run free.
     batch_stream_min_clips
-                     the smallest batch that is split (default 448: parts of >= 224 clips,
-                     a whole round of the dt_proj-in-scan grid each).
+                     the smallest batch that is split (default 224: parts of >= 112 clips).
+                     With the phase lock, B = 224 split in two runs 217.2 vs 221.0-222.8 ms
+                     per step on one stream; B = 112 split runs 143.0-143.3 vs 113.1-113.6 ms,
+                     so smaller batches stay whole (profiles/r05zzu_small_split_lock_ab.jsonl;
+                     448 before the lock, when B = 224 split was slower).
     in_proj_z_stream False (default): True makes the mixer at streaming batches (at most
                      ``in_proj_split_clips`` clips, default 8) run in_proj as two launches,
                      the x half on the current stream and the z half (read only by the scan's
@@ -111,7 +114,7 @@ class Options:
     batch_stream_lock: bool = True
     in_proj_z_stream: bool = False
     in_proj_split_clips: int = 8
-    batch_stream_min_clips: int = 448
+    batch_stream_min_clips: int = 224
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
 
