@@ -494,20 +494,24 @@ def _base_line(args, cfg, world, global_batch, per_rank, elapsed, strong):
                    "model": cfg["name"], "global_batch": global_batch,
                    "per_gpu_batch": per_rank, "frames": T, "seq_len": 1 + T * 196,
                    "parallelism": f"batch-sharded x{world}, no data-path collectives",
-                   "sub_batch_streams": _sub_batch_streams(per_rank)},
+                   "sub_batch_streams": _sub_batch_streams(per_rank, cfg["embed_dim"])},
         "per_gpu_value": round(value / world, 1),
     }
 
 
-def _sub_batch_streams(batch):
+def _sub_batch_streams(batch, embed_dim=576):
     """How many HIP streams the model's forward splits this per-GPU batch over
-    (options.batch_streams; bit-identical to one stream)."""
+    (options.batch_streams from batch_stream_min_clips clips and batch_stream_min_work
+    clip-channels, d_inner = 2 x embed_dim; bit-identical to one stream) —
+    the rule of PretrainVideoMamba._stream_parts."""
     try:
         from videomamba_amd import options
     except Exception:  # the CPU stub run
         return 1
     o = options.get()
-    return int(o.batch_streams) if batch >= max(int(o.batch_stream_min_clips), 2) else 1
+    split = (batch >= max(int(o.batch_stream_min_clips), 2)
+             and batch * 2 * embed_dim >= int(o.batch_stream_min_work))
+    return int(o.batch_streams) if split else 1
 
 
 def main_stub_cpu(args):
@@ -626,7 +630,7 @@ def main():
         from videomamba_amd.mamba_simple import mixer_layout
         mx0 = model.layers[0].mixer
         # the scan as the step launches it: one sub-batch stream's clips per launch
-        rb = max(B // _sub_batch_streams(B), 1)
+        rb = max(B // _sub_batch_streams(B, cfg["embed_dim"]), 1)
         hn0 = torch.empty((1, 1, cfg["embed_dim"]), device=device,
                           dtype=torch.bfloat16).expand(rb, 3144, cfg["embed_dim"])
         _progress("scan roofline leg")

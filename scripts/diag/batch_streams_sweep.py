@@ -34,11 +34,11 @@ with torch.no_grad():
         x = torch.randn(B, 3, 16, 224, 224, device=dev, generator=g).to(torch.bfloat16)
         st = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
         for n in streams:  # warm every mode (workspaces per stream)
-            with options.override(batch_streams=n, batch_stream_min_clips=2):
+            with options.override(batch_streams=n, batch_stream_min_clips=2, batch_stream_min_work=0):
                 model(x, ssm_state=st, temporal_pos_offset=0)
         for r in range(rounds):
             for n in streams:
-                with options.override(batch_streams=n, batch_stream_min_clips=2):
+                with options.override(batch_streams=n, batch_stream_min_clips=2, batch_stream_min_work=0):
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for _ in range(3):

@@ -1197,7 +1197,7 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts, lo
     def run(n):
         st = make_state()
         outs = []
-        with options.override(batch_streams=n, batch_stream_min_clips=2,
+        with options.override(batch_streams=n, batch_stream_min_clips=2, batch_stream_min_work=0,
                               batch_stream_lock=lock), torch.no_grad():
             for off in (0, 2):
                 kw = dict(keep_temporal=kind == "keep_temporal", mask=mask if off == 0 else None)

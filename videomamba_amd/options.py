@@ -69,6 +69,13 @@ documented options object; tests and sweeps change them with :func:`override`.
                      per step on one stream; B = 112 split runs 143.0-143.3 vs 113.1-113.6 ms,
                      so smaller batches stay whole (profiles/r05zzu_small_split_lock_ab.jsonl;
                      448 before the lock, when B = 224 split was slower).
+    batch_stream_min_work
+                     ... and at least this many clip-channels (B x d_inner; default 224 x 1152,
+                     VideoMamba-M's 224 clips), so a narrower model needs more clips for each
+                     part's scan grid to fill the chip: VideoMamba-Ti (d_inner 384) splits from
+                     672 clips.  C2 (Ti-8f, 512 clips) on one stream: 13.65-13.67 M
+                     video-tokens/s against 13.51-13.53 M as two locked streams
+                     (profiles/r05zzw_c2_streams_ab.jsonl).
     in_proj_z_stream False (default): True makes the mixer at streaming batches (at most
                      ``in_proj_split_clips`` clips, default 8) run in_proj as two launches,
                      the x half on the current stream and the z half (read only by the scan's
@@ -115,6 +122,7 @@ class Options:
     in_proj_z_stream: bool = False
     in_proj_split_clips: int = 8
     batch_stream_min_clips: int = 224
+    batch_stream_min_work: int = 224 * 1152
     small_gemm_rows: int = 4096
     small_gemm_max_n: int = 1024
 

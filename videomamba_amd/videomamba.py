@@ -684,13 +684,16 @@ class PretrainVideoMamba(nn.Module):
     # ------------------------------------------------------------------ batch streams
     def _stream_parts(self, x, ssm_state, tpos, conv_out) -> int:
         """How many sub-batches (one HIP stream each) this forward runs as:
-        ``options.batch_streams`` from ``batch_stream_min_clips`` clips up, outside graph
+        ``options.batch_streams`` from ``batch_stream_min_clips`` clips and
+        ``batch_stream_min_work`` clip-channels (B x d_inner) up, outside graph
         capture and the graph runner's buffers, when every layer's state (if any) is one kind
         (full (conv, ssm) pairs of one conv dtype, or legacy ssm-only tensors)."""
         o = options.get()
         n = int(o.batch_streams)
         B = x.shape[0]
-        if (n <= 1 or B < max(int(o.batch_stream_min_clips), 2) or tpos is not None
+        d_inner = int(self.layers[0].mixer.d_inner) if len(self.layers) else 0
+        if (n <= 1 or B < max(int(o.batch_stream_min_clips), 2)
+                or B * d_inner < int(o.batch_stream_min_work) or tpos is not None
                 or conv_out is not None or torch.cuda.is_current_stream_capturing()):
             return 1
         if ssm_state is not None:
