@@ -75,3 +75,27 @@ def test_failing_part_releases_the_others(fail):
 def test_bad_shape():
     with pytest.raises(ValueError):
         PhaseLock(0, 3, record=lambda p, i: None, wait=lambda p, i: None)
+
+
+@pytest.mark.parametrize("embed,batch,want", [(576, 1344, 2), (576, 224, 2), (576, 112, 1),
+                                              (192, 512, 1), (192, 672, 2), (384, 336, 2)])
+def test_split_rule_model_and_bench_agree(embed, batch, want, monkeypatch):
+    """PretrainVideoMamba._stream_parts (the forward's split) and bench.py's
+    _sub_batch_streams (what the bench line reports, and the per-launch batch its roofline
+    leg times) apply the same rule: options.batch_streams from batch_stream_min_clips clips
+    and batch_stream_min_work clip-channels (B x d_inner) up."""
+    import os
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from videomamba_amd.videomamba import PretrainVideoMamba
+
+    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=1, embed_dim=embed,
+                               num_frames=2, pool_type="avg")
+    x = torch.empty(batch, 3, 2, 32, 32, device="meta")
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)  # no device
+    assert model._stream_parts(x, None, None, None) == want
+    assert bench._sub_batch_streams(batch, embed) == want
