@@ -228,6 +228,36 @@ def scan_roofline(batch, reps, device, layout="tm", dtp=False):
                                    "issue costs, 2.4 GHz; the HBM floor is below it"}}
 
 
+def scan_in_step(step, L=3137, D=1152, N=16):
+    """The scan as the timed step sees it: one more, untimed step with a
+    HIP-event pair recorded around every token-major scan launch on its own launch stream
+    (mamba_simple.scan_event_log), so the duration includes the other sub-batch stream's
+    kernels sharing the CUs.  Priced with the same SURVEY 8(d) bytes as ``roofline``; the
+    median launch is the headline (the first layer of each stream starts beside the patch
+    embed, the last beside the final norm)."""
+    from videomamba_amd.mamba_simple import scan_event_log
+    torch.cuda.synchronize()
+    with torch.no_grad(), scan_event_log() as log:
+        step()
+    torch.cuda.synchronize()
+    if not log:
+        return None
+    us = sorted(a.elapsed_time(b) * 1e3 for a, b, _ in log)
+    batch = log[0][2]
+    e = 2
+    algo = batch * D * L * 4 * e + 2 * batch * N * L * e + 4 * D * N + 8 * D + 2 * batch * D * N * e
+    med = statistics.median(us)
+    mean = sum(us) / len(us)
+    return {"launches": len(us), "batch_per_launch": batch, "median_us": round(med, 2),
+            "mean_us": round(mean, 2), "min_us": round(us[0], 2), "max_us": round(us[-1], 2),
+            "frac": round(algo / (med * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_mean": round(algo / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": "HIP events around each scan launch of one untimed bench step "
+                      "(videomamba_amd.mamba_simple.scan_event_log); the rocprofv3 trace of "
+                      "the same command: profiles/*_bench_kernel_stats.csv, "
+                      "scripts/traffic_summary.py in-step"}
+
+
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
@@ -637,6 +667,9 @@ def main():
         roof = scan_roofline(rb, args.scan_reps, device,
                              mixer_layout(rb, cfg["embed_dim"] * 2, device),
                              dtp=cfg["embed_dim"] == 576 and mx0._dtp_ok(hn0, 3137))
+        if cfg["embed_dim"] == 576 and T == 16 and not args.full_sequence:  # the C3 step
+            _progress("scan in-step leg")
+            roof["in_step"] = scan_in_step(step)
         b1 = b1_kernel_rooflines(device) if cfg["embed_dim"] == 576 and not args.no_b1 else None
 
     if rank == 0:

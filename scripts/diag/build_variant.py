@@ -36,8 +36,9 @@ VARIANTS = {
                     "    for (int tg = t_beg; EMIT && tg < t_end; tg += kPF) {")],
     "ch_noloop2": [("vm_scan_seq.hip", "    for (int tg = t_beg; tg < t_end; tg += kPF) {",
                     "    for (int tg = t_beg; !EMIT && tg < t_end; tg += kPF) {")],
-    # dt_proj-in-scan kernel without the d16_hi u / z loads and fp32 dt block (round 5 A/B)
-    "dtp_nod16": [("vm_scan_seq.hip", "constexpr bool kDtpD16 = true;", "constexpr bool kDtpD16 = false;")],
+    # dt_proj-in-scan kernel with the inline-asm d16_hi u / z loads and fp32 dt block (the
+    # round-5 A/B, measured slower: DESIGN.md §3.1.1; built from LEGACY_REV)
+    "dtp_d16": [("vm_scan_seq.hip", "constexpr bool kDtpD16 = false;", "constexpr bool kDtpD16 = true;")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],
@@ -380,7 +381,16 @@ VARIANTS = {
 }
 
 
+# Variants whose toggles left the product sources after round 5 (no untested
+# path compiled into a product kernel): they patch the round-5 head's sources instead.
+LEGACY_REV = "45fb10e"
+LEGACY = {"ch_xcd", "dtp_d16", "tg_split", "tg_defer", "tg_sync", "tg_prio1", "tg_prio2",
+          "tg_stamp", "tg_lgkm0", "tg_sw1", "tg_st_nodrain"}
+
+
 def build(name, rev=None):
+    if rev is None and name in LEGACY:
+        rev = LEGACY_REV
     src = os.path.join(ROOT, "videomamba_amd", "csrc")
     work = os.path.join(ROOT, "build", "var", name, "src", "csrc")  # ../../include resolves
     shutil.rmtree(work, ignore_errors=True)

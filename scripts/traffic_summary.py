@@ -18,6 +18,44 @@ import glob
 import json
 import sys
 
+
+def in_step(stats_csv, bench_json=None, batch=672, kname="scan_seq_dtp_kernel"):
+    """The scan's HBM fraction as the bench step sees it, from committed
+    files only: the rocprofv3 --stats kernel summary of a bench command (every launch of
+    the scan there ran inside the step, beside the other sub-batch stream's kernels) and,
+    when given, that command's bench line (its isolated ``roofline.frac`` and live
+    ``roofline.in_step``).  Bytes: SURVEY 8(d) per stateful bf16 launch of ``batch`` clips.
+
+        python scripts/traffic_summary.py in-step profiles/r05zzp_bench_kernel_stats.csv \
+            [profiles/r05zzp_bench.json] [batch]
+    """
+    D_, L_, N_, e_ = 1152, 3137, 16, 2
+    algo_ = (batch * D_ * L_ * 4 * e_ + 2 * batch * N_ * L_ * e_ + 4 * D_ * N_ + 8 * D_
+             + 2 * batch * D_ * N_ * e_)
+    rows = [r for r in csv.DictReader(open(stats_csv)) if kname in r["Name"]]
+    calls = sum(int(r["Calls"]) for r in rows)
+    avg_ns = sum(float(r["TotalDurationNs"]) for r in rows) / calls
+    out = {"kernel": kname, "batch_per_launch": batch, "bytes_per_launch": algo_,
+           "trace": stats_csv, "trace_launches": calls, "trace_avg_us": round(avg_ns / 1e3, 2),
+           "trace_frac": round(algo_ / (avg_ns * 1e-9) / 8e12, 4)}
+    if bench_json:
+        line = json.load(open(bench_json))
+        line = line.get("parsed", line)
+        roof = line["roofline"]
+        out["isolated_avg_us"], out["isolated_frac"] = roof["avg_us"], roof["frac"]
+        if roof.get("in_step"):
+            out["events_median_us"] = roof["in_step"]["median_us"]
+            out["events_frac"] = roof["in_step"]["frac"]
+    print(json.dumps(out, indent=1))
+    return out
+
+
+if len(sys.argv) > 1 and sys.argv[1] == "in-step":
+    a = sys.argv[2:]
+    in_step(a[0], a[1] if len(a) > 1 and a[1].endswith(".json") else None,
+            int(a[-1]) if len(a) > 1 and a[-1].isdigit() else 672)
+    sys.exit(0)
+
 rnd, batch, kname = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 base = f"gpurun_out/{rnd}"
 D, L, N, e = 1152, 3137, 16, 2

@@ -1170,12 +1170,16 @@ def test_batch_streams_forward_is_bitwise_the_one_stream_forward(kind, parts, lo
     issued from one host thread each with their pre phases ordered in a ring (phase_lock.py),
     or free-running streams issued from the caller's thread."""
     torch.manual_seed(5)
-    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=64, channels=3,
+    # embed_dim 192: in_proj / out_proj K (192, 384) on the row-invariant HIP GEMM, which the
+    # split requires (PretrainVideoMamba._row_invariant_projections)
+    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=192, channels=3,
                                kernel_size=1, num_frames=4, pool_type="avg",
                                fused_add_norm=True, rms_norm=True, residual_in_fp32=True)
     model = model.to(DEV).to(torch.bfloat16).eval()
     B = 7
     x = torch.randn(B, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
+    with options.override(batch_streams=parts, batch_stream_min_clips=2, batch_stream_min_work=0):
+        assert model._stream_parts(x[:, :, :2], None, None, None) == parts
     mask = None
     if kind == "mask":  # a 2-frame chunk: 4 patch tokens per frame x 2 (+ CLS); keep 6
         g = torch.Generator(device="cpu").manual_seed(3)
@@ -1256,3 +1260,81 @@ def test_in_proj_z_stream_is_bitwise_the_one_launch_in_proj(bsz):
             gv, gp = runner.run(x, temporal_pos_offset=0)
             torch.cuda.synchronize()
         assert torch.equal(gv, res[True][0]) and torch.equal(gp, res[True][1])
+
+
+def test_c4_bench_batch_clips_bitwise_equal_small_batch():
+    """C4's per-rank bench batch (the extent class test_c3_bench_batch_* does
+    not reach): VideoMamba-M 32x224^2 bf16, one stateful 32-frame chunk at B = 1344 clips, as
+    ``bench.py --config m32`` runs it on each rank — two locked 672-clip sub-batch streams,
+    per launch xz 19.4 GB and u / y 9.7 GB (every buffer offset past 31 bits, L = 6,273).
+    Clips {0, 1, 671, 672, 1342, 1343} (both sides of the sub-batch boundary) of x_vis,
+    x_pool and every layer's returned (conv, ssm) state are bit-equal to the same clips in a
+    B = 9 batch with scan_segments = 1 (every kernel form is row-invariant).  No oracle: the
+    C4 clip shape's oracle comparison is test_c4_m_32f_chunked_equals_full_and_token_major_batch
+    and the C3 one test_c3_bench_batch_*; this test pins the extents (reference
+    videomamba.py:943-1067, mamba_simple.py:331-339, :443-446)."""
+    B = 1344
+    torch.manual_seed(0)
+    model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=32, pool_type="cls+avg")
+    with torch.no_grad():
+        model.temporal_pos_embedding.normal_(0, 0.02)
+    model = model.to(torch.bfloat16).eval().to(DEV)
+    half = B // options.get().batch_streams
+    picks = [0, 1, half - 1, half, B - 2, B - 1]
+    x = torch.empty(B, 3, 32, 224, 224, device=DEV, dtype=torch.bfloat16)
+    assert model._stream_parts(x, None, None, None) == 2
+    g = torch.Generator(device=DEV).manual_seed(32)
+    for i in range(0, B, 32):
+        x[i:i + 32] = torch.randn(min(32, B - i), 3, 32, 224, 224, device=DEV, generator=g)
+    assert half * 6280 * 2304 * 2 > 2 ** 34 and half * 6280 * 1152 * 2 > 2 ** 33
+    with torch.no_grad():
+        st = model.allocate_state(B, dtype=torch.bfloat16, device=DEV)
+        xv, xp, st = model(x, ssm_state=st, temporal_pos_offset=0)
+        torch.cuda.synchronize()
+        K.check_scan_sync()
+        big_v = xv[picks].clone()
+        big_p = xp[picks].clone()
+        big_s = [(c[picks].clone(), s[picks].clone()) for c, s in st]
+        x9 = torch.cat([x[picks], x[2:5]]).contiguous()
+        del xv, xp, st, x
+        torch.cuda.empty_cache()
+        st9 = model.allocate_state(9, dtype=torch.bfloat16, device=DEV)
+        with options.override(scan_segments=1):
+            v9, p9, st9 = model(x9, ssm_state=st9, temporal_pos_offset=0)
+    n = len(picks)
+    assert torch.isfinite(big_v.float()).all()
+    assert torch.equal(big_v, v9[:n]), (big_v.float() - v9[:n].float()).abs().max().item()
+    assert torch.equal(big_p, p9[:n])
+    for i, ((c, s), (c9, s9)) in enumerate(zip(big_s, st9)):
+        assert torch.equal(c, c9[:n]) and torch.equal(s, s9[:n]), i
+
+
+def test_sub_batch_split_stays_off_where_it_could_change_bits():
+    """the sub-batch forward runs its parts on host threads of their own, so it
+    must not split where a part could compute differently from the whole batch — under
+    autocast (thread-local in torch: the issue threads would not inherit it), with the fused
+    out_proj + add + RMSNorm (its pollers assume every producer of the launch runs), on
+    library projection GEMMs (their kernel choice depends on the row count) and in a mixed-
+    dtype model.  The eligible bf16 model splits."""
+    torch.manual_seed(1)
+    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=2, embed_dim=192,
+                               num_frames=4).to(DEV).to(torch.bfloat16).eval()
+    x = torch.randn(6, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
+    with options.override(batch_streams=2, batch_stream_min_clips=2, batch_stream_min_work=0):
+        assert model._stream_parts(x, None, None, None) == 2
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert model._stream_parts(x, None, None, None) == 1
+        with options.override(fuse_out_norm=True):
+            assert model._stream_parts(x, None, None, None) == 1
+        with options.override(projection_gemm="library"):
+            assert model._stream_parts(x, None, None, None) == 1
+        model.norm.float()
+        assert model._stream_parts(x, None, None, None) == 1
+        model.norm.to(torch.bfloat16)
+        assert model._stream_parts(x, None, None, None) == 2
+        # autocast forward: on one stream, the same bits as outside autocast (no torch op on
+        # the HIP path autocasts)
+        ref = model(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            got = model(x)
+        assert all(torch.equal(a, b) for a, b in zip(ref, got))

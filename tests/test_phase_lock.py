@@ -83,7 +83,8 @@ def test_split_rule_model_and_bench_agree(embed, batch, want, monkeypatch):
     """PretrainVideoMamba._stream_parts (the forward's split) and bench.py's
     _sub_batch_streams (what the bench line reports, and the per-launch batch its roofline
     leg times) apply the same rule: options.batch_streams from batch_stream_min_clips clips
-    and batch_stream_min_work clip-channels (B x d_inner) up."""
+    and batch_stream_min_work clip-channels (B x d_inner) up (for the bench's bf16 models,
+    whose projections all run on the row-invariant HIP GEMM)."""
     import os
     import sys
 
@@ -94,8 +95,8 @@ def test_split_rule_model_and_bench_agree(embed, batch, want, monkeypatch):
     from videomamba_amd.videomamba import PretrainVideoMamba
 
     model = PretrainVideoMamba(img_size=32, patch_size=16, depth=1, embed_dim=embed,
-                               num_frames=2, pool_type="avg")
-    x = torch.empty(batch, 3, 2, 32, 32, device="meta")
+                               num_frames=2, pool_type="avg").to(torch.bfloat16)
+    x = torch.empty(batch, 3, 2, 32, 32, device="meta", dtype=torch.bfloat16)
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)  # no device
     assert model._stream_parts(x, None, None, None) == want
     assert bench._sub_batch_streams(batch, embed) == want

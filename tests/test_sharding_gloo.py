@@ -141,38 +141,61 @@ def test_bench_control_flow_world2_global_batch_split():
     assert abs(line["value"] - want) / want < 1e-3
 
 
-def _encoder_shard_worker(rank, world, port, q):
+def _encoder_shard_worker(rank, world, port, q, split=False):
     """One rank of the batch-sharded encoder: its contiguous clip range through the HIP
-    encoder on cuda:0, then the pooled-feature all-gather (gloo, so CPU tensors)."""
+    encoder on cuda:0, then the pooled-feature all-gather (gloo, so CPU tensors).  ``split``:
+    the rank's shard runs as the phase-locked two-stream sub-batch forward (its own host
+    issue threads), as bench.py's ranks do at their 1344-clip batch."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from videomamba_amd.videomamba import PretrainVideoMamba
+        from videomamba_amd import options
         torch.manual_seed(0)
-        model = PretrainVideoMamba(img_size=64, patch_size=16, depth=3, embed_dim=64,
-                                   num_frames=4).eval()
-        x = torch.randn(4, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
+        model = _shard_model(split)
+        x = torch.randn(_SHARD_CLIPS, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
         local = shard_batch(x, world, rank)
-        with torch.no_grad():
-            xv, xp = model.to("cuda:0")(local.to("cuda:0"))
-        pooled = gather_pooled(xp.cpu())
-        q.put((rank, local.shape[0], xv.cpu(), pooled))
+        kw = dict(batch_streams=2, batch_stream_lock=True, batch_stream_min_clips=2,
+                  batch_stream_min_work=0) if split else dict(batch_streams=1)
+        with torch.no_grad(), options.override(**kw):
+            model = model.to("cuda:0")
+            xl = local.to("cuda:0")
+            parts = model._stream_parts(xl, None, None, None)
+            xv, xp = model(xl)
+        pooled = gather_pooled(xp.float().cpu())  # gloo: fp32 rows (bf16 converts exactly)
+        q.put((rank, local.shape[0], xv.cpu(), pooled, parts))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-def test_gpu_encoder_batch_sharded_world2_matches_single_process():
-    """SURVEY §8e on hardware we have: 2 fresh processes (gloo, both on cuda:0) each run
-    their shard of a 4-clip batch through the HIP encoder and all-gather x_pool.  Every
-    rank's features equal the single-process forward of the same shard bit for bit, and the
-    gathered x_pool equals the single-process forward of the whole batch (1e-5: the
-    library GEMMs may pick other kernels for a different batch size)."""
+_SHARD_CLIPS = 6
+
+
+def _shard_model(split):
+    """The sharded-encoder test model: embed_dim 192 (in_proj / out_proj on the row-invariant
+    HIP GEMM, which the sub-batch split requires), bf16 when ``split``."""
     from videomamba_amd.videomamba import PretrainVideoMamba
+    model = PretrainVideoMamba(img_size=64, patch_size=16, depth=3, embed_dim=192,
+                               num_frames=4).eval()
+    return model.to(torch.bfloat16) if split else model
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+def test_gpu_encoder_batch_sharded_world2_matches_single_process(split):
+    """SURVEY §8e on hardware we have: 2 fresh processes (gloo, both on cuda:0) each run
+    their shard of a 6-clip batch through the HIP encoder and all-gather x_pool.  Every
+    rank's features equal the single-process forward of the same shard bit for bit, and the
+    gathered x_pool equals the single-process forward of the whole batch.  ``split``
+    (VERDICT r5 #4): each rank's 3 clips run as the phase-locked two-stream sub-batch
+    forward, so two processes, each with its own host issue threads, run concurrently on one
+    GPU; their features and pooled rows are bit-equal to one process on one stream (bf16:
+    every projection on the row-invariant HIP GEMM).  fp32 (library GEMMs, whose kernel
+    choice depends on the row count) compares x_pool at 1e-5."""
+    from videomamba_amd import options
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_encoder_shard_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_encoder_shard_worker, args=(r, world, port, q, split))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -181,16 +204,19 @@ def test_gpu_encoder_batch_sharded_world2_matches_single_process():
         p.join(120)
         assert p.exitcode == 0
     torch.manual_seed(0)
-    model = PretrainVideoMamba(img_size=64, patch_size=16, depth=3, embed_dim=64,
-                               num_frames=4).eval().to("cuda:0")
-    x = torch.randn(4, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
-    with torch.no_grad():
-        xv_all, xp_all = model(x.to("cuda:0"))
-        for rank, n, xv, pooled in out:
-            a, b = shard_range(4, world, rank)
+    model = _shard_model(split).to("cuda:0")
+    x = torch.randn(_SHARD_CLIPS, 3, 4, 64, 64, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad(), options.override(batch_streams=1):
+        xv_all, xp_all = model(x.to("cuda:0").to(model.patch_embed.proj.weight.dtype))
+        for rank, n, xv, pooled, parts in out:
+            a, b = shard_range(_SHARD_CLIPS, world, rank)
             assert n == b - a
-            xv_ref, _ = model(x[a:b].to("cuda:0"))
+            assert parts == (2 if split else 1)
+            xv_ref, _ = model(x[a:b].to("cuda:0").to(xv_all.dtype))
             assert torch.equal(xv, xv_ref.cpu())
             assert pooled.shape == xp_all.shape
-            torch.testing.assert_close(pooled, xp_all.cpu(), rtol=1e-5, atol=1e-5)
+            if split:
+                assert torch.equal(pooled, xp_all.float().cpu())
+            else:
+                torch.testing.assert_close(pooled, xp_all.float().cpu(), rtol=1e-5, atol=1e-5)
     assert torch.equal(out[0][3], out[1][3])  # every rank holds the same gathered batch

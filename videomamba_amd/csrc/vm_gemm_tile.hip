@@ -26,7 +26,7 @@
 //     LDS-DMA load (LLVM treats mixed VMEM reads / writes on vmcnt as out of order): a wait
 //     that allowed the S stores of the previous tile as "younger ops" let a wave read a
 //     half-tile that had not landed (1 launch in 30 differed at B = 72,
-//     scripts/diag/determinism_b72.py).  No wait counts a store; see kTileStoreWait;
+//     scripts/diag/determinism_b72.py).  No wait counts a store (see the wait rule below);
 //   * waves 4-7 (the SIMD partners of waves 0-3) run one barrier behind (stagger), so a
 //     SIMD's two waves alternate MFMA and LDS / issue segments;
 //   * the MFMA computes out^T tiles (A operand = W rows, B operand = x rows): a lane holds 4
@@ -115,43 +115,17 @@ struct TileRes {  // one output tile: its x rows' buffer, its w rows' offset, it
   int t;      // tile index, -1 past the workgroup's run
 };
 
-// How the waits around a tile's output stores stay exact (stores never count as "younger"):
-//   0: every wait is vmcnt(8): the first wait after the stores (the next tile's first phase)
-//      also waits for them to complete;
-//   1: the last phase before the stores waits vmcnt(4) (also covering the two half-tiles
-//      the next tile's first two waits would retire), those two waits are skipped, and the
-//      next tile's phase-3 wait, vmcnt(8), drains the stores a K-tile later.
-constexpr int kTileStoreWait = 0;
-// s_setprio around the MFMA clusters: 0 none, 1 setprio(1) / (0) around each quadrant's MFMAs
-// (cdna_hip_programming.md T5), 2 waves 4-7 at priority 1 for the whole loop (T5 static form)
-constexpr int kTilePrio = 0;
-// where a phase waits for its own fragment reads: false before its first barrier, true after
-// it (just before the MFMAs: the reads overlap the barrier wait; cdna_hip_programming.md's
-// 8-phase template order)
-constexpr bool kTileLgkmLate = true;
-// (Reading phase 1's B-right fragments right after phase 0's first barrier, to overlap
-// phase 0's MFMAs, reads an unlanded half-tile: waves 4-7 pass their phase-0 wait only after
-// that barrier — the stagger needs the read one phase after the wait; measured wrong in every
-// launch.)
-
-// Phase timestamps for probe builds (scripts/diag/build_variant.py tg_stamp): s_memtime at
-// five points of every phase of one steady-state iteration, waves 0 and 4 of workgroup 0.
-// Off in the product (the calls are discarded; the sink is defined only by the probe build).
-constexpr bool kTileStamps = false;
-// store the A-top half of a finished tile after phase 1 of its last K-tile (its quadrants
-// (top, left) and (top, right) are final there) and the A-bottom half after phase 3, instead
-// of all 2 x TMH x TNH stores after phase 3 (the burst is split across the stagger)
-constexpr bool kTileSplitStore = false;
-// store the A-bottom half of a finished tile one phase into the next tile (after its phase-1
-// MFMAs; those accumulators are next used in its phase 2) instead of with the A-top half
-constexpr bool kTileDeferStore = false;
-// all eight waves store a finished tile together (waves 0-3 wait for 4-7's last MFMAs, 4-7
-// re-stagger after their stores) instead of each half beside the other half's MFMAs
-constexpr bool kTileSyncStore = false;
+// The wait rule: every wait is vmcnt(8) and never counts a tile's output stores as
+// "younger" ops: the first wait after the stores (the next tile's first phase) also waits
+// for them to complete.  A phase waits for its own fragment reads after its first barrier,
+// just before its MFMAs (the reads overlap the barrier wait; cdna_hip_programming.md's 8-phase
+// template order).  (Reading phase 1's B-right fragments right after phase 0's first barrier,
+// to overlap phase 0's MFMAs, reads an unlanded half-tile: waves 4-7 pass their phase-0 wait
+// only after that barrier — the stagger needs the read one phase after the wait; measured
+// wrong in every launch.)  The store placements, wave priorities and wait forms measured
+// against this one live in git history, not in the product source.
 
 }  // namespace
-
-__device__ void tg_stamp_sink(int idx, unsigned long long t);
 
 template <int WGM, int TMH, int TNH, int NK, bool NORM = false, int NC = 1>
 __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) {
@@ -443,7 +417,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       }
     }
   };
-  int prev_t = -1;   // kTileDeferStore: the tile whose A-bottom half is still to be stored
   int sig_mt = -1;   // NORM: the producer row block wave 4 counts in after its next barrier
   int pend_mt = -1;  // NORM: the polled row block normalised at the end of the next tile
 
@@ -453,33 +426,22 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
 
   // ---- prologue: K-tiles 0 (all four halves) and 1 (A top, B left) of the first tile;
   // the wait retires what the first phases read before their own waits run (A top / B left
-  // of K-tile 0; kTileStoreWait 1 skips the first two waits: all of K-tile 0)
+  // of K-tile 0)
   issue(cur0, 0, 0, 0);
   issue(cur0, 2, 0, 0);
   issue(cur0, 3, 0, 0);
   issue(cur0, 1, 0, 0);
   issue(cur0, 0, 1, 1);
   issue(cur0, 2, 1, 1);
-  tg_wait_vm<kTileStoreWait == 1 ? VM / 2 : VM>();
+  tg_wait_vm<VM>();
   tg_barrier();
   if (wave >= 4) tg_barrier();  // stagger: waves 4-7 run one barrier behind
-  if constexpr (kTilePrio == 2) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  }
 
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
     static_for<QI * 4>([&](auto ic) __attribute__((always_inline)) {
       constexpr int q = decltype(ic)::value / 4, P = decltype(ic)::value % 4;
       constexpr int kt = q % NK, tp = q / NK, buf = q & 1;
-      auto stamp = [&](int point) __attribute__((always_inline)) {
-        if constexpr (kTileStamps) {
-          if (blockIdx.x == 0 && it == 2 && (wave == 0 || wave == 4) && lane == 0)
-            tg_stamp_sink(((wave >> 2) * (QI * 4) + decltype(ic)::value) * 5 + point,
-                          __builtin_amdgcn_s_memtime());
-        }
-      };
-      stamp(0);
       // 1. this phase's half-tile: p0 B right (q+1), p1 A bottom (q+1), p2 A top (q+2),
       //    p3 B left (q+2); past the iteration it belongs to the next one's first tile
       constexpr int qt = q + (P < 2 ? 1 : 2);
@@ -492,17 +454,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
       if constexpr (P == 1) read_b(buf, 1);
       if constexpr (P == 2) read_a(buf, 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!kTileLgkmLate) tg_wait_lgkm0();
       // 3. retire the half-tile(s) the next phase reads (never counting output stores)
-      if constexpr (kTileStoreWait == 0) {
-        if constexpr (P != 2) tg_wait_vm<VM>();
-      } else {
-        if constexpr (P == 3 && kt == NK - 1) tg_wait_vm<VM / 2>();  // before the stores
-        else if constexpr (P == 3 || (P == 0 && kt != 0) || (P == 1 && kt != 0)) tg_wait_vm<VM>();
-      }
-      stamp(1);
+      if constexpr (P != 2) tg_wait_vm<VM>();
       tg_barrier();
-      stamp(2);
       if constexpr (NORM && P == 0 && kt == 0) {
         // every wave's stores of the previous tile completed before this barrier (waves 0-3
         // run one barrier ahead of wave 4): count the producer tile in
@@ -510,56 +464,18 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
           __hip_atomic_fetch_add(&p.cnt[16 + sig_mt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sig_mt = -1;
       }
-      if constexpr (kTileLgkmLate) {
-        tg_wait_lgkm0();
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      tg_wait_lgkm0();
+      __builtin_amdgcn_sched_barrier(0);
       // 4. the quadrant's MFMAs
-      if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(1);
       if constexpr (P == 0) mfma(0, 0);
       if constexpr (P == 1) mfma(0, 1);
       if constexpr (P == 2) mfma(1, 1);
       if constexpr (P == 3) mfma(1, 0);
-      if constexpr (kTilePrio == 1) __builtin_amdgcn_s_setprio(0);
-      stamp(3);
       tg_barrier();
-      stamp(4);
       // 5. the tile is done after its last quadrant: store it, restart the accumulators
-      if constexpr (kTileSplitStore && !NORM && P == 1 && kt == NK - 1) {
-        if constexpr (tp == 0) store_tile(cur0, 0, 1);
-        else store_tile(cur1, 0, 1);
-#pragma unroll
-        for (int i = 0; i < TMH; ++i)
-#pragma unroll
-          for (int g = 0; g < 2; ++g)
-#pragma unroll
-            for (int j = 0; j < TNH; ++j) acc[0][i][g][j] = tg_f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      if constexpr (kTileDeferStore && !NORM && P == 1 && kt == 0) {
-        if (prev_t >= 0) {  // the previous tile's A-bottom half
-          TileRes pr;
-          pr.t = prev_t;
-          store_tile(pr, 1, 2);
-#pragma unroll
-          for (int i = 0; i < TMH; ++i)
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-              for (int j = 0; j < TNH; ++j) acc[1][i][g][j] = tg_f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      if constexpr (kTileSyncStore && !NORM && P == 3 && kt == NK - 1) {
-        if (wave < 4) tg_barrier();
-      }
       if constexpr (P == 3 && kt == NK - 1) {
-        constexpr int h0 = (kTileSplitStore && !NORM) ? 1 : 0;
-        constexpr int h1 = (kTileDeferStore && !NORM) ? 1 : 2;
-        if constexpr (tp == 0) store_tile(cur0, h0, h1);
-        else store_tile(cur1, h0, h1);
-        if constexpr (kTileDeferStore && !NORM) prev_t = tp == 0 ? cur0.t : cur1.t;
-        if constexpr (kTileSyncStore && !NORM) {
-          if (wave >= 4) tg_barrier();
-        }
+        if constexpr (tp == 0) store_tile(cur0, 0, 2);
+        else store_tile(cur1, 0, 2);
         if constexpr (NORM) {
           __builtin_amdgcn_s_waitcnt(0);  // this wave's sc1 stores are acknowledged
           const int mt = cur0.t / p.ntn;
@@ -588,7 +504,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
           if (poller) pend_mt = mt;
         }
 #pragma unroll
-        for (int h = 0; h < ((kTileDeferStore && !NORM) ? 1 : 2); ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int i = 0; i < TMH; ++i)
 #pragma unroll
@@ -600,13 +516,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(const TileGemmParams p) 
     cur0 = nxt;
     if (TPI == 2) cur1 = tile_res(TPI * it + TPI + 1);
     nxt = tile_res(TPI * it + 2 * TPI);
-  }
-  if constexpr (kTileDeferStore && !NORM) {
-    if (prev_t >= 0) {
-      TileRes pr;
-      pr.t = prev_t;
-      store_tile(pr, 1, 2);
-    }
   }
   // the last prefetches (out of range) still write LDS: drain before the workgroup ends
   __builtin_amdgcn_s_waitcnt(0);

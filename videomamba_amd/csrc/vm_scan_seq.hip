@@ -44,7 +44,6 @@ constexpr int kPF = 8;        // u / delta / z prefetch distance in steps
 constexpr int kMaxSeg = 256;  // segments per sequence
 constexpr int kSeqNW = 2;     // waves (channel groups of 64) per workgroup
 constexpr bool kSeqXcdRemap = true;  // grids renumbered per XCD (see scan_seq_kernel)
-constexpr bool kChunkXcdRemap = false;
 constexpr bool kSeqDeltaAhead = true;  // next step's delta computed a step early
 constexpr bool kSeqGateAhead = true;   // next step's output-gate factor computed a step early
 
@@ -523,37 +522,6 @@ constexpr int kDtG = 16;    // steps per dt block
 // gaps (s_nop) instead of the step's tail
 constexpr bool kDtpYLate = true;
 constexpr int kDtRow = 10;  // dwords per channel row of the LDS dt block (16 bf16 + pad)
-// kDtpD16: u / z / dt reach the step as fp32 with no unpacking VALU (round 5):
-// u and z by buffer_load_short_d16_hi (the bf16 lands in the high half of a VGPR whose low
-// half is 0: the fp32 value), dt as one dword per step in the LDS block (v_cvt_pk_bf16_f32
-// with a zero low operand: the same RNE rounding, stored as its fp32 value).  hipcc emits
-// no d16_hi loads, so these loads are inline asm and every wait on them is counted here:
-// loads return in order, so `vmcnt(younger loads)` retires a load whatever the stores do.
-constexpr bool kDtpD16 = false;
-constexpr int kDtRowD16 = 20;  // dwords per channel row (16 steps + pad; 16-B aligned rows)
-__device__ __forceinline__ void d16_load(float& dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  asm volatile("buffer_load_short_d16_hi %0, %1, %2, %3 offen" : "+v"(dst) : "v"(voff), "s"(r), "s"(soff));
-}
-// the prologue's form: its descriptor may come straight from v_readfirstlane (a VALU SGPR
-// write that a VMEM read of it must trail by 4 wait states; hipcc pads no asm operand)
-__device__ __forceinline__ void d16_load_first(float& dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  asm volatile("s_nop 4\n\tbuffer_load_short_d16_hi %0, %1, %2, %3 offen"
-               : "+v"(dst) : "v"(voff), "s"(r), "s"(soff));
-}
-// the u refill: du2 and yd (the old u's products) pass through the statement, so the old
-// value's last uses come before it and its register takes the load (no copy)
-__device__ __forceinline__ void d16_load_u(float& dst, __attribute__((ext_vector_type(2))) float& du2,
-                                           float& yd, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  asm volatile("buffer_load_short_d16_hi %0, %3, %4, %5 offen"
-               : "+v"(dst), "+v"(du2), "+v"(yd) : "v"(voff), "s"(r), "s"(soff));
-}
-// s_waitcnt vmcnt(N) that the consumers of a and b cannot be scheduled above
-template <int N>
-__device__ __forceinline__ void d16_wait(float& a, float& b) {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
-}
-
 typedef short dtp_s4 __attribute__((ext_vector_type(4)));
 typedef __bf16 dtp_b2 __attribute__((ext_vector_type(2)));
 typedef float dtp_f2 __attribute__((ext_vector_type(2)));
@@ -573,7 +541,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   constexpr int ES = 2;
   constexpr int KP = 16 * NKS + 4;    // bf16 per LDS W_dt row (8-byte pad: fewer bank conflicts)
   __shared__ __attribute__((aligned(16))) bf16_t sW[NW][64 * KP];
-  constexpr int DR = kDtpD16 ? kDtRowD16 : kDtRow;
+  constexpr int DR = kDtRow;
   __shared__ __attribute__((aligned(16))) uint32_t sD[NW][64 * DR];
 
   const int tid = threadIdx.x;
@@ -646,23 +614,12 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   const int a_last = 16 * (NKS - 1) + 4 * (lane >> 4) < q.dt_rank
                          ? a_voff + 16 * (NKS - 1) * ES
                          : static_cast<int>(0x80000000u);
-  // the in-loop form (hand-counted beside the d16 loads when kDtpD16) and the prologue's
-  // compiler-counted form (an asm load's destination may be copied before it lands: the
-  // prologue, which waits for it at once, keeps the builtin)
-  auto a_load = [&](int tg, uint2 (&af)[NKS], bool in_loop = true) {
+  auto a_load = [&](int tg, uint2 (&af)[NKS]) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const int off = ks == NKS - 1 ? a_last : a_voff + 16 * ks * ES;
-      if (kDtpD16 && in_loop) {
-        typedef unsigned au2 __attribute__((ext_vector_type(2)));
-        au2 v;
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen"
-                     : "=v"(v) : "v"(off), "s"(dtr), "s"(tg * dls));
-        af[ks] = uint2{v[0], v[1]};
-      } else {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(dtr, off, tg * dls, 0);
-        af[ks] = uint2{v[0], v[1]};
-      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(dtr, off, tg * dls, 0);
+      af[ks] = uint2{v[0], v[1]};
     }
   };
   // in stages, so no step waits on a dependent MFMA / LDS chain: the MFMAs of channel
@@ -682,36 +639,24 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
       }
     }
   };
-  typedef unsigned dq_t __attribute__((ext_vector_type(kDtpD16 ? 4 : 2)));
+  typedef unsigned dq_t __attribute__((ext_vector_type(2)));
   auto dt_store = [&]() {
 #pragma unroll
     for (int tile = 0; tile < 4; ++tile) {
       // D[4 (lane>>4) + i][lane & 15] -> channel 16 tile + (lane & 15), steps 4 (lane>>4) + i
-      if constexpr (kDtpD16) {  // one dword per step: bf16(v) << 16 = the rounded value in fp32
-        typedef unsigned dq4_t __attribute__((ext_vector_type(4)));
-        const dq4_t v = {cvt_pk_bf16(0.0f, dacc[tile][0]), cvt_pk_bf16(0.0f, dacc[tile][1]),
-                         cvt_pk_bf16(0.0f, dacc[tile][2]), cvt_pk_bf16(0.0f, dacc[tile][3])};
-        *reinterpret_cast<dq4_t*>(&sD[wave][(16 * tile + (lane & 15)) * DR + 4 * (lane >> 4)]) = v;
-      } else {
-        const uint32_t p01 = cvt_pk_bf16(dacc[tile][0], dacc[tile][1]);
-        const uint32_t p23 = cvt_pk_bf16(dacc[tile][2], dacc[tile][3]);
-        typedef unsigned dq2_t __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<dq2_t*>(&sD[wave][(16 * tile + (lane & 15)) * DR + 2 * (lane >> 4)]) =
-            dq2_t{p01, p23};
-      }
+      const uint32_t p01 = cvt_pk_bf16(dacc[tile][0], dacc[tile][1]);
+      const uint32_t p23 = cvt_pk_bf16(dacc[tile][2], dacc[tile][3]);
+      *reinterpret_cast<dq_t*>(&sD[wave][(16 * tile + (lane & 15)) * DR + 2 * (lane >> 4)]) =
+          dq_t{p01, p23};
     }
   };
   // a lane's own channel, steps 4k .. 4k+3 of the block
   auto dq_read = [&](int k) {
-    return *reinterpret_cast<const dq_t*>(&sD[wave][lane * DR + (kDtpD16 ? 4 : 2) * k]);
+    return *reinterpret_cast<const dq_t*>(&sD[wave][lane * DR + 2 * k]);
   };
   auto dt_of = [&](const dq_t& dq, int j) {  // step j % 4 of a quad
-    if constexpr (kDtpD16) {
-      return __uint_as_float(dq[j & 3]);
-    } else {
-      const uint32_t w = (j & 2) ? dq[1] : dq[0];
-      return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
-    }
+    const uint32_t w = (j & 2) ? dq[1] : dq[0];
+    return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
   };
   auto delta_of = [&](float dr) {  // delta' = softplus(dt + bias) * log2e (log2 units)
     const float x = fmaf(dr, kLog2e, bias);
@@ -724,7 +669,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
 
   // prologue: block 0's dt, the first quad, u / z / B|C of the first kPF steps
   uint2 af[NKS];
-  a_load(0, af, false);
+  a_load(0, af);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();  // sW is written (each wave reads only its own rows; one barrier is cheap)
   dt_mfma(af, 0, 4);
@@ -732,36 +677,19 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   dq_t dqa[4];  // the block's four quads (steps 4k .. 4k+3), each read a quad ahead
   dqa[0] = dq_read(0);
   dqa[1] = dqa[2] = dqa[3] = dqa[0];
-  // kDtpD16: fu / fz hold u / z as fp32 (low halves 0 from here on: only d16_hi loads write
-  // them); otherwise ru / rz hold the raw bf16
+  // ru / rz hold the raw bf16 of u / z
   uint32_t ru[kPF], rz[kPF];
-  float fu[kPF], fz[kPF];
   bc_load(0, bcw[0]);
 #pragma unroll
   for (int j = 0; j < kPF; ++j) {
     const int t = min(j, tlast);
-    if constexpr (kDtpD16) {
-      fu[j] = 0.0f;
-      fz[j] = 0.0f;
-      d16_load_first(fu[j], ur, voff, t * us);
-      d16_load_first(fz[j], zr, voff, t * zs);
-    } else {
-      ru[j] = bload<T>(ur, voff, t * us);
-      rz[j] = bload<T>(zr, voff, t * zs);
-    }
+    ru[j] = bload<T>(ur, voff, t * us);
+    rz[j] = bload<T>(zr, voff, t * zs);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (kDtpD16) {
-    d16_wait<0>(fu[0], fz[0]);  // (the prologue's loads: all landed, the dt operands too)
-#pragma unroll
-    for (int j = 1; j < kPF; ++j) asm volatile("" : "+v"(fu[j]), "+v"(fz[j]));
-  }
   __builtin_amdgcn_s_waitcnt(0);
-  auto gate_f = [&](float zz) {
-    return zz * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e));
-  };
   float dl_nx = delta_of(dt_of(dqa[0], 0));
-  float g_nx = kDtpD16 ? gate_f(fz[0]) : gate_of(rz[0]);
+  float g_nx = gate_of(rz[0]);
   // kDtpYLate: the previous step's y accumulators, gate and store offset (dead: out of range)
   f2 ya_p = {0.0f, 0.0f}, yb_p = {0.0f, 0.0f};
   float gf_p = 0.0f;
@@ -779,26 +707,15 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     float dl = dl_nx;
     dl = live ? dl : 0.0f;
     const f2 dl2 = {dl, dl};
-    f2 du2, ya;
-    if constexpr (kDtpD16) {
-      // u's uses first, then its slot takes the refill (no copy of the old value)
-      const float uu = fu[s];
-      du2 = dl2 * f2{uu, uu};
-      float yd = Dv * uu;
-      d16_load_u(fu[s], du2, yd, ur, vu, su);
-      d16_load(fz[s], zr, vz, sz);
-      ya = f2{yd, 0.0f};
-    } else {
-      const float uu = raw_f32<T>(ru[s]);
-      ru[s] = bload<T>(ur, vu, su);
-      rz[s] = bload<T>(zr, vz, sz);
-      // du as a genuine register pair (one packed multiply): a {du, du} pair formed with
-      // op_sel leaves its unused half free for the allocator, which can make it the
-      // destination of an in-flight refill load — the packed read then waits for that load
-      // (a vmcnt(1) at the block head)
-      du2 = dl2 * f2{uu, uu};
-      ya = f2{Dv * uu, 0.0f};
-    }
+    const float uu = raw_f32<T>(ru[s]);
+    ru[s] = bload<T>(ur, vu, su);
+    rz[s] = bload<T>(zr, vz, sz);
+    // du as a genuine register pair (one packed multiply): a {du, du} pair formed with
+    // op_sel leaves its unused half free for the allocator, which can make it the
+    // destination of an in-flight refill load — the packed read then waits for that load
+    // (a vmcnt(1) at the block head)
+    const f2 du2 = dl2 * f2{uu, uu};
+    f2 ya = f2{Dv * uu, 0.0f};
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this step's B|C rows have landed
     bc_load(t + 1 < tlast ? t + 1 : tlast, bcw[(j + 1) & 1]);
     __builtin_amdgcn_sched_barrier(0);
@@ -810,16 +727,7 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     // current quad, the next quad (j % 4 == 3), or the next block's first quad (j == 15)
     dl_nx = delta_of(dt_of(dqa[((j + 1) >> 2) & 3], (j + 1) & 3));
     const float gf = g_nx;
-    if constexpr (kDtpD16) {
-      // slot s + 1 (step t + 1) was loaded 7 steps ago: younger loads are the 7 steps since
-      // (u, z each) and, in block steps 0 .. 7, the dt_low rows issued at block step 0
-      const int sn = (s + 1) & (kPF - 1);
-      if ((j & 15) <= 7) d16_wait<2 * (kPF - 1) + NKS>(fz[sn], fu[sn]);
-      else d16_wait<2 * (kPF - 1)>(fz[sn], fu[sn]);
-      g_nx = gate_f(fz[sn]);
-    } else {
-      g_nx = gate_of(rz[(s + 1) & (kPF - 1)]);
-    }
+    g_nx = gate_of(rz[(s + 1) & (kPF - 1)]);
     const uint32_t (&cw)[2 * NWD] = bcw[j & 1];
     f2 yb = {0.0f, 0.0f};
 #pragma unroll
@@ -851,13 +759,6 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
   auto around = [&](const int tg, const int j) {
     if (j == 0) a_load(tg + kDtG, afn);
     if ((j & 3) == 0 && j < 12) dqa[(j >> 2) + 1] = dq_read((j >> 2) + 1);
-    if constexpr (kDtpD16) {
-      if (j == 9) {  // issued at block step 0: the u / z refills of steps 1 .. 9 are younger
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
-          asm volatile("s_waitcnt vmcnt(%2)" : "+v"(afn[ks].x), "+v"(afn[ks].y) : "i"(2 * 9));
-      }
-    }
     if (j == 9) dt_mfma(afn, 0, 2);
     if (j == 10) dt_mfma(afn, 2, 4);
     if (j == 12) dt_store();
@@ -888,7 +789,6 @@ __global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel(const ScanPar
     }
   }
   if constexpr (kDtpYLate) y_finish(ya_p, yb_p, gf_p, vo_p, so_p);  // the last step's y
-  if constexpr (kDtpD16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm refills
   if (L > 0) {
 #pragma unroll
     for (int n = 0; n < kMaxN; ++n)
@@ -976,7 +876,6 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;
-  if constexpr (kChunkXcdRemap) xcd_order(gx, gy, gz);  // a block's channel groups share an XCD
   const int blk = gy;
   const int b = gz;
   const int d0 = __builtin_amdgcn_readfirstlane(gx * 64);

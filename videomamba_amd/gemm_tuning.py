@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import threading
 
 import torch
 
@@ -25,6 +26,12 @@ from . import options
 RESULTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning",
                        "tunableop_gfx950.csv")
 _loaded = {"mode": None}
+# TunableOp's enable flags are process-wide: nested and concurrent users (the sub-batch
+# forward's issue threads) share one switch, turned on by the first to enter and restored to
+# the caller's setting by the last to leave (one thread's exit must not switch it
+# off under another thread's GEMM)
+_lock = threading.Lock()
+_users = {"n": 0, "saved": None, "mode": None}
 
 
 def _prepare(mode: str) -> bool:
@@ -50,17 +57,37 @@ def _prepare(mode: str) -> bool:
 
 @contextlib.contextmanager
 def tuned():
-    """Run the enclosed GEMMs with the shipped TunableOp results (see module doc)."""
+    """Run the enclosed GEMMs with the shipped TunableOp results (see module doc).
+    Re-entrant and thread-safe: the switch stays on while any thread is inside."""
     mode = options.get().gemm_tuning
-    if mode == "off" or torch.are_deterministic_algorithms_enabled() or not _prepare(mode):
+    if mode == "off" or torch.are_deterministic_algorithms_enabled():
         yield False
         return
     tun = torch.cuda.tunable
-    was_on, was_tuning = tun.is_enabled(), tun.tuning_is_enabled()
-    tun.enable(True)
-    tun.tuning_enable(mode == "tune")
+    with _lock:
+        if _users["n"] == 0:
+            if not _prepare(mode):
+                ok = False
+            else:
+                _users["saved"] = (tun.is_enabled(), tun.tuning_is_enabled())
+                _users["mode"] = mode
+                tun.enable(True)
+                tun.tuning_enable(mode == "tune")
+                ok = True
+        else:
+            ok = _users["mode"] is not None
+        if ok:
+            _users["n"] += 1
+    if not ok:
+        yield False
+        return
     try:
         yield True
     finally:
-        tun.tuning_enable(was_tuning)
-        tun.enable(was_on)
+        with _lock:
+            _users["n"] -= 1
+            if _users["n"] == 0:
+                was_on, was_tuning = _users["saved"]
+                tun.tuning_enable(was_tuning)
+                tun.enable(was_on)
+                _users["saved"] = _users["mode"] = None

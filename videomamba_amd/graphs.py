@@ -176,12 +176,18 @@ class StreamingChunkGraph:
         return self._ws
 
     def check(self) -> None:
-        """Raise if a replayed one-launch scan ever timed out on a block hand-off (its
-        outputs were NaN); synchronises with the queued replays.  See K.check_scan_sync."""
+        """Raise if a replayed one-launch scan ever timed out on a block hand-off, or a
+        replayed fused out_proj + add + RMSNorm on a row-block hand-off (their outputs were
+        NaN); synchronises with the queued replays.  See K.check_scan_sync and
+        K.check_linear_add_norm."""
         if self._sync is not None and K.scan_sync_status(self._sync):
             K.clear_scan_sync_error(self._sync)
             raise RuntimeError("StreamingChunkGraph: a replayed one-launch scan timed out on a "
                                "block hand-off; the affected outputs were NaN")
+        if self._cnt is not None and K.linear_add_norm_status(self._cnt):
+            self._cnt.zero_()  # whole buffer: late producers may have left counts behind
+            raise RuntimeError("StreamingChunkGraph: a replayed fused out_proj + add + RMSNorm "
+                               "timed out on a row-block hand-off; the affected rows were NaN")
 
     def _capture(self, has_cls: bool, parity: int):
         # the warm-up passes advance the ssm states in place and write the other conv

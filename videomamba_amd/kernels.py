@@ -19,6 +19,7 @@ its padded channel-major layouts.
 
 from __future__ import annotations
 
+import threading
 import weakref
 from typing import Optional, Tuple
 
@@ -96,8 +97,17 @@ def _channel_contig(t: Optional[Tensor]) -> Optional[Tensor]:
 
 
 # --------------------------------------------------------------------------- raw launchers
+class _Slot(threading.local):
+    """A per-host-thread override slot.  The sub-batch forward issues its streams from one
+    host thread each (videomamba._issue_phase_locked): an override entered on one thread (a
+    graph capture's scratch, sync and counter buffers) must never reach a launch issued by
+    another thread onto another stream, which would then share those buffers unordered."""
+
+    value = None
+
+
 _WORKSPACE = {}
-_WS_OVERRIDE = [None]
+_WS_OVERRIDE = _Slot()
 
 
 class scratch_override:
@@ -111,12 +121,12 @@ class scratch_override:
         self.buf = buf
 
     def __enter__(self):
-        self.prev = _WS_OVERRIDE[0]
-        _WS_OVERRIDE[0] = self.buf
+        self.prev = _WS_OVERRIDE.value
+        _WS_OVERRIDE.value = self.buf
         return self.buf
 
     def __exit__(self, *exc):
-        _WS_OVERRIDE[0] = self.prev
+        _WS_OVERRIDE.value = self.prev
         return False
 
 
@@ -128,7 +138,7 @@ def scratch(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
     never reach this cache."""
     if nbytes <= 0:
         return None
-    ov = _WS_OVERRIDE[0]
+    ov = _WS_OVERRIDE.value
     if ov is not None:
         if ov.numel() < nbytes:
             raise RuntimeError(f"scratch_override buffer too small: {ov.numel()} < {nbytes}")
@@ -142,7 +152,7 @@ def scratch(device: torch.device, stream: int, nbytes: int) -> Optional[Tensor]:
 
 
 _SYNC = {}
-_SYNC_OVERRIDE = [None]
+_SYNC_OVERRIDE = _Slot()
 _SYNC_SEEN = weakref.WeakValueDictionary()  # id -> caller-owned sync buffer (sync_override)
 
 
@@ -155,13 +165,13 @@ class sync_override:
         self.buf = buf
 
     def __enter__(self):
-        self.prev = _SYNC_OVERRIDE[0]
-        _SYNC_OVERRIDE[0] = self.buf
+        self.prev = _SYNC_OVERRIDE.value
+        _SYNC_OVERRIDE.value = self.buf
         _SYNC_SEEN[id(self.buf)] = self.buf
         return self.buf
 
     def __exit__(self, *exc):
-        _SYNC_OVERRIDE[0] = self.prev
+        _SYNC_OVERRIDE.value = self.prev
         return False
 
 
@@ -172,7 +182,7 @@ def sync_buffer(device: torch.device, stream: int, nbytes: int) -> Optional[Tens
     more."""
     if nbytes <= 0:
         return None
-    ov = _SYNC_OVERRIDE[0]
+    ov = _SYNC_OVERRIDE.value
     if ov is not None:
         return ov if ov.numel() >= nbytes else None
     key = (device.type, device.index, stream)
@@ -463,7 +473,8 @@ def linear(x: Tensor, w: Tensor, b32: Optional[Tensor] = None,
 
 
 _CNT = {}
-_CNT_OVERRIDE = [None]
+_CNT_OVERRIDE = _Slot()
+_CNT_SEEN = weakref.WeakValueDictionary()  # id -> caller-owned counter buffer (counter_override)
 
 
 class counter_override:
@@ -475,17 +486,18 @@ class counter_override:
         self.buf = buf
 
     def __enter__(self):
-        self.prev = _CNT_OVERRIDE[0]
-        _CNT_OVERRIDE[0] = self.buf
+        self.prev = _CNT_OVERRIDE.value
+        _CNT_OVERRIDE.value = self.buf
+        _CNT_SEEN[id(self.buf)] = self.buf
         return self.buf
 
     def __exit__(self, *exc):
-        _CNT_OVERRIDE[0] = self.prev
+        _CNT_OVERRIDE.value = self.prev
         return False
 
 
 def counter_buffer(device: torch.device, stream: int, nbytes: int) -> Tensor:
-    ov = _CNT_OVERRIDE[0]
+    ov = _CNT_OVERRIDE.value
     if ov is not None:
         if ov.numel() < nbytes:
             raise RuntimeError(f"counter_override buffer too small: {ov.numel()} < {nbytes}")
@@ -500,6 +512,34 @@ def counter_buffer(device: torch.device, stream: int, nbytes: int) -> Tensor:
 
 def linear_add_norm_counter_bytes(m: int) -> int:
     return int(_lib.load().vm_linear_add_norm_counter_bytes(m))
+
+
+def linear_add_norm_status(buf: Tensor) -> int:
+    """0 when no ``vm_linear_add_norm_fwd`` launch that used the counter buffer ``buf``
+    timed out waiting for a row block's producers, else non-zero (that launch's normalised
+    rows are NaN).  Reads the error word (word 0); a device buffer is copied to the host,
+    which synchronises with the work queued on it."""
+    w = buf.detach().reshape(-1)[:4].to(torch.uint8)
+    w = w.cpu() if w.is_cuda else w
+    return int.from_bytes(bytes(w.tolist()), "little")
+
+
+def check_linear_add_norm(clear: bool = True) -> None:
+    """Raise RuntimeError if any counter buffer this process has used (the per-stream ones
+    and those passed through :class:`counter_override`) recorded a timed-out hand-off of the
+    fused out_proj + add + RMSNorm.  With ``clear`` every such buffer is re-zeroed whole, not
+    just its error word: a timed-out poller resets its block's counter while late producers
+    may still add to it, which would leave a stale count that lets a later launch pass its
+    poll early.  The status read synchronises first, so every producer has finished."""
+    bad = 0
+    for buf in list(_CNT.values()) + list(_CNT_SEEN.values()):
+        if linear_add_norm_status(buf):
+            bad += 1
+            if clear:
+                buf.zero_()
+    if bad:
+        raise RuntimeError(f"fused out_proj + add + RMSNorm: {bad} counter buffer(s) recorded a "
+                           "timed-out row-block hand-off; the affected rows are NaN")
 
 
 def linear_add_norm(x: Tensor, w: Tensor, residual: Tensor, norm_w32: Tensor, eps: float,

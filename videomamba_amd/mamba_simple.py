@@ -34,9 +34,10 @@ and keeps the state in fp32 internally.  State semantics:
 
 from __future__ import annotations
 
+import contextlib
 import math
 import os
-from typing import Any, MutableMapping, Optional, Protocol, Tuple, Union
+from typing import Any, List, MutableMapping, Optional, Protocol, Tuple, Union
 
 import torch
 import torch.nn as nn
@@ -106,6 +107,32 @@ def _linear_into(x: Tensor, w: Tensor, b: Optional[Tensor], out: Tensor,
 
 
 _Z_STREAMS = {}
+
+# Measurement hook (bench.py's roofline.in_step): while a list is installed here, every
+# token-major scan launch is bracketed by two timing events on its own launch stream, so the
+# scan's duration inside a real step (beside the other sub-batch stream's kernels) can be
+# read without a profiler.  None (the default) records nothing.
+_SCAN_EVENTS: List[Optional[list]] = [None]
+
+
+@contextlib.contextmanager
+def scan_event_log():
+    """Collect (start, end, batch) timing events around every token-major scan launch in
+    the block, from every issuing thread (list.append is atomic)."""
+    log: list = []
+    prev, _SCAN_EVENTS[0] = _SCAN_EVENTS[0], log
+    try:
+        yield log
+    finally:
+        _SCAN_EVENTS[0] = prev
+
+
+def _scan_event(log: Optional[list]):
+    if log is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
 
 
 def _z_stream(device: torch.device) -> torch.cuda.Stream:
@@ -437,6 +464,8 @@ class Mamba(nn.Module):
         y = torch.empty_like(u)
         h0_s = (h0.stride(0), h0.stride(1)) if h0 is not None else (0, 0)
         hl_s = (h_last.stride(0), h_last.stride(1)) if h_last is not None else (0, 0)
+        log = _SCAN_EVENTS[0]
+        ev0 = _scan_event(log)
         if dtp:  # dt_proj inside the scan: no dt rows written or read
             _, wdt_pad = self._padded_proj_weights()
             K.scan_dtproj_raw(u, s_u, x_dbl, (Lp * E, E), R, wdt_pad, A, x_dbl[:, R:R + N],
@@ -446,6 +475,8 @@ class Mamba(nn.Module):
             K.scan_raw(u, s_u, dt, s_u, A, x_dbl[:, R:R + N], s_bc, x_dbl[:, R + N:], s_bc, Dv,
                        xz[:, Dm:], s_xz, dbias, True, h0, h0_s, h_last, hl_s,
                        y, s_u, Lp, Bsz, Dm, seqlen, N, dt_code, stream)
+        if log is not None:
+            log.append((ev0, _scan_event(log), Bsz))
         if (next_norm is not None and next_norm.residual is not None
                 and _small_gemm_ok(y, self.out_proj.weight, self.out_proj.bias, clips=Bsz)):
             # out_proj + the next block's residual add + RMSNorm in one kernel

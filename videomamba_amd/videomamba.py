@@ -687,14 +687,29 @@ class PretrainVideoMamba(nn.Module):
         ``options.batch_streams`` from ``batch_stream_min_clips`` clips and
         ``batch_stream_min_work`` clip-channels (B x d_inner) up, outside graph
         capture and the graph runner's buffers, when every layer's state (if any) is one kind
-        (full (conv, ssm) pairs of one conv dtype, or legacy ssm-only tensors)."""
+        (full (conv, ssm) pairs of one conv dtype, or legacy ssm-only tensors).
+
+        It also stays on one stream under autocast (thread-local in torch: the
+        issue threads would not inherit it), with the fused out_proj + add + RMSNorm
+        (``options.fuse_out_norm``: its pollers assume every producer workgroup of the
+        launch runs, which a concurrent launch on another stream can prevent), and when the
+        patch embed, the mixers and the final norm do not share one dtype (the split
+        forward's shared features buffer takes that dtype; the one-stream forward writes the
+        final norm's output dtype).  And it splits only where every projection runs on the
+        row-invariant HIP GEMM (``projection_gemm == "hip"``, bf16, in_proj / out_proj K in
+        the HIP GEMM's set, the fused conv_proj for x_proj): a library GEMM picks its kernel
+        by the row count, so a half-batch could round differently from the whole batch, and
+        the split forward promises the one-stream forward's bits."""
         o = options.get()
         n = int(o.batch_streams)
         B = x.shape[0]
         d_inner = int(self.layers[0].mixer.d_inner) if len(self.layers) else 0
         if (n <= 1 or B < max(int(o.batch_stream_min_clips), 2)
                 or B * d_inner < int(o.batch_stream_min_work) or tpos is not None
-                or conv_out is not None or torch.cuda.is_current_stream_capturing()):
+                or conv_out is not None
+                or (x.is_cuda and torch.cuda.is_current_stream_capturing())
+                or torch.is_autocast_enabled("cuda") or o.fuse_out_norm
+                or not self._row_invariant_projections(x, -(-B // min(n, B)))):
             return 1
         if ssm_state is not None:
             kinds = set()
@@ -709,6 +724,44 @@ class PretrainVideoMamba(nn.Module):
             if len(kinds) != 1:
                 return 1
         return min(n, B)
+
+    def _features_dtype(self) -> Optional[torch.dtype]:
+        """The dtype every forward's features take when the patch embed, every mixer and
+        the final norm share one parameter dtype (then the one-stream forward's final norm
+        writes it whether or not ``fused_add_norm``); None when they differ."""
+        dt = self.patch_embed.proj.weight.dtype
+        if self.norm.weight.dtype != dt:
+            return None
+        for layer in self.layers:
+            mx = layer.mixer
+            if mx.in_proj.weight.dtype != dt or mx.out_proj.weight.dtype != dt:
+                return None
+        return dt
+
+    def _row_invariant_projections(self, x: Tensor, part: int) -> bool:
+        """Every mixer projection of a bf16 forward of ``part``-clip sub-batches of ``x``
+        runs on the HIP GEMM (whose rows do not depend on the row count):
+        ``options.projection_gemm == "hip"``, one bf16 dtype over the model, the token-major
+        mixer, in_proj / out_proj K in vm_linear_fwd's unrolled set, no projection bias, and
+        the fused conv_proj for x_proj (dt_proj runs in it or in the scan) at the sub-batch's
+        extents (the longest chunk kind: with the CLS row)."""
+        from .mamba_simple import _SMALL_GEMM_K
+        o = options.get()
+        if (o.projection_gemm != "hip" or o.mixer_layout == "cm"
+                or self._features_dtype() != torch.bfloat16):
+            return False
+        gh, gw = self._spatial_token_grid(x.shape[-2], x.shape[-1])
+        L = self._validate_temporal_length(x.shape[2]) * gh * gw + 1
+        hn = torch.empty((1, 1, self.embed_dim), dtype=torch.bfloat16,
+                         device=x.device).expand(part, round_up(L), self.embed_dim)
+        for layer in self.layers:
+            mx = layer.mixer
+            if (mx.in_proj.weight.shape[1] not in _SMALL_GEMM_K
+                    or mx.out_proj.weight.shape[1] not in _SMALL_GEMM_K
+                    or mx.in_proj.bias is not None or mx.out_proj.bias is not None
+                    or not mx._fused_conv_proj_ok(hn, L)):
+                return False
+        return True
 
     def _prepare_param_caches(self) -> None:
         """Materialise every parameter-derived cache (fp32 copies, padded projection
@@ -765,8 +818,7 @@ class PretrainVideoMamba(nn.Module):
         has_cls = self._has_cls_token_for_forward(ssm_state, temporal_pos_offset)
         gh, gw = self._spatial_token_grid(x.shape[-2], x.shape[-1])
         L = self._validate_temporal_length(x.shape[2]) * gh * gw + (1 if has_cls else 0)
-        feats = torch.empty((B, L, self.embed_dim), dtype=self.patch_embed.proj.weight.dtype,
-                            device=dev)
+        feats = torch.empty((B, L, self.embed_dim), dtype=self._features_dtype(), device=dev)
         outs: List[Any] = [None] * parts
 
         def issue(i: int) -> None:
