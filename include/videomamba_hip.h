@@ -19,6 +19,9 @@
  *   vm_causal_conv1d_update    <- causal_conv1d_update  (mamba_simple.py:468-474)
  *   vm_conv_proj_fwd           <- causal_conv1d_fn + x_proj + dt_proj, fused, token-major
  *                                 (mamba_simple.py:381-416)
+ *   vm_in_proj_conv_proj_fwd   <- in_proj + causal_conv1d_fn + x_proj + dt_proj at small
+ *                                 batches, the conv and x_proj in in_proj's epilogue
+ *                                 (mamba_simple.py:333-339, :381-416)
  *   vm_conv_proj_cm_fwd        <- the same three steps on the channel-major small-batch
  *                                 layout (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
@@ -57,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 13
+#define VM_ABI_VERSION 14
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -286,6 +289,36 @@ int vm_conv_proj_fits(int batch, int out_len, int seqlen, int dim, int e, int r_
                       int dt_softplus, long long xz_sb, long long xz_sl, int has_conv_state_in,
                       int cs_in_dtype, long long csi_sb, long long csi_sd, int width,
                       long long u_sl);
+
+/*
+ * ABI v14.  in_proj + the mixer middle in two launches at small batches (token-major, bf16):
+ *   xz = hn @ w_in^T (mamba_simple.py:333-339) — only its z half is written, to `z`
+ *   (ntok, dim), row stride ldz; the x half stays in the GEMM's LDS tiles, where
+ *   u = silu(conv1d([conv_state_in | x])) (:381-404), written to `u` (row stride u_tl), and
+ *   the fixed 128-channel split partials of x_dbl = u @ W_x^T (:409) are formed; then
+ *   x_dbl (row stride xd_tl) and, when `dt` is not NULL, dt = x_dbl[:, :r] @ W_dt^T
+ *   (:410-413; row stride dt_tl) — every output bit-identical to vm_linear_fwd followed by
+ *   vm_conv_proj_fwd (its small-batch forms), so chunked == full stays exact.
+ * hn: (batch * out_len, k) bf16, row stride ldh; w_in: (2 dim, k) bf16, row stride ldw;
+ * k in {192, 384, 576, 768, 1152, 1536}; batch <= 8, out_len >= 56 (even), dim % 128 == 0
+ * and <= 2048, R + 2N <= 76 (e_pad <= 80), width <= 4; conv weights / state, wx_pad,
+ * wdt_pad as vm_conv_proj_fwd.  Rows with step >= seqlen get u = 0.  `workspace`:
+ * vm_in_proj_conv_proj_workspace_bytes() bytes (the x_dbl partials).
+ * vm_in_proj_conv_proj_fits: 1 when the shape is accepted (pure host code).
+ */
+int vm_in_proj_conv_proj_fwd(const void* hn, long long ldh, const void* w_in, long long ldw, int k,
+                             void* z, long long ldz, const float* conv_weight,
+                             const float* conv_bias, const void* cs_in, int cs_in_dtype,
+                             long long csi_sb, long long csi_sd, void* cs_out, int cs_out_dtype,
+                             long long cso_sb, long long cso_sd, const void* wx_pad, int e,
+                             int e_pad, const void* wdt_pad, int r, int r_pad, void* u,
+                             long long u_tl, void* xdbl, long long xd_tl, void* dt,
+                             long long dt_tl, int out_len, int batch, int dim, int seqlen,
+                             int width, void* workspace, long long workspace_bytes,
+                             vm_stream_t stream);
+long long vm_in_proj_conv_proj_workspace_bytes(int batch, int out_len, int dim, int e);
+int vm_in_proj_conv_proj_fits(int k, int batch, int out_len, int dim, int e, int e_pad,
+                              int r_pad, int width, int has_dt);
 
 /*
  * Channel-major mixer middle (bf16, small batches; the (D, B*L) layout of

@@ -1338,3 +1338,53 @@ def test_sub_batch_split_stays_off_where_it_could_change_bits():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             got = model(x)
         assert all(torch.equal(a, b) for a, b in zip(ref, got))
+
+
+@pytest.mark.parametrize("bsz", [1, 2])
+def test_in_proj_conv_epilogue_is_bitwise_the_two_kernel_model(bsz):
+    """options.in_proj_conv_clips (in_proj with the conv + SiLU and the x_proj partials in
+    its epilogue, vm_in_proj_conv_proj_fwd) changes no bit of the model: VideoMamba-M
+    16x224^2 bf16, two stateful chunks (a CLS chunk of 8 frames, then 8 more: the conv state
+    carried through the new kernel's epilogue) at B = 1 and 2 — x_vis, x_pool and every
+    layer's (conv, ssm) state equal to in_proj + conv_proj (in_proj_conv_clips = 0) — and the
+    hipGraph replay of the B = 1 chunk equals the eager call."""
+    from videomamba_amd.graphs import StreamingChunkGraph
+    from videomamba_amd.mamba_simple import Mamba
+    model = _m_model(16, add_pool_norm=True)
+    model.pool_type = "avg"
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = torch.randn(bsz, 3, 16, 224, 224, device=DEV, generator=g).to(torch.bfloat16)
+    calls = {"n": 0}
+    orig = K.in_proj_conv_proj_raw
+
+    def counting(*a, **kw):
+        calls["n"] += 1
+        return orig(*a, **kw)
+
+    outs = {}
+    for clips in (0, 2):
+        st = model.allocate_state(bsz, dtype=torch.bfloat16, device=DEV)
+        res = []
+        K.in_proj_conv_proj_raw = counting
+        try:
+            with options.override(in_proj_conv_clips=clips), torch.no_grad():
+                for off in (0, 8):
+                    xv, xp, st = model(x[:, :, off:off + 8], ssm_state=st, temporal_pos_offset=off)
+                    res.append((xv.clone(), xp.clone(), [(c.clone(), s.clone()) for c, s in st]))
+        finally:
+            K.in_proj_conv_proj_raw = orig
+        outs[clips] = res
+    assert calls["n"] == 2 * 32  # the new path ran for every layer of both chunks
+    for (av, ap, ast), (bv, bp, bst) in zip(outs[0], outs[2]):
+        assert torch.equal(av, bv) and torch.equal(ap, bp)
+        for (c0, s0), (c1, s1) in zip(ast, bst):
+            assert torch.equal(c0, c1) and torch.equal(s0, s1)
+    if bsz == 1:
+        model.pool_type = "cls+avg"
+        st = model.allocate_state(1, dtype=torch.bfloat16, device=DEV)
+        with torch.no_grad():
+            ev, ep, _ = model(x, ssm_state=st, temporal_pos_offset=0)
+            runner = StreamingChunkGraph(model, batch=1, frames=16)
+            gv, gp = runner.run(x, temporal_pos_offset=0)
+        assert torch.equal(gv, ev) and torch.equal(gp, ep)
+    assert isinstance(model.layers[0].mixer, Mamba)

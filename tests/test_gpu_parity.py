@@ -1203,3 +1203,73 @@ def test_persistent_linear_is_repeatable_at_chip_filling_rows():
         bad = sum(int(not torch.equal(K.linear(x, w, form="persistent"), r0)) for _ in range(40))
         assert bad == 0, (n, k, bad)
         del x, w, r0
+
+
+@pytest.mark.parametrize("d_model", [192, 576])
+@pytest.mark.parametrize("bsz", [1, 2, 3])
+def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
+    """vm_in_proj_conv_proj_fwd (in_proj with the conv + SiLU and the x_proj split partials
+    in its epilogue, vm_inproj_conv.hip) against the two steps it replaces: vm_linear_fwd
+    (in_proj, mamba_simple.py:333-339) then vm_conv_proj_fwd (conv + x_proj + dt_proj,
+    :381-416).  z, u, x_dbl, dt and the new conv state are bit-identical — for sequences
+    shorter than a 112-row tile and longer than many, chunks padded past their length,
+    sequence starts mid-tile (bsz > 1), a carried conv state in bf16 / fp32 or none, dt rows
+    or none (the scan computes them), and the M-16f chunk shape (3137 tokens)."""
+    from videomamba_amd.mamba_simple import Mamba
+    torch.manual_seed(d_model + bsz)
+    m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
+    C, Dm, E, R, W = d_model, m.d_inner, m.dt_rank + 2 * m.d_state, m.dt_rank, m.d_conv
+    _, _, _, cw, cb = m._fp32_params()
+    wx_pad, wdt_pad = m._padded_proj_weights()
+    w_in = m.in_proj.weight
+    st = torch.cuda.current_stream().cuda_stream
+    cases = [(57, 64, "bf16", True), (100, 112, None, False), (3, 56, "fp32", True),
+             (230, 232, "bf16", False)]
+    if d_model == 576 and bsz == 1:
+        cases.append((3137, 3144, "bf16", False))  # the B = 1 chunk (dt inside the scan)
+    for L, Lp, cs_kind, with_dt in cases:
+        n = bsz * Lp
+        hn = torch.zeros(bsz, Lp, C, device=DEV, dtype=torch.bfloat16)
+        hn[:, :L] = torch.randn(bsz, L, C, device=DEV).to(torch.bfloat16)
+        hn = hn.view(n, C)
+        cs = None
+        if cs_kind:
+            cs = torch.randn(bsz, Dm, W, device=DEV).to(
+                torch.bfloat16 if cs_kind == "bf16" else torch.float32)
+        csi_s = (cs.stride(0), cs.stride(1)) if cs is not None else (0, 0)
+        outs = []
+        for fused in (False, True):
+            cso = torch.full((bsz, Dm, W), float("nan"), device=DEV, dtype=torch.bfloat16)
+            u = torch.full((n, Dm), float("nan"), device=DEV, dtype=torch.bfloat16)
+            xd = torch.full((n, E), float("nan"), device=DEV, dtype=torch.bfloat16)
+            dt = torch.full((n, Dm), float("nan"), device=DEV, dtype=torch.bfloat16) if with_dt else None
+            xz = torch.full((n, 2 * Dm), float("nan"), device=DEV, dtype=torch.bfloat16)
+            if fused:
+                assert K.in_proj_conv_proj_fits(C, bsz, Lp, Dm, E, wx_pad.shape[0],
+                                                wdt_pad.shape[1], W, with_dt)
+                K.in_proj_conv_proj_raw(hn, w_in, xz[:, Dm:], cw, cb, cs, csi_s, cso,
+                                        (Dm * W, W), wx_pad, E, wdt_pad, R, u, xd, dt, Lp,
+                                        bsz, Dm, L, W, st)
+            else:
+                K.linear(hn, w_in, out=xz)
+                K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, csi_s, cso, (Dm * W, W),
+                                wx_pad, E, wdt_pad if with_dt else None, R, u, (Lp * Dm, Dm),
+                                xd, (Lp * E, E), dt, (Lp * Dm, Dm), Lp, bsz, Dm, L, W, st)
+            outs.append((xz[:, Dm:], u, xd, dt, cso))
+        torch.cuda.synchronize()
+        for name, a, b in zip(("z", "u", "x_dbl", "dt", "conv_state"), *outs):
+            if a is None:
+                continue
+            assert torch.equal(a, b), (L, Lp, cs_kind, name,
+                                       (a.float() - b.float()).abs().nan_to_num(9.0).max().item())
+
+
+def test_in_proj_conv_proj_rejects_unsupported_shapes():
+    """vm_in_proj_conv_proj_fits / _fwd refuse what the kernel does not cover (batch > 8,
+    chunks under 56 padded tokens, d_inner % 128, in_proj K outside the GEMM's set) — the
+    mixer then runs in_proj + conv_proj."""
+    assert K.in_proj_conv_proj_fits(576, 1, 3144, 1152, 68, 80, 64, 4, False)
+    assert not K.in_proj_conv_proj_fits(576, 9, 3144, 1152, 68, 80, 64, 4, False)
+    assert not K.in_proj_conv_proj_fits(576, 1, 48, 1152, 68, 80, 64, 4, False)
+    assert not K.in_proj_conv_proj_fits(576, 1, 3144, 1088, 68, 80, 64, 4, False)
+    assert not K.in_proj_conv_proj_fits(640, 1, 3144, 1152, 68, 80, 64, 4, False)

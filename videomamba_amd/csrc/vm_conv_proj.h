@@ -29,6 +29,8 @@ constexpr int kSkMaxBatch = 8;
 constexpr int kSkMaxEp = 76;  // round_up(R + 2N, 4) the split-K form stages per token row
 long long conv_proj_sk_workspace_bytes(int batch, int out_len, int dim, int e);
 void conv_proj_sk_launch(const ConvProjTmArgs& a, float* part, hipStream_t s);
+// its second kernel alone (partials -> x_dbl [-> dt]), shared with vm_inproj_conv.hip
+void conv_proj_sk_reduce_launch(const ConvProjTmArgs& a, float* part, hipStream_t s);
 // The fused small-batch form (one launch, no partials; bit-identical to the split-K form)
 // for dim <= 1152 and out_len >= 16.
 bool conv_proj_fused_ok(const ConvProjTmArgs& a);

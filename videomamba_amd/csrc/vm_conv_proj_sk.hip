@@ -1035,6 +1035,19 @@ void conv_proj_sk_launch(const ConvProjTmArgs& a, float* part, hipStream_t s) {
     VM_SK_CASE(5) VM_SK_CASE(6) VM_SK_CASE(7) VM_SK_CASE(8)
 #undef VM_SK_CASE
   }
+  conv_proj_sk_reduce_launch(a, part, s);
+}
+
+// The split-K form's second kernel alone: x_dbl from the partials, dt_proj (a.wdt) — also
+// the tail of vm_in_proj_conv_proj_fwd, whose in_proj epilogue writes the same partials.
+void conv_proj_sk_reduce_launch(const ConvProjTmArgs& a, float* part, hipStream_t s) {
+  SkTmParams q{};
+  q.a = a;
+  q.part = part;
+  q.ntok = a.batch * a.out_len;
+  q.nsplit = (a.dim + kSkCh - 1) / kSkCh;
+  q.ep = (a.e + 3) / 4 * 4;
+  const unsigned tiles = static_cast<unsigned>((q.ntok + kCmTok - 1) / kCmTok);
   const unsigned cblocks = a.wdt ? static_cast<unsigned>((a.dim + 127) / 128) : 1u;
   const dim3 g2(tiles, cblocks);
   switch (q.nsplit) {

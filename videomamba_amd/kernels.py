@@ -402,6 +402,36 @@ def conv_proj_raw(xz, xz_s, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e, 
     _lib.check(rc, "vm_conv_proj_fwd")
 
 
+def in_proj_conv_proj_fits(k: int, batch: int, out_len: int, dim: int, e: int, e_pad: int,
+                           r_pad: int, width: int, has_dt: bool) -> bool:
+    """Whether ``vm_in_proj_conv_proj_fwd`` takes this shape (pure host query)."""
+    return bool(_lib.load().vm_in_proj_conv_proj_fits(k, batch, out_len, dim, e, e_pad, r_pad,
+                                                      width, int(has_dt)))
+
+
+def in_proj_conv_proj_raw(hn, w_in, z, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e,
+                          wdt_pad, r, u, xdbl, dt, out_len, batch, dim, seqlen, width, stream):
+    """in_proj + conv1d + SiLU -> x_proj [-> dt_proj] in two launches (bf16, small batches,
+    token-major): hn (n, k), w_in (2 dim, k); z (n, dim) receives in_proj's z half (any row
+    stride, e.g. the right half of an (n, 2 dim) xz), u (n, dim), xdbl (n, e), dt (n, dim) or
+    None (the scan computes dt).  Bit-identical to ``linear`` + :func:`conv_proj_raw`.
+    Scratch for the x_proj partials comes from :func:`scratch`."""
+    lib = _lib.load()
+    nbytes = int(lib.vm_in_proj_conv_proj_workspace_bytes(batch, out_len, dim, e))
+    ws = scratch(hn.device, int(stream), nbytes)
+    rc = lib.vm_in_proj_conv_proj_fwd(
+        _p(hn), hn.stride(0), _p(w_in), w_in.stride(0), hn.shape[1], _p(z), z.stride(0),
+        _p(cw32), _p(cb32),
+        _p(cs_in), dtype_code(cs_in.dtype) if cs_in is not None else 0, csi_s[0], csi_s[1],
+        _p(cs_out), dtype_code(cs_out.dtype) if cs_out is not None else 0, cso_s[0], cso_s[1],
+        _p(wx_pad), e, wx_pad.shape[0], _p(wdt_pad if dt is not None else None), r,
+        wdt_pad.shape[1] if (wdt_pad is not None and dt is not None) else 0,
+        _p(u), u.stride(0), _p(xdbl), xdbl.stride(0), _p(dt),
+        dt.stride(0) if dt is not None else 0, out_len, batch, dim, seqlen, width,
+        _p(ws), nbytes, stream)
+    _lib.check(rc, "vm_in_proj_conv_proj_fwd")
+
+
 def conv_proj_fits(batch: int, out_len: int, seqlen: int, dim: int, e: int, r_pad: int,
                    xz_s, u_sl: int, cs_in: Optional[Tensor], width: int) -> bool:
     """Whether ``vm_conv_proj_fwd`` accepts this token-major shape (``vm_conv_proj_fits``):

@@ -380,6 +380,23 @@ class Mamba(nn.Module):
         _, _, _, cw, cb = self._fp32_params()
         s_u, s_xz = (Lp * Dm, 1, Dm), (Lp * 2 * Dm, 1, 2 * Dm)
         z_side = None
+        if bufs is None and self._in_proj_conv_ok(hn, seqlen, want_dt):
+            # in_proj with the conv + SiLU and the x_proj split partials in its epilogue
+            # (vm_in_proj_conv_proj_fwd): x stays in the GEMM's LDS tiles; bit-identical to
+            # the in_proj + conv_proj pair below
+            wx_pad, wdt_pad = self._padded_proj_weights()
+            xz = torch.empty((n, 2 * Dm), dtype=hn.dtype, device=hn.device)  # z half written
+            u = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device)
+            x_dbl = torch.empty((n, E), dtype=hn.dtype, device=hn.device)
+            dt = torch.empty((n, Dm), dtype=hn.dtype, device=hn.device) if want_dt else None
+            csi_s = ((conv_state_in.stride(0), conv_state_in.stride(1))
+                     if conv_state_in is not None else (0, 0))
+            cso_s = ((conv_state_out.stride(0), conv_state_out.stride(1))
+                     if conv_state_out is not None else (0, 0))
+            K.in_proj_conv_proj_raw(hn.view(n, C), self.in_proj.weight, xz[:, Dm:], cw, cb,
+                                    conv_state_in, csi_s, conv_state_out, cso_s, wx_pad, E,
+                                    wdt_pad, R, u, x_dbl, dt, Lp, Bsz, Dm, seqlen, W, stream)
+            return xz, u, x_dbl, dt
         if bufs is None and self._split_in_proj_ok(hn, Bsz):
             # in_proj as two launches: x (what conv_proj needs) here, z (what only the scan's
             # gate reads) on a side stream, so it runs beside conv_proj; the current stream
@@ -433,6 +450,25 @@ class Mamba(nn.Module):
         if z_side is not None:  # the z half is complete before anything after this reads xz
             torch.cuda.current_stream(hn.device).wait_stream(z_side)
         return xz, u, x_dbl, dt
+
+    def _in_proj_conv_ok(self, hn: Tensor, seqlen: int, want_dt: bool) -> bool:
+        """in_proj runs with the conv and the x_proj partials in its epilogue
+        (``options.in_proj_conv_clips``): streaming batches whose in_proj would take the
+        row-tile HIP GEMM, the fused conv_proj path (bf16, its shape limits) and the shapes
+        ``vm_in_proj_conv_proj_fwd`` takes (in_proj K in the GEMM's set, d_inner % 128 == 0,
+        a chunk of at least 56 padded tokens)."""
+        o = options.get()
+        Bsz, Lp, C = hn.shape
+        if (Bsz > o.in_proj_conv_clips or o.projection_gemm != "hip" or o.in_proj_z_stream
+                or self.in_proj.bias is not None or not self._fused_conv_proj_ok(hn, seqlen)):
+            return False
+        w = self.in_proj.weight
+        if not _small_gemm_ok(hn.view(Bsz * Lp, C), w, None, clips=Bsz):
+            return False
+        wx_pad, wdt_pad = self._padded_proj_weights()
+        E = self.dt_rank + 2 * self.d_state
+        return K.in_proj_conv_proj_fits(C, Bsz, Lp, self.d_inner, E, wx_pad.shape[0],
+                                        wdt_pad.shape[1], self.d_conv, want_dt)
 
     def _split_in_proj_ok(self, hn: Tensor, clips: int) -> bool:
         """in_proj runs as x / z halves on two streams (``options.in_proj_z_stream``) at

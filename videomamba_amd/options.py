@@ -83,6 +83,13 @@ documented options object; tests and sweeps change them with :func:`override`.
                      rows do not depend on the column count).  Measured slower: the B = 1
                      graph replay 2.97-2.99 vs 2.56-2.58 ms (each cross-stream edge of the
                      replayed graph costs more than the z half's ~6 us), so it is off.
+    in_proj_conv_clips
+                     Mixers of at most this many clips (default 2; 0 turns it off) run in_proj
+                     with the depthwise conv + SiLU and the x_proj split partials in its
+                     epilogue (``vm_in_proj_conv_proj_fwd``, vm_inproj_conv.hip): x never
+                     reaches HBM and conv_proj's per-tile W_x stream is gone.  Bit-identical
+                     to in_proj + conv_proj (the split-K form's arithmetic), so the choice
+                     never changes a result.
     small_gemm_rows  ("library" mode) in_proj / out_proj with at most this many token rows (one clip's
                      chunk) run on the HIP small-M GEMM (vm_linear_fwd, bf16); larger ones,
                      or 0, on the library.  Default 4096 (B = 1 at M-16f: 3144 rows).
@@ -121,6 +128,7 @@ class Options:
     batch_stream_lock: bool = True
     in_proj_z_stream: bool = False
     in_proj_split_clips: int = 8
+    in_proj_conv_clips: int = 2
     batch_stream_min_clips: int = 224
     batch_stream_min_work: int = 224 * 1152
     small_gemm_rows: int = 4096
