@@ -261,6 +261,36 @@ def scan_in_step(step, L=3137, D=1152, N=16):
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
+def _graph_us(fn, reps, calls=20):
+    """Average device time of fn() as replayed from a captured HIP graph of ``calls``
+    back-to-back calls (HIP events around ``reps`` replays): what the B = 1 chunk's own graph
+    sees per kernel, including the dependent-kernel boundary — eager launches from Python at
+    these sizes measure the host's issue rate instead (~20 us per call).  Kernel scratch
+    comes from one buffer owned here (scratch_override), as the chunk graph's does."""
+    from videomamba_amd import kernels as K
+    ws = torch.empty(1 << 27, dtype=torch.uint8, device="cuda")
+    with K.scratch_override(ws):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(calls):
+                fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * calls)
+
+
 def _event_us(fn, reps):
     """Average HIP-event time of fn() on the current stream, after warm-up."""
     for _ in range(3):
@@ -283,7 +313,12 @@ def b1_kernel_rooflines(device, reps=50):
     in_proj GEMM, fused conv+x_proj (+ conv state out; + dt_proj only when the mixer keeps it
     there), the scan (scan_roofline at B=1: the segmented chunk form, computing dt_proj per
     segment when the mixer does), out_proj GEMM — each the kernel the mixer runs for a
-    one-clip chunk (the projections on the row-invariant HIP GEMM, clips=1)."""
+    one-clip chunk (the projections on the row-invariant HIP GEMM, clips=1).  Since round 6
+    the mixer runs in_proj with the conv + x_proj partials in its epilogue at this batch
+    (``in_proj_conv``: vm_in_proj_conv_proj_fwd, its two launches), and ``layer_us_sum``
+    adds the stages the mixer runs; in_proj / conv_proj stay listed for comparison.  Every
+    stage but the scan is timed from a captured HIP graph (_graph_us: the chunk graph's own
+    per-kernel cost; the eager host-issued timing of rounds 1-5 is ``us_eager``)."""
     from videomamba_amd import kernels as K
     from videomamba_amd.layers import round_up
     from videomamba_amd.mamba_simple import Mamba, _linear
@@ -322,28 +357,45 @@ def b1_kernel_rooflines(device, reps=50):
                      "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4)}
 
+    def stage(name, fn, kind, amount):
+        (hbm if kind == "hbm" else mfma)(name, _graph_us(fn, reps), amount)
+        out[name]["us_eager"] = round(_event_us(fn, reps), 2)
+
     with torch.no_grad():
-        hbm("add_norm", _event_us(lambda: K.add_norm_raw(x, res, w32, None, hn, res, Lp, C, 1e-5,
-                                                         True, stream), reps), 12 * Lp * C)
+        stage("add_norm", lambda: K.add_norm_raw(x, res, w32, None, hn, res, Lp, C, 1e-5, True,
+                                                 torch.cuda.current_stream().cuda_stream),
+              "hbm", 12 * Lp * C)
         hn.normal_()
-        mfma("in_proj", _event_us(lambda: _linear(hn, mx.in_proj.weight, clips=1), reps),
-             2 * Lp * C * 2 * Dm)
+        stage("in_proj", lambda: _linear(hn, mx.in_proj.weight, clips=1), "mfma",
+              2 * Lp * C * 2 * Dm)
         # the mixer's choice at this shape: dt_proj inside the segmented scan (no dt rows)
         dtp = mx._dtp_ok(hn.view(1, Lp, C), L)
         wd, dto = (None, None) if dtp else (wdt_pad, dt)
-        hbm("conv_proj", _event_us(lambda: K.conv_proj_raw(
+        stage("conv_proj", lambda: K.conv_proj_raw(
             xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs_in, (cs_in.stride(0), cs_in.stride(1)),
             cs_out, (cs_out.stride(0), cs_out.stride(1)), wx_pad, E, wd, R, u,
-            (Lp * Dm, Dm), xdbl, (Lp * E, E), dto, (Lp * Dm, Dm), Lp, 1, Dm, L, W, stream), reps),
+            (Lp * Dm, Dm), xdbl, (Lp * E, E), dto, (Lp * Dm, Dm), Lp, 1, Dm, L, W,
+            torch.cuda.current_stream().cuda_stream), "hbm",
             2 * Lp * ((2 if dtp else 3) * Dm + E) + 2 * wx_pad.numel()
             + (0 if dtp else 2 * wdt_pad.numel()))
+        fused = mx._in_proj_conv_ok(hn.view(1, Lp, C), L, not dtp)
+        if fused:  # what the mixer runs at this batch instead of the two stages above
+            stage("in_proj_conv", lambda: K.in_proj_conv_proj_raw(
+                hn, mx.in_proj.weight, xz[:, Dm:], cw, cb, cs_in,
+                (cs_in.stride(0), cs_in.stride(1)), cs_out, (cs_out.stride(0), cs_out.stride(1)),
+                wx_pad, E, wdt_pad, R, u, xdbl, dto, Lp, 1, Dm, L, W,
+                torch.cuda.current_stream().cuda_stream), "mfma",
+                2 * Lp * C * 2 * Dm + 2 * Lp * Dm * E)
         sc = scan_roofline(1, reps, device, "tm", dtp=dtp)
         out["scan"] = {k: sc[k] for k in ("avg_us", "bound", "achieved", "peak", "unit", "frac")}
         out["scan"]["us"] = out["scan"].pop("avg_us")
         out["scan"]["dt_proj_inside"] = bool(dtp)
-        mfma("out_proj", _event_us(lambda: _linear(y, mx.out_proj.weight, clips=1), reps),
-             2 * Lp * Dm * C)
-    out["layer_us_sum"] = round(sum(v["us"] for v in out.values()), 2)
+        stage("out_proj", lambda: _linear(y, mx.out_proj.weight, clips=1), "mfma",
+              2 * Lp * Dm * C)
+    run = ["add_norm"] + (["in_proj_conv"] if fused else ["in_proj", "conv_proj"]) + ["scan",
+                                                                                      "out_proj"]
+    out["layer_us_sum"] = round(sum(out[k]["us"] for k in run), 2)
+    out["layer_stages"] = run
     out["shape"] = f"VideoMamba-M layer, B=1, L={L} (padded {Lp}), bf16, stages launched alone"
     return out
 

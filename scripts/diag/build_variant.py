@@ -373,6 +373,36 @@ VARIANTS = {
                   "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n")],
     "cp_prio3": [("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
                   "void conv_proj_kernel(const ConvProjParams p) {\n  __builtin_amdgcn_s_setprio(3);\n")],
+    # in_proj + conv epilogue pricing (results wrong): x tiles stop after the LDS tile
+    # (ic_noepi), skip the conv + u stores (ic_noconv), skip the x_proj MFMA + partial
+    # stores (ic_nopart)
+    "ic_noepi": [("vm_inproj_conv.hip", "  if (!xt) {  // ---- z tile", "  if (xt) return;\n  if (!xt) {  // ---- z tile")],
+    "ic_noconv": [("vm_inproj_conv.hip", "  uint32_t upk[kRows];\n#pragma unroll\n  for (int i = 0; i < kRows; ++i) {\n    float al",
+                   "  uint32_t upk[kRows];\n#pragma unroll\n  for (int i = 0; i < kRows && tok_lo < -100; ++i) {\n    float al"),
+                  ("vm_inproj_conv.hip", "    if (st < 3) {  // uniform", "    upk[i] = xw[i];\n    if (st < 3 && tok_lo < -100) {  // uniform"),
+                  ("vm_inproj_conv.hip", "    if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u", "    if (tok < -5) *reinterpret_cast<uint32_t*>(p.u")],
+    "ic_nopart": [("vm_inproj_conv.hip", "  const bool mw = wave < kIcOut / 16;", "  if (tok_lo >= 0) return;\n  const bool mw = wave < kIcOut / 16;")],
+    # ... no u global stores (ic_nou), no partial global stores (ic_nops), z tiles skipped
+    # (ic_noz), no conv-state / new-conv-state work (ic_nocs)
+    "ic_nou": [("vm_inproj_conv.hip", "    if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u", "    if (tok < -5) *reinterpret_cast<uint32_t*>(p.u")],
+    "ic_nops": [("vm_inproj_conv.hip", "      if (tok < q.ntok)\n        *reinterpret_cast<float4*>(q.part", "      if (tok < -5)\n        *reinterpret_cast<float4*>(q.part")],
+    "ic_noz": [("vm_inproj_conv.hip", "  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;", "  if (!xt) return;\n  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;")],
+    # in_proj + conv epilogue phase stamps (scripts/diag/inproj_conv_stamps.py): wave 0 of every
+    # workgroup records s_memrealtime at 8 points into g_ic_stamps[workgroup][8]
+    "ic_stamp": [
+        ("vm_inproj_conv.hip", "template <int NK, int NB>\n__global__ __launch_bounds__(512) void inproj_conv_kernel(",
+         "__device__ unsigned long long g_ic_stamps[4096 * 8];\n#define IC_ST(P) do { if (tid == 0 && blockIdx.x < 4096) g_ic_stamps[blockIdx.x * 8 + (P)] = __builtin_amdgcn_s_memrealtime(); } while (0)\n"
+         "template <int NK, int NB>\n__global__ __launch_bounds__(512) void inproj_conv_kernel("),
+        ("vm_inproj_conv.hip", "  const int wm = wave >> 1, wn = wave & 1;\n", "  const int wm = wave >> 1, wn = wave & 1;\n  IC_ST(0);\n"),
+        ("vm_inproj_conv.hip", "  __syncthreads();  // every wave is past its last fragment reads\n", "  __syncthreads();  // every wave is past its last fragment reads\n  IC_ST(1);\n"),
+        ("vm_inproj_conv.hip", "  // ---- x tile epilogue ----\n", "  // ---- x tile epilogue ----\n  IC_ST(2);\n"),
+        ("vm_inproj_conv.hip", "  // conv + SiLU: channels c, c + 1 (one packed word)", "  IC_ST(3);\n  // conv + SiLU: channels c, c + 1 (one packed word)"),
+        ("vm_inproj_conv.hip", "  __syncthreads();  // every wave is past its reads of the x tile: u takes its rows\n", "  IC_ST(4);\n  __syncthreads();  // every wave is past its reads of the x tile: u takes its rows\n"),
+        ("vm_inproj_conv.hip", "  __syncthreads();  // the u / W_x tiles are free", "  IC_ST(5);\n  __syncthreads();  // the u / W_x tiles are free"),
+        ("vm_inproj_conv.hip", "  __builtin_amdgcn_wave_barrier();\n  if (mw) {\n    const int nq", "  IC_ST(6);\n  __builtin_amdgcn_wave_barrier();\n  if (mw) {\n    const int nq"),
+        ("vm_inproj_conv.hip", "}  // namespace vm\n\nusing namespace vm;\n",
+         "}  // namespace vm\n\nusing namespace vm;\nextern \"C\" int vm_ic_stamps(unsigned long long* host) {\n"
+         "  return hipMemcpyFromSymbol(host, HIP_SYMBOL(vm::g_ic_stamps), sizeof(vm::g_ic_stamps)) == hipSuccess ? 0 : -1;\n}\n")],
     "ancp_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
                     "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n"),
                    ("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
@@ -409,7 +439,8 @@ def build(name, rev=None):
         s = open(p).read()
         assert s.count(old) >= 1, (name, fname, old)
         open(p, "w").write(s.replace(old, new))
-    out = os.path.join(ROOT, "tools", "probes", "var", name)
+    # VARIANT_DIR=ab puts the build where gpurun pushes it (tools/probes/var is not pushed)
+    out = os.path.join(ROOT, "tools", "probes", os.environ.get("VARIANT_DIR", "var"), name)
     os.makedirs(out, exist_ok=True)
     subprocess.check_call(["make", "-C", work, "-j8", f"OUT={out}/libvideomamba_hip.so",
                            f"BUILD={os.path.join(ROOT, 'build', 'var', name, 'obj')}"])

@@ -57,6 +57,15 @@ constexpr int kIcLds = (2 * kIcStage > kIcOBytes + kIcWBytes + kIcCBytes)
 
 __device__ __forceinline__ int ic_slot(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// Workgroup barrier over LDS traffic only: __syncthreads() also waits vmcnt(0), which would
+// make every barrier of the epilogue wait for the u / partial stores issued before it.
+__device__ __forceinline__ void ic_lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt at their maximum
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 template <int NK, int NB>
 __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) {
   constexpr int R = kIcRow;
@@ -70,13 +79,16 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-contiguous renumbering (linear_dma_kernel's): a row tile's splits share one L2
-  const int nwg = gridDim.x, h = blockIdx.x;
-  const int xcd = h & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int l = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);
+  // The x tiles come first in dispatch order, so the hardware spreads them one per CU
+  // before any CU takes a second workgroup (x and z tiles then pair up on a CU instead of
+  // whole XCDs holding only x tiles); within each part an XCD-contiguous renumbering
+  // (linear_dma_kernel's) lets a row tile's splits share one L2.
   const int nx = q.nxr * q.nsplit;
-  const bool xt = l < nx;  // uniform
-  const int lt = xt ? l : l - nx;
+  const bool xt = static_cast<int>(blockIdx.x) < nx;  // uniform
+  const int h = xt ? blockIdx.x : blockIdx.x - nx;
+  const int nwg = xt ? nx : gridDim.x - nx;
+  const int xcd = h & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int lt = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);
   const int rt = lt / q.nsplit, sp = lt - rt * q.nsplit;
   // A rows: x tiles rt * 112 - 16 .. + 127 (rows < 0 read as zero), z tiles rt * 128 ..
   const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;
@@ -149,26 +161,47 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
   constexpr int kCI = (kIcCsSeq * 3 * 128 + NT - 1) / NT;  // conv-state taps per thread
   uint4 wv[kWI];
   float cv[kCI];
+  float wl[4], wh[4], bl = 0.0f, bh = 0.0f;  // conv taps right-aligned to 4 (conv_xproj_tm_kernel)
   const int b_lo = tok_lo / p.out_len;
   const int nbs = (xt && p.csi)
                       ? min(p.batch - 1, (tok_lo + kIcOut - 1) / p.out_len) - b_lo + 1 : 0;
+  // every epilogue operand as a branch-free buffer load (absent / padding pieces read 0
+  // through out-of-range offsets): a divergent "load or zero" makes hipcc wait vmcnt(0) at
+  // its join, which would also drain the last K step's stage
   auto epi_loads = [&]() {
+    const auto cwr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.cw), 0, p.dim * W * 4, 0x00020000);
+    const auto cbr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.cb), 0, p.cb ? p.dim * 4 : 0, 0x00020000);
+    const auto wxr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.wx), 0, p.e_pad * p.dim * 2, 0x00020000);
+    constexpr int kOut = static_cast<int>(0x80000000u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int kk = k - (4 - W);  // taps right-aligned: leading taps of a short filter are 0
+      wl[k] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(cwr, kk >= 0 ? (c * W + kk) * 4 : kOut, 0, 0));
+      wh[k] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(cwr, kk >= 0 ? ((c + 1) * W + kk) * 4 : kOut, 0, 0));
+    }
+    bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cbr, c * 4, 0, 0));
+    bh = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(cbr, (c + 1) * 4, 0, 0));
 #pragma unroll
     for (int k = 0; k < kWI; ++k) {
       const int i = tid + k * NT;
       const int e = i >> 4, qd = i & 15;
-      wv[k] = make_uint4(0, 0, 0, 0);
-      if (i < NB * 16 * 16) wv[k] = *reinterpret_cast<const uint4*>(p.wx + (long long)e * p.dim + c0 + qd * 8);
+      const int off = i < NB * 16 * 16 ? (e * p.dim + c0 + qd * 8) * 2 : kOut;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wxr, off, 0, 0);
+      wv[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
+    if (nbs > 0) {  // uniform: only tiles holding a sequence start read the old conv state
 #pragma unroll
-    for (int k = 0; k < kCI; ++k) {
-      const int i = tid + k * NT;
-      const int bb = i / (3 * 128), m = (i / 128) % 3, ch = i % 128;
-      const int tap = W - 1 - m;  // state column of step -(m + 1)
-      cv[k] = 0.0f;
-      if (bb < nbs && tap >= 0)
-        cv[k] = load_dyn(p.csi, (b_lo + bb) * p.csi_sb + (long long)(c0 + ch) * p.csi_sd + tap,
-                         p.csi_dtype);
+      for (int k = 0; k < kCI; ++k) {
+        const int i = tid + k * NT;
+        const int bb = i / (3 * 128), m = (i / 128) % 3, ch = i % 128;
+        const int tap = W - 1 - m;  // state column of step -(m + 1)
+        cv[k] = 0.0f;
+        if (bb < nbs && tap >= 0)
+          cv[k] = load_dyn(p.csi, (b_lo + bb) * p.csi_sb + (long long)(c0 + ch) * p.csi_sd + tap,
+                           p.csi_dtype);
+      }
     }
   };
 
@@ -176,13 +209,11 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);  // stage kt (and, at the last step, the epilogue operands)
+    __builtin_amdgcn_s_waitcnt(0);  // stage kt has landed
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (kt + 1 < NK) issue(kt + 1, (kt + 1) & 1);
-    if (kt + 2 == NK || (NK == 1 && kt == 0)) {
-      if (xt) epi_loads();
-    }
+    if (kt + 1 == NK && xt) epi_loads();  // in flight during the last K step's MFMAs
     compute(kt & 1);
   }
   __builtin_amdgcn_s_waitcnt(0);
@@ -204,7 +235,7 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
       }
     }
   if (!xt) {  // ---- z tile: 16-byte row stores (z column = n0 - dim) ----
-    __syncthreads();
+    ic_lds_barrier();
     for (int pc = tid; pc < 128 * 16; pc += NT) {
       const int row = pc >> 4, cq = pc & 15;
       const int gm = m0 + row;
@@ -215,7 +246,8 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
     return;
   }
 
-  // ---- x tile epilogue ----
+  // ---- x tile epilogue (every barrier LDS-only: the u / partial / conv-state stores stay in
+  // flight until the kernel ends) ----
   bf16_t* sW = reinterpret_cast<bf16_t*>(dsm + kIcOBytes);                  // [e][kIcPitch]
   float* sC = reinterpret_cast<float*>(dsm + kIcOBytes + kIcWBytes);        // [seq][3][128]
 #pragma unroll
@@ -228,14 +260,7 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
     const int i = tid + k * NT;
     if (i / (3 * 128) < nbs) sC[i] = cv[k];
   }
-  float wl[4], wh[4];  // taps right-aligned to 4 (conv_xproj_tm_kernel)
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    wl[k] = k >= 4 - W ? p.cw[c * W + k - (4 - W)] : 0.0f;
-    wh[k] = k >= 4 - W ? p.cw[(c + 1) * W + k - (4 - W)] : 0.0f;
-  }
-  const float bl = p.cb ? p.cb[c] : 0.0f, bh = p.cb ? p.cb[c + 1] : 0.0f;
-  __syncthreads();
+  ic_lds_barrier();
 
   // new conv state: the last `width` raw inputs of every sequence whose last step lies in
   // this tile's output rows (its W - 1 <= 3 rows before are in the halo rows)
@@ -267,17 +292,14 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
   const int tw = m0 + r0;  // the wave's first token
   const int bw = tw / p.out_len;
   const int sw = tw - bw * p.out_len;
-  auto token_pos = [&](int i, int& b, int& st) {  // out_len >= 56: at most 1 wrap in 14
-    b = bw;
-    st = sw + i;
-    if (st >= p.out_len) { st -= p.out_len; ++b; }
-  };
   auto pack = [&](float al, float ah, bool live) -> uint32_t {
     const float ul = live ? al * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-al * kLog2e)) : 0.0f;
     const float uh = live ? ah * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-ah * kLog2e)) : 0.0f;
     return static_cast<uint32_t>(from_f32<bf16_t>(ul)) |
            (static_cast<uint32_t>(from_f32<bf16_t>(uh)) << 16);
   };
+  // every row from the tile (branch-free); the rows in the first 3 steps of a sequence are
+  // redone below.  (out_len >= 56 > 14: a wave's rows span at most one sequence boundary)
   uint32_t upk[kRows];
 #pragma unroll
   for (int i = 0; i < kRows; ++i) {
@@ -287,35 +309,47 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
       al = fmaf(wl[k], __uint_as_float(xw[i + k] << 16), al);
       ah = fmaf(wh[k], __uint_as_float(xw[i + k] & 0xffff0000u), ah);
     }
-    int b, st;
-    token_pos(i, b, st);
+    const int st = sw + i >= p.out_len ? sw + i - p.out_len : sw + i;
     upk[i] = pack(al, ah, st < p.seqlen && tw + i < q.ntok);
   }
+  // rows with step < 3: i0 + r (r = step 0, 1, 2) — the taps before the sequence are the
+  // old conv state (staged in sC) or zeros, as conv_xproj_tm_kernel's redo
+  const int i0 = sw < 3 ? -sw : p.out_len - sw;
+  if (i0 < kRows) {  // uniform
+    const int bs = sw < 3 ? bw : bw + 1;  // the sequence whose steps 0 .. 2 these rows are
+    uint32_t red[3];
 #pragma unroll
-  for (int i = 0; i < kRows; ++i) {
-    int b, st;
-    token_pos(i, b, st);
-    if (st < 3) {  // uniform: a sequence starts at or just before this token
-      float al = bl, ah = bh;
+    for (int r = 0; r < 3; ++r) {
+      const int i = i0 + r;
+      red[r] = 0;
+      if (i >= 0 && i < kRows) {  // uniform
+        float al = bl, ah = bh;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = st - 3 + k;  // input step in the virtual sequence
-        float vl = __uint_as_float(xw[i + k] << 16), vh = __uint_as_float(xw[i + k] & 0xffff0000u);
-        if (j < 0) {
-          vl = vh = 0.0f;
-          if (p.csi && tw + i < q.ntok && k >= 4 - W) {
-            const float2 cs = *reinterpret_cast<const float2*>(&sC[((b - b_lo) * 3 - j - 1) * 128 + 2 * lane]);
+        for (int k = 0; k < 4; ++k) {
+          const int j = r - 3 + k;  // input step in the virtual sequence
+          float vl = 0.0f, vh = 0.0f;
+          if (j >= 0) {
+            const uint32_t xv = *reinterpret_cast<const uint32_t*>(&sO[(r0 + i - 3 + k) * kIcPitch + 2 * lane]);
+            vl = __uint_as_float(xv << 16);
+            vh = __uint_as_float(xv & 0xffff0000u);
+          } else if (p.csi && tw + i < q.ntok && k >= 4 - W) {
+            const float2 cs = *reinterpret_cast<const float2*>(&sC[((bs - b_lo) * 3 - j - 1) * 128 + 2 * lane]);
             vl = cs.x;
             vh = cs.y;
           }
+          al = fmaf(wl[k], vl, al);
+          ah = fmaf(wh[k], vh, ah);
         }
-        al = fmaf(wl[k], vl, al);
-        ah = fmaf(wh[k], vh, ah);
+        red[r] = pack(al, ah, r < p.seqlen && tw + i < q.ntok);
       }
-      upk[i] = pack(al, ah, st < p.seqlen && tw + i < q.ntok);
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = i - i0;
+      upk[i] = r == 0 ? red[0] : r == 1 ? red[1] : r == 2 ? red[2] : upk[i];
     }
   }
-  __syncthreads();  // every wave is past its reads of the x tile: u takes its rows
+  ic_lds_barrier();  // every wave is past its reads of the x tile: u takes its rows
   bf16_t* sU = sO;  // [112][kIcPitch]: output row i at row i
 #pragma unroll
   for (int i = 0; i < kRows; ++i) {
@@ -323,7 +357,7 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
     const int tok = tw + i;
     if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c) = upk[i];
   }
-  __syncthreads();
+  ic_lds_barrier();
 
   // x_proj partial (conv_xproj_tm_kernel's MFMA layout): waves 0..6, tokens 16 w .. 16 w + 15
   // x all e_pad columns, K = the split's 128 channels in four 32-deep steps
@@ -346,7 +380,7 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
       }
     }
   }
-  __syncthreads();  // the u / W_x tiles are free: stage the partial rows there
+  ic_lds_barrier();  // the u / W_x tiles are free: stage the partial rows there
   constexpr int kPP = kSkMaxEp;
   float* sP = reinterpret_cast<float*>(dsm) + wave * 16 * kPP;
   if (mw) {
@@ -369,6 +403,34 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
             *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd]);
     }
   }
+}
+
+// x_dbl = bf16(sum of the split partials in split order) — xdbl_dt_tm_kernel's sum (from
+// 0, split 0 first, fp32) without its dt phase, one thread per (token, 4 columns) so the
+// whole reduction is one round of loads (that kernel's 64-token tiles take two dependent
+// rounds on a 50-workgroup grid at B = 1).  dt == NULL only (the scan computes dt).
+template <int NSPL>
+__global__ __launch_bounds__(256) void xdbl_reduce_kernel(const InConvParams q) {
+  const ConvProjTmArgs& p = q.a;
+  const int q4 = (p.e + 3) >> 2;
+  const int it = blockIdx.x * 256 + threadIdx.x;
+  if (it >= q.ntok * q4) return;
+  const int t = it / q4, e0 = (it - t * q4) * 4;
+  const long long sstride = (long long)q.ntok * q.ep;
+  const float* src = q.part + (long long)t * q.ep + e0;
+  float4 part[NSPL];
+#pragma unroll
+  for (int sp = 0; sp < NSPL; ++sp) part[sp] = *reinterpret_cast<const float4*>(src + sp * sstride);
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int sp = 0; sp < NSPL; ++sp) {
+    sum.x += part[sp].x; sum.y += part[sp].y; sum.z += part[sp].z; sum.w += part[sp].w;
+  }
+  const float sv[4] = {sum.x, sum.y, sum.z, sum.w};
+  bf16_t* dst = p.xdbl + (long long)t * p.xd_tl + e0;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    if (e0 + kk < p.e) dst[kk] = from_f32<bf16_t>(sv[kk]);
 }
 
 bool inproj_conv_ok(int k, const ConvProjTmArgs& a) {
@@ -480,6 +542,17 @@ extern "C" int vm_in_proj_conv_proj_fwd(
   q.nzr = static_cast<int>((ntok + 127) / 128);
   hipStream_t s = static_cast<hipStream_t>(stream);
   inproj_conv_launch(q, s);
-  conv_proj_sk_reduce_launch(a, q.part, s);
+  if (dt) {
+    conv_proj_sk_reduce_launch(a, q.part, s);
+  } else {
+    const unsigned blocks = static_cast<unsigned>((ntok * ((e + 3) / 4) + 255) / 256);
+    switch (q.nsplit) {
+#define VM_XR(NS) case NS: hipLaunchKernelGGL(xdbl_reduce_kernel<NS>, dim3(blocks), dim3(256), 0, s, q); break;
+      VM_XR(1) VM_XR(2) VM_XR(3) VM_XR(4) VM_XR(5) VM_XR(6) VM_XR(7) VM_XR(8)
+      VM_XR(9) VM_XR(10) VM_XR(11) VM_XR(12) VM_XR(13) VM_XR(14) VM_XR(15) VM_XR(16)
+#undef VM_XR
+      default: break;
+    }
+  }
   return vmhost::launch_status("vm_in_proj_conv_proj_fwd");
 }
