@@ -403,6 +403,10 @@ VARIANTS = {
         ("vm_inproj_conv.hip", "}  // namespace vm\n\nusing namespace vm;\n",
          "}  // namespace vm\n\nusing namespace vm;\nextern \"C\" int vm_ic_stamps(unsigned long long* host) {\n"
          "  return hipMemcpyFromSymbol(host, HIP_SYMBOL(vm::g_ic_stamps), sizeof(vm::g_ic_stamps)) == hipSuccess ? 0 : -1;\n}\n")],
+    # ... x tiles at raised wave priority (ic_prio), no XCD renumbering in either part (ic_norenum)
+    "ic_prio": [("vm_inproj_conv.hip", "  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;", "  if (xt) __builtin_amdgcn_s_setprio(2);\n  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;")],
+    "ic_norenum": [("vm_inproj_conv.hip", "  const int lt = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);",
+                    "  const int lt = h + 0 * (xcd + qq + rr + nwg);")],
     "ancp_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
                     "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n"),
                    ("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
