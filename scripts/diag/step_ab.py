@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 LIB = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--lib=")]
 if LIB:  # a probe variant (scripts/diag/build_variant.py)
     import videomamba_amd._lib as L
-    L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", LIB[0], "libvideomamba_hip.so")
+    L.LIB_PATH = os.path.join(ROOT, "tools", "probes", os.environ.get("VARIANT_DIR", "var"), LIB[0],
+                              "libvideomamba_hip.so")
 import torch  # noqa: E402
 from videomamba_amd import options  # noqa: E402
 from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
