@@ -407,11 +407,9 @@ VARIANTS = {
     "ic_prio": [("vm_inproj_conv.hip", "  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;", "  if (xt) __builtin_amdgcn_s_setprio(2);\n  const int m0 = xt ? rt * kIcOut - kIcHalo : rt * 128;")],
     "ic_norenum": [("vm_inproj_conv.hip", "  const int lt = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);",
                     "  const int lt = h + 0 * (xcd + qq + rr + nwg);")],
-    # add + RMSNorm with one row per wave at every row count (the round-5 form; the product
-    # takes kAnRowsPerWave rows per wave from kAnMultiRows rows up)
-    "an_rpw1": [("vm_norm.hip", "constexpr long long kAnMultiRows = 1ll << 20;", "constexpr long long kAnMultiRows = 1ll << 62;")],
-    "an_rpw4": [("vm_norm.hip", "constexpr int kAnRowsPerWave = 8;", "constexpr int kAnRowsPerWave = 4;")],
-    "an_rpw16": [("vm_norm.hip", "constexpr int kAnRowsPerWave = 8;", "constexpr int kAnRowsPerWave = 16;")],
+    # add + RMSNorm with 8 / 4 / 16 rows per wave at >= 2^20 rows (round 6, measured no gain
+    # in the 1344-clip step, profiles/r06k_add_norm_rows_per_wave_step_ab.jsonl): build from
+    # commit 5c0d0d1 with --rev
     "ancp_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
                     "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n"),
                    ("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",

@@ -1274,26 +1274,3 @@ def test_in_proj_conv_proj_rejects_unsupported_shapes():
     assert not K.in_proj_conv_proj_fits(576, 1, 3144, 1088, 68, 80, 64, 4, False)
     assert not K.in_proj_conv_proj_fits(640, 1, 3144, 1152, 68, 80, 64, 4, False)
 
-
-def test_add_rms_rows_per_wave_is_bitwise_one_row_per_wave():
-    """vm_add_norm_fwd at chip-filling row counts (>= 2^20 rows: the bench's 672-clip
-    sub-batch has 2.1 M) runs add_rms_bf16_kernel with 8 rows per wave, the next row's loads
-    in flight while a row is reduced; every row is the same arithmetic as the one-row-per-wave
-    form, which row slices below 2^20 take: the head, a middle run and the ragged tail of a
-    1,048,579-row call (not a multiple of 32 rows) are bit-equal to the same rows normalised
-    in small calls (reference videomamba.py:141-166, the fused add + RMSNorm)."""
-    torch.manual_seed(7)
-    rows, C = (1 << 20) + 3, 576
-    x = torch.randn(rows, C, device=DEV).to(torch.bfloat16)
-    res = torch.randn(rows, C, device=DEV)
-    w = torch.randn(C, device=DEV)
-    st = torch.cuda.current_stream().cuda_stream
-    hn = torch.empty(rows, C, device=DEV, dtype=torch.bfloat16)
-    ro = torch.empty(rows, C, device=DEV)
-    K.add_norm_raw(x, res, w, None, hn, ro, rows, C, 1e-5, True, st)
-    for a, b in ((0, 1000), (524_287, 524_400), (rows - 37, rows)):
-        n = b - a
-        hs = torch.empty(n, C, device=DEV, dtype=torch.bfloat16)
-        rs = torch.empty(n, C, device=DEV)
-        K.add_norm_raw(x[a:b], res[a:b], w, None, hs, rs, n, C, 1e-5, True, st)
-        assert torch.equal(hs, hn[a:b]) and torch.equal(rs, ro[a:b]), (a, b)

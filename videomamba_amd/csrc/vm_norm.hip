@@ -50,10 +50,6 @@ __device__ __forceinline__ void store4_dyn(void* p, long long i, int dtype, cons
 // round trips per row that set the B = 1 chunk's add+norm at ~7 us.  Same arithmetic in
 // the same order as add_norm_vec_kernel (bit-identical outputs).
 constexpr int kNormOut = 0x7ffffff0;
-// add_rms_bf16_kernel's rows per wave from this many rows up (the bench batch: 2.1 M rows
-// per sub-batch launch; B = 1 chunks keep one row per wave)
-constexpr long long kAnMultiRows = 1ll << 20;
-constexpr int kAnRowsPerWave = 8;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base, int bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
@@ -64,91 +60,71 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base
 // (no early exit for the rows past the end: their buffers have 0-byte ranges, so every
 // access is a no-op, and the kernel-argument loads are not split by a branch into two
 // dependent rounds before the first global load)
-template <int CPL, bool RES, bool RO, int RPW = 1>  // RPW: rows per wave, one after another
+template <int CPL, bool RES, bool RO>
 __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
-  // wave w of workgroup g normalises rows (4 g + w) RPW .. + RPW - 1; with RPW > 1 the next
-  // row's loads are issued before the current row's reduction, so a wave keeps a row in
-  // flight while it computes (a workgroup lives RPW rows: at the bench batch one wave per
-  // row meant ~500 k short-lived workgroups, which get few dispatch slots beside the
-  // issue-bound scan of the other sub-batch stream)
-  const long long wrow0 =
-      ((long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * RPW;
+  const long long row0 = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool live = row0 < p.rows;
+  const long long row = live ? row0 : 0;
   const int lane = threadIdx.x & 63;
+  const long long base = row * p.cols;
+  const int cb2 = live ? p.cols * 2 : 0, cb4 = live ? p.cols * 4 : 0;
+  const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, cb2);
+  const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, cb4);
   const auto wr = norm_row_rsrc(p.w, p.cols * 4);
+  const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, cb2);
+  const auto ror = norm_row_rsrc(RO ? static_cast<float*>(p.res_out) + base : p.w, cb4);
   typedef __attribute__((__vector_size__(4 * sizeof(float)))) float v4f;
   auto off = [&](int j, int es) {
     int o = lane * 4 + 256 * j < p.cols ? (lane * 4 + 256 * j) * es : kNormOut;
     asm volatile("" : "+v"(o));  // a select, not a branch around the access
     return o;
   };
-  uint32_t xq[2][CPL][2];
-  v4f rq[2][CPL], wq[CPL];
-  auto load_row = [&](int k, long long row0) {  // row0's x / residual into slot k
-    const bool live = row0 < p.rows;
-    const long long base = (live ? row0 : 0) * p.cols;
-    const int cb2 = live ? p.cols * 2 : 0, cb4 = live ? p.cols * 4 : 0;
-    const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, cb2);
-    const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, cb4);
+  uint32_t xq[CPL][2];
+  v4f rq[CPL], wq[CPL];
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
-      xq[k][j][0] = q[0];
-      xq[k][j][1] = q[1];
-      if constexpr (RES) rq[k][j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));
-    }
-  };
-  load_row(0, wrow0);
+  for (int j = 0; j < CPL; ++j) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
+    xq[j][0] = q[0];
+    xq[j][1] = q[1];
+    if constexpr (RES) rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));
+  }
 #pragma unroll
   for (int j = 0; j < CPL; ++j)
     wq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(wr, off(j, 4), 0, 0));
   __builtin_amdgcn_sched_barrier(0);  // all of the row's loads in flight before any use
+  float v[CPL][4];
 #pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int k = r & 1;
-    if (r + 1 < RPW) {
-      load_row(k ^ 1, wrow0 + r + 1);
-      __builtin_amdgcn_sched_barrier(0);  // the next row's loads before this row's reduce
+  for (int j = 0; j < CPL; ++j) {
+    v[j][0] = __uint_as_float(xq[j][0] << 16); v[j][1] = __uint_as_float(xq[j][0] & 0xffff0000u);
+    v[j][2] = __uint_as_float(xq[j][1] << 16); v[j][3] = __uint_as_float(xq[j][1] & 0xffff0000u);
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[j][i] += rq[j][i];
     }
-    const long long row0 = wrow0 + r;
-    const bool live = row0 < p.rows;
-    const long long base = (live ? row0 : 0) * p.cols;
-    const int cb2 = live ? p.cols * 2 : 0, cb4 = live ? p.cols * 4 : 0;
-    const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, cb2);
-    const auto ror = norm_row_rsrc(RO ? static_cast<float*>(p.res_out) + base : p.w, cb4);
-    float v[CPL][4];
+  }
+  float sq = 0.0f;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      v[j][0] = __uint_as_float(xq[k][j][0] << 16); v[j][1] = __uint_as_float(xq[k][j][0] & 0xffff0000u);
-      v[j][2] = __uint_as_float(xq[k][j][1] << 16); v[j][3] = __uint_as_float(xq[k][j][1] & 0xffff0000u);
-      if constexpr (RES) {
+  for (int j = 0; j < CPL; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[j][i] += rq[k][j][i];
-      }
-    }
-    float sq = 0.0f;
+    for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
+  const float rstd = rsqrtf(wave_sum(sq) / p.cols + p.eps);
+  const float mean = 0.0f;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j)
+  for (int j = 0; j < CPL; ++j) {
+    float y[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sq = fmaf(v[j][i], v[j][i], sq);
-    const float rstd = rsqrtf(wave_sum(sq) / p.cols + p.eps);
-    const float mean = 0.0f;
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      float y[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) y[i] = (v[j][i] - mean) * rstd * wq[j][i];
-      typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
-      const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
-                                       (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
-                      static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
-                                       (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
-      __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);
-      if constexpr (RO) {
-        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
-        const v4i r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
-                        static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
-        __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);
-      }
+    for (int i = 0; i < 4; ++i) y[i] = (v[j][i] - mean) * rstd * wq[j][i];
+    typedef __attribute__((__vector_size__(2 * sizeof(int)))) int v2i;
+    const v2i o2 = {static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[0])) |
+                                     (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
+                    static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
+                                     (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
+    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);
+    if constexpr (RO) {
+      typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+      const v4i r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
+                      static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
+      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);
     }
   }
 }
@@ -773,26 +749,20 @@ extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual,
       (!residual || res_dtype == VM_DTYPE_F32) && (!residual_out || res_out_dtype == VM_DTYPE_F32) &&
       cols <= 256 * 4) {
     const int cpl = (cols + 255) / 256;
-    // at chip-filling row counts a wave takes kAnRowsPerWave rows (same per-row arithmetic)
-    const bool multi = rows >= kAnMultiRows;
-    const dim3 gm(static_cast<unsigned>((rows + 4 * kAnRowsPerWave - 1) / (4 * kAnRowsPerWave)));
-#define VM_RMS_BF16_RPW(CPLV, R1, R2, RPWV, G)                                                    \
-    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, R1, R2, RPWV>), G, dim3(256), 0, s, p);
-#define VM_RMS_BF16_RR(CPLV, R1, R2)                                                             \
-    if (multi) { VM_RMS_BF16_RPW(CPLV, R1, R2, kAnRowsPerWave, gm) }                            \
-    else { VM_RMS_BF16_RPW(CPLV, R1, R2, 1, grid) }
 #define VM_RMS_BF16(CPLV)                                                                   \
-  if (residual && residual_out) { VM_RMS_BF16_RR(CPLV, true, true) }                        \
-  else if (residual) { VM_RMS_BF16_RR(CPLV, true, false) }                                  \
-  else if (residual_out) { VM_RMS_BF16_RR(CPLV, false, true) }                              \
-  else { VM_RMS_BF16_RR(CPLV, false, false) }
+  if (residual && residual_out)                                                             \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, true>), grid, dim3(256), 0, s, p);   \
+  else if (residual)                                                                        \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, false>), grid, dim3(256), 0, s, p);  \
+  else if (residual_out)                                                                    \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, false, true>), grid, dim3(256), 0, s, p);  \
+  else                                                                                      \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, false, false>), grid, dim3(256), 0, s, p);
     if (cpl <= 1) { VM_RMS_BF16(1) }
     else if (cpl <= 2) { VM_RMS_BF16(2) }
     else if (cpl <= 3) { VM_RMS_BF16(3) }
     else { VM_RMS_BF16(4) }
 #undef VM_RMS_BF16
-#undef VM_RMS_BF16_RR
-#undef VM_RMS_BF16_RPW
     return vmhost::launch_status("vm_add_norm_fwd");
   }
   if (vec) {
