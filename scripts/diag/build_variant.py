@@ -408,8 +408,8 @@ VARIANTS = {
     "ic_norenum": [("vm_inproj_conv.hip", "  const int lt = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (h >> 3);",
                     "  const int lt = h + 0 * (xcd + qq + rr + nwg);")],
     # add + RMSNorm with 8 / 4 / 16 rows per wave at >= 2^20 rows (round 6, measured no gain
-    # in the 1344-clip step, profiles/r06k_add_norm_rows_per_wave_step_ab.jsonl): build from
-    # commit 5c0d0d1 with --rev
+    # in the 1344-clip step, profiles/r06k_add_norm_rows_per_wave_step_ab.jsonl): the product
+    # sources of commit bb2e338 (python build_variant.py --rev bb2e338 NAME)
     "ancp_prio3": [("vm_norm.hip", "void add_rms_bf16_kernel(const NormParams p) {\n",
                     "void add_rms_bf16_kernel(const NormParams p) {\n  __builtin_amdgcn_s_setprio(3);\n"),
                    ("vm_conv_proj.hip", "void conv_proj_kernel(const ConvProjParams p) {\n",
