@@ -43,9 +43,13 @@ def in_step(stats_csv, bench_json=None, batch=672, kname="scan_seq_dtp_kernel"):
         line = line.get("parsed", line)
         roof = line["roofline"]
         out["isolated_avg_us"], out["isolated_frac"] = roof["avg_us"], roof["frac"]
-        if roof.get("in_step"):
-            out["events_median_us"] = roof["in_step"]["median_us"]
-            out["events_frac"] = roof["in_step"]["frac"]
+        ins = roof.get("in_step") or {}
+        ev = ins.get("events", ins)  # round 6: {"trace": .., "events": ..}
+        if "median_us" in ev:
+            out["events_median_us"] = ev["median_us"]
+            out["events_frac"] = ev["frac"]
+        if ins.get("trace"):
+            out["line_trace_frac"], out["line_trace_source"] = ins["trace"]["frac"], ins["trace"]["source"]
     print(json.dumps(out, indent=1))
     return out
 

@@ -220,3 +220,28 @@ def test_gpu_encoder_batch_sharded_world2_matches_single_process(split):
             else:
                 torch.testing.assert_close(pooled, xp_all.float().cpu(), rtol=1e-5, atol=1e-5)
     assert torch.equal(out[0][3], out[1][3])  # every rank holds the same gathered batch
+
+
+def test_in_step_scan_fraction_reproduces_from_committed_trace():
+    """the scan's in-step HBM fraction (the kernel's own begin-end times in a
+    committed rocprofv3 trace of a bench command) is what bench.py reports as
+    roofline.in_step.trace, and scripts/traffic_summary.py in-step reproduces it from the
+    same file; the isolated figure (roofline.frac) is larger."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    algo = 672 * 1152 * 3137 * 4 * 2 + 2 * 672 * 16 * 3137 * 2 + 4 * 1152 * 16 + 8 * 1152 \
+        + 2 * 672 * 1152 * 16 * 2
+    tr = bench._trace_in_step(algo)
+    assert tr is not None and tr["source"] == bench.IN_STEP_TRACES[0]
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "traffic_summary.py"),
+                          "in-step", os.path.join(root, tr["source"]), "672"],
+                         capture_output=True, text=True, check=True).stdout
+    rec = json.loads(out)
+    assert rec["bytes_per_launch"] == algo
+    assert abs(rec["trace_frac"] - tr["frac"]) < 1e-4 and abs(rec["trace_avg_us"] - tr["avg_us"]) < 0.01
+    line = json.load(open(os.path.join(root, "profiles", "r06j_bench.json")))
+    assert line["roofline"]["frac"] > tr["frac"]
