@@ -1206,14 +1206,14 @@ def test_persistent_linear_is_repeatable_at_chip_filling_rows():
 
 
 @pytest.mark.parametrize("d_model", [192, 576])
-@pytest.mark.parametrize("bsz", [1, 2, 3])
+@pytest.mark.parametrize("bsz", [1, 2, 3, 8])
 def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
     """vm_in_proj_conv_proj_fwd (in_proj with the conv + SiLU and the x_proj split partials
     in its epilogue, vm_inproj_conv.hip) against the two steps it replaces: vm_linear_fwd
     (in_proj, mamba_simple.py:333-339) then vm_conv_proj_fwd (conv + x_proj + dt_proj,
     :381-416).  z, u, x_dbl, dt and the new conv state are bit-identical — for sequences
     shorter than a 112-row tile and longer than many, chunks padded past their length,
-    sequence starts mid-tile (bsz > 1), a carried conv state in bf16 / fp32 or none, dt rows
+    sequence starts mid-tile (bsz > 1; batch 8, the kernel's maximum), a carried conv state in bf16 / fp32 or none, dt rows
     or none (the scan computes them), and the M-16f chunk shape (3137 tokens)."""
     from videomamba_amd.mamba_simple import Mamba
     torch.manual_seed(d_model + bsz)

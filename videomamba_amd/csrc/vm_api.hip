@@ -2,6 +2,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <atomic>
+
 #include "vm_common.h"
 
 namespace {
@@ -23,6 +25,23 @@ int launch_status(const char* what) {
     return VM_E_LAUNCH;
   }
   return VM_OK;
+}
+
+int device_cus(hipStream_t stream) {
+  static std::atomic<int> cached[64];
+  int dev = 0;
+  if (stream) {
+    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return 0;
+  }
+  if (dev < 0 || dev >= 64) return 0;
+  int n = cached[dev].load(std::memory_order_relaxed);
+  if (!n) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 }  // namespace vmhost
 

@@ -108,4 +108,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline int dsize(int dtype) { return dtype == VM_DTYPE_BF16 ? 2 : 4; }
 inline bool dtype_ok(int dtype) { return dtype == VM_DTYPE_F32 || dtype == VM_DTYPE_BF16; }
 int launch_status(const char* what);
+// CU count of the device that owns `stream` (the current device for the null stream),
+// cached per device id; 0 when it cannot be queried
+int device_cus(hipStream_t stream);
 }  // namespace vmhost

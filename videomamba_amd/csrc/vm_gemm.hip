@@ -440,24 +440,7 @@ void gemm_tile_norm_launch(const bf16_t* x, long long ldx, const bf16_t* w, long
 // in_proj (12,544 rows, 441 tiles) 41.9 -> ~35 us, the C5 chunk 8.55 -> 8.26 ms
 constexpr int kTileMinPerCU2 = 3;
 
-// CUs of the device that owns `stream` (the current device for the null stream), cached per
-// device id; 0 when it cannot be queried
-static int device_cus(hipStream_t stream) {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (stream) {
-    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
-  } else if (hipGetDevice(&dev) != hipSuccess) {
-    return 0;
-  }
-  if (dev < 0 || dev >= 64) return 0;
-  if (!cus[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
+using vmhost::device_cus;
 
 }  // namespace vm
 

@@ -1585,24 +1585,9 @@ static void launch_seq(const ScanParams& p, const SeqWork& w, hipStream_t s) {
   }
 }
 
-// CU count of the device that owns `stream` (the current device for the null stream);
-// 0 when it cannot be queried (no device: the size queries then assume kCalibCUs).
-static int device_cus(hipStream_t stream) {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (stream) {
-    if (hipStreamGetDevice(stream, &dev) != hipSuccess) return 0;
-  } else if (hipGetDevice(&dev) != hipSuccess) {
-    return 0;
-  }
-  if (dev < 0 || dev >= 64) return 0;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      cached[dev] = n;
-  }
-  return cached[dev];
-}
+// (vmhost::device_cus: 0 when it cannot be queried — no device: the size queries then
+// assume kCalibCUs)
+using vmhost::device_cus;
 
 static constexpr int kCalibCUs = 256;  // the part the cost model below was swept on
 static int cus_or_calib(int cus) { return cus > 0 ? cus : kCalibCUs; }
