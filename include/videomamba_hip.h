@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 15
+#define VM_ABI_VERSION 14
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -305,11 +305,6 @@ int vm_conv_proj_fits(int batch, int out_len, int seqlen, int dim, int e, int r_
  * wdt_pad as vm_conv_proj_fwd.  Rows with step >= seqlen get u = 0.  `workspace`:
  * vm_in_proj_conv_proj_workspace_bytes() bytes (the x_dbl partials).
  * vm_in_proj_conv_proj_fits: 1 when the shape is accepted (pure host code).
- * ABI v15: `counters` (nullable): vm_in_proj_conv_proj_counter_bytes() ZEROED bytes, 4-byte
- * aligned, one buffer per stream (no two concurrent launches may share it); every launch
- * leaves them zeroed.  With counters, no dt rows and dim <= 1152 the launch is ONE kernel:
- * the last of a row tile's splits to finish sums the partials (same bits as the second
- * launch, which runs otherwise).
  */
 int vm_in_proj_conv_proj_fwd(const void* hn, long long ldh, const void* w_in, long long ldw, int k,
                              void* z, long long ldz, const float* conv_weight,
@@ -320,9 +315,8 @@ int vm_in_proj_conv_proj_fwd(const void* hn, long long ldh, const void* w_in, lo
                              long long u_tl, void* xdbl, long long xd_tl, void* dt,
                              long long dt_tl, int out_len, int batch, int dim, int seqlen,
                              int width, void* workspace, long long workspace_bytes,
-                             void* counters, long long counter_bytes, vm_stream_t stream);
+                             vm_stream_t stream);
 long long vm_in_proj_conv_proj_workspace_bytes(int batch, int out_len, int dim, int e);
-long long vm_in_proj_conv_proj_counter_bytes(int batch, int out_len);
 int vm_in_proj_conv_proj_fits(int k, int batch, int out_len, int dim, int e, int e_pad,
                               int r_pad, int width, int has_dt);
 

@@ -15,12 +15,6 @@ if len(sys.argv) > 2:  # option overrides, e.g. small_gemm_max_n=4096
     from videomamba_amd import options
     for kv in sys.argv[2:]:
         k, v = kv.split("=")
-        if k == "ic_sum":  # ic_sum=launch: the x_dbl partials summed by a second launch
-            import functools
-            from videomamba_amd import kernels as K
-            K.in_proj_conv_proj_raw = functools.partial(K.in_proj_conv_proj_raw,
-                                                        in_kernel_sum=(v != "launch"))
-            continue
         t = type(getattr(options.get(), k))
         val = v.lower() in ("1", "true", "yes", "on") if t is bool else t(v)
         options._OPTS = options.dataclasses.replace(options.get(), **{k: val})

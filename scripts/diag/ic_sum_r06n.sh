@@ -2,6 +2,7 @@
 # Round 6: the in_proj + conv kernel's x_dbl partials summed by the row tile's last
 # arriving split (one launch, ABI v15) against the second reduce launch: parity tests,
 # then the B = 1 chunk graph alternating, then a kernel trace of the product form.
+# Ran against commit 90c4891 (the in-kernel sum and b1_chunk_graph.py's ic_sum= hook; reverted).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r06n}

@@ -14,7 +14,6 @@ import torch
 import video_mamba
 import videomamba_amd.videomamba as vm_module
 from videomamba_amd import _lib
-from videomamba_amd import kernels as K
 from videomamba_amd.mamba_simple import Mamba
 from videomamba_amd.videomamba import PretrainVideoMamba, create_block, load_state_dict
 
@@ -295,19 +294,6 @@ def test_scan_workspace_query_without_gpu():
     assert lib.vm_selective_scan_sync_bytes(2, 64, 100, 16, 4) == 16 + 2 * 1 * 1 * 17 * 64 * 8
     assert lib.vm_selective_scan_sync_bytes(72, 1152, 3137, 16, 0) == 0
     assert lib.vm_selective_scan_sync_bytes(1, 1152, 3137, 16, 0) > 0
-
-
-def test_in_proj_conv_counter_span_without_gpu():
-    """vm_in_proj_conv_proj_fwd's arrival counters (ABI v15): one 4-byte word per 112-row
-    x tile, rounded to 64 bytes, placed after the region vm_linear_add_norm_fwd uses at the
-    same row count, so the two kernels never share a counter word in one buffer."""
-    lib = _lib.load()
-    assert lib.vm_in_proj_conv_proj_counter_bytes(1, 3144) == ((3144 + 111) // 112 * 4 + 63) // 64 * 64
-    assert lib.vm_in_proj_conv_proj_counter_bytes(2, 3144) == ((6288 + 111) // 112 * 4 + 63) // 64 * 64
-    assert lib.vm_in_proj_conv_proj_counter_bytes(0, 3144) == 0
-    off, nb = K.in_proj_conv_counter_span(1, 3144)
-    assert off >= lib.vm_linear_add_norm_counter_bytes(3144) and off % 64 == 0
-    assert nb == lib.vm_in_proj_conv_proj_counter_bytes(1, 3144)
 
 
 def test_scan_segment_cost_model_choices_without_gpu():

@@ -1214,10 +1214,7 @@ def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
     :381-416).  z, u, x_dbl, dt and the new conv state are bit-identical — for sequences
     shorter than a 112-row tile and longer than many, chunks padded past their length,
     sequence starts mid-tile (bsz > 1; batch 8, the kernel's maximum), a carried conv state in bf16 / fp32 or none, dt rows
-    or none (the scan computes them), and the M-16f chunk shape (3137 tokens).  Without dt
-    rows the partials are summed either by the row tile's last arriving split inside the
-    kernel (ABI v15, the product form) or by a second launch: both are checked, the in-kernel
-    sum over three repeated launches on one counter buffer, which must be zero after each."""
+    or none (the scan computes them), and the M-16f chunk shape (3137 tokens)."""
     from videomamba_amd.mamba_simple import Mamba
     torch.manual_seed(d_model + bsz)
     m = Mamba(d_model=d_model, d_state=16, d_conv=4, expand=2, layer_idx=0).to(DEV, torch.bfloat16)
@@ -1241,8 +1238,7 @@ def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
                 torch.bfloat16 if cs_kind == "bf16" else torch.float32)
         csi_s = (cs.stride(0), cs.stride(1)) if cs is not None else (0, 0)
         outs = []
-        forms = [(False, False), (True, False), (True, True), (True, True), (True, True)]
-        for fused, in_kernel_sum in forms:
+        for fused in (False, True):
             cso = torch.full((bsz, Dm, W), float("nan"), device=DEV, dtype=torch.bfloat16)
             u = torch.full((n, Dm), float("nan"), device=DEV, dtype=torch.bfloat16)
             xd = torch.full((n, E), float("nan"), device=DEV, dtype=torch.bfloat16)
@@ -1253,11 +1249,7 @@ def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
                                                 wdt_pad.shape[1], W, with_dt)
                 K.in_proj_conv_proj_raw(hn, w_in, xz[:, Dm:], cw, cb, cs, csi_s, cso,
                                         (Dm * W, W), wx_pad, E, wdt_pad, R, u, xd, dt, Lp,
-                                        bsz, Dm, L, W, st, in_kernel_sum=in_kernel_sum)
-                if in_kernel_sum:
-                    off, nb = K.in_proj_conv_counter_span(bsz, Lp)
-                    cbuf = K.counter_buffer(hn.device, st, off + nb)
-                    assert int(cbuf[off:off + nb].count_nonzero()) == 0, (L, "counters left set")
+                                        bsz, Dm, L, W, st)
             else:
                 K.linear(hn, w_in, out=xz)
                 K.conv_proj_raw(xz, (Lp * 2 * Dm, 2 * Dm), cw, cb, cs, csi_s, cso, (Dm * W, W),
@@ -1265,12 +1257,11 @@ def test_in_proj_conv_proj_bitwise_equals_in_proj_then_conv_proj(d_model, bsz):
                                 xd, (Lp * E, E), dt, (Lp * Dm, Dm), Lp, bsz, Dm, L, W, st)
             outs.append((xz[:, Dm:], u, xd, dt, cso))
         torch.cuda.synchronize()
-        for form, other in zip(forms[1:], outs[1:]):
-            for name, a, b in zip(("z", "u", "x_dbl", "dt", "conv_state"), outs[0], other):
-                if a is None:
-                    continue
-                assert torch.equal(a, b), (L, Lp, cs_kind, form, name,
-                                           (a.float() - b.float()).abs().nan_to_num(9.0).max().item())
+        for name, a, b in zip(("z", "u", "x_dbl", "dt", "conv_state"), *outs):
+            if a is None:
+                continue
+            assert torch.equal(a, b), (L, Lp, cs_kind, name,
+                                       (a.float() - b.float()).abs().nan_to_num(9.0).max().item())
 
 
 def test_in_proj_conv_proj_rejects_unsupported_shapes():

@@ -32,7 +32,6 @@ namespace vm {
 
 typedef __attribute__((__vector_size__(8 * sizeof(short)))) short ic_bf16x8;
 typedef __attribute__((__vector_size__(4 * sizeof(float)))) float ic_f32x4;
-typedef __attribute__((__vector_size__(4 * sizeof(int)))) unsigned ic_u32x4;
 
 struct InConvParams {
   const bf16_t* x; long long ldx;  // hn (ntok, k)
@@ -40,8 +39,6 @@ struct InConvParams {
   bf16_t* z; long long ldz;        // z half of xz: (ntok, dim)
   ConvProjTmArgs a;                // conv / x_proj operands (a.x unused)
   float* part;                     // [nsplit][ntok][ep] fp32 x_proj partials
-  unsigned* cnt;                   // per x row tile arrival counters (zeroed, left zeroed) or
-                                   // nullptr: the partials are summed by a second launch
   int ntok, nsplit, ep, k;
   int nxr, nzr;                    // x row tiles (112 rows), z row tiles (128 rows)
 };
@@ -51,8 +48,6 @@ constexpr int kIcOut = 112;                  // x output rows per tile
 constexpr int kIcHalo = 16;                  // rows above them computed for the conv
 constexpr int kIcPitch = 136;                // bf16 pitch of the LDS x / u tile
 constexpr int kIcCsSeq = 3;                  // sequences starting in a tile (out_len >= 56)
-constexpr int kIcMaxSplit = 9;               // in-kernel x_dbl sum: dim <= 1152
-constexpr int kIcSC1 = 16;                   // buffer cache-policy bit: sc1 (agent-coherent)
 constexpr int kIcStage = (128 + 128) * kIcRow;  // one K-step stage: A and B rows
 constexpr int kIcOBytes = 128 * kIcPitch * 2;   // x tile [128][kIcPitch] bf16
 constexpr int kIcWBytes = 80 * kIcPitch * 2;    // W_x slice [e_pad <= 80][kIcPitch]
@@ -69,54 +64,6 @@ __device__ __forceinline__ void ic_lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt at their maximum
   __builtin_amdgcn_s_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// x_dbl rows tok_lo .. tok_lo + 111 = bf16(sum of the NS split partials in split order):
-// xdbl_reduce_kernel's arithmetic (from 0, split 0 first, fp32), one item per (token,
-// 4 columns), two items per thread per round so each round is one batch of 2 NS sc1 loads.
-template <int NS>
-__device__ __forceinline__ void ic_reduce_rows(const InConvParams& q, __amdgpu_buffer_rsrc_t prr,
-                                               int tok_lo, int tid) {
-  constexpr int NT = 512;
-  const ConvProjTmArgs& p = q.a;
-  const int nq = q.ep >> 2;
-  const int nitem = min(kIcOut, q.ntok - tok_lo) * nq;
-  const int e_q = (p.e + 3) >> 2;
-#pragma unroll 1
-  for (int i0 = 0; i0 < nitem; i0 += 2 * NT) {
-    ic_u32x4 pv[2][NS];
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int it = i0 + h2 * NT + tid;
-      const int r = it / nq, qd = it - r * nq;
-      const bool live = it < nitem && qd < e_q;
-#pragma unroll
-      for (int s2 = 0; s2 < NS; ++s2)
-        pv[h2][s2] = __builtin_bit_cast(ic_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-            prr, live ? ((s2 * q.ntok + tok_lo + r) * q.ep + 4 * qd) * 4
-                      : static_cast<int>(0x80000000u), 0, kIcSC1));
-    }
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int it = i0 + h2 * NT + tid;
-      const int r = it / nq, qd = it - r * nq;
-      if (it >= nitem || qd >= e_q) continue;
-      float sv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < NS; ++s2)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) sv[kk] += __uint_as_float(pv[h2][s2][kk]);
-      bf16_t* dst = p.xdbl + (long long)(tok_lo + r) * p.xd_tl + 4 * qd;
-#pragma unroll
-      for (int kk = 0; kk < 4; kk += 2)
-        if (4 * qd + kk + 1 < p.e)
-          *reinterpret_cast<uint32_t*>(dst + kk) =
-              static_cast<uint32_t>(from_f32<bf16_t>(sv[kk])) |
-              (static_cast<uint32_t>(from_f32<bf16_t>(sv[kk + 1])) << 16);
-        else if (4 * qd + kk < p.e)
-          dst[kk] = from_f32<bf16_t>(sv[kk]);
-    }
-  }
 }
 
 template <int NK, int NB>
@@ -446,45 +393,15 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
       }
   }
   __builtin_amdgcn_wave_barrier();
-  // the partial rows: sc1 (write-through) 16-byte stores, so the row tile's last arriving
-  // split can read them back from another XCD without a release / acquire pair
-  const auto prr = __builtin_amdgcn_make_buffer_rsrc(
-      q.part, 0, static_cast<int>((long long)q.nsplit * q.ntok * q.ep * 4), 0x00020000);
   if (mw) {
     const int nq = q.ep >> 2;
     for (int i = lane; i < 16 * nq; i += 64) {
       const int r = i / nq, qd = i - r * nq;
       const int tok = tok_lo + wave * 16 + r;
       if (tok < q.ntok)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(ic_u32x4, *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd])),
-            prr, ((sp * q.ntok + tok) * q.ep + 4 * qd) * 4, 0, kIcSC1);
+        *reinterpret_cast<float4*>(q.part + ((long long)sp * q.ntok + tok) * q.ep + 4 * qd) =
+            *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd]);
     }
-  }
-  if (q.cnt == nullptr) return;  // uniform: xdbl_reduce_kernel sums the partials
-
-  // ---- the row tile's last arriving split sums the partials (MI355X_MICROARCH.md cross-
-  // workgroup table, row 1): every partial store is sc1; each storing wave waits vmcnt(0),
-  // a workgroup barrier, then one lane adds to the row tile's counter (agent-scope atomic);
-  // the workgroup whose add returns nsplit - 1 came last: it resets the counter (so the
-  // buffer is zero again for the next launch or graph replay) and, after a barrier, reads
-  // every split's rows with sc1 loads.  No workgroup ever waits on another.
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's partial (and u / state) stores acknowledged
-  __syncthreads();
-  int& s_last = *reinterpret_cast<int*>(dsm + kIcLds - 16);
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(&q.cnt[rt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == static_cast<unsigned>(q.nsplit - 1);
-    if (last) __hip_atomic_store(&q.cnt[rt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;  // uniform
-  switch (q.nsplit) {  // uniform
-#define VM_ICR(NS) case NS: ic_reduce_rows<NS>(q, prr, tok_lo, tid); break;
-    VM_ICR(1) VM_ICR(2) VM_ICR(3) VM_ICR(4) VM_ICR(5) VM_ICR(6) VM_ICR(7) VM_ICR(8) VM_ICR(9)
-#undef VM_ICR
-    default: break;
   }
 }
 
@@ -525,8 +442,7 @@ bool inproj_conv_ok(int k, const ConvProjTmArgs& a) {
   return k % 64 == 0 && a.batch >= 1 && a.batch <= kSkMaxBatch && a.dim % 128 == 0 &&
          a.dim <= 2048 && a.out_len >= 56 && a.e_pad <= 80 && a.e_pad % 16 == 0 &&
          (a.e + 3) / 4 * 4 <= kSkMaxEp && (a.wdt == nullptr || a.r_pad <= 64) &&
-         a.width >= 1 && a.width <= 4 && ntok * a.u_tl * 2 < (1ll << 31) &&
-         static_cast<long long>(a.dim / 128) * ntok * ((a.e + 3) / 4 * 4) * 4 < (1ll << 31);
+         a.width >= 1 && a.width <= 4 && ntok * a.u_tl * 2 < (1ll << 31);
 }
 
 void inproj_conv_launch(const InConvParams& q0, hipStream_t s) {
@@ -554,15 +470,6 @@ extern "C" long long vm_in_proj_conv_proj_workspace_bytes(int batch, int out_len
   return conv_proj_sk_workspace_bytes(batch, out_len, dim, e);
 }
 
-// in-kernel x_dbl sum (counters given, no dt rows): one arrival counter per 112-row x tile
-static bool ic_fused_sum(int dim, bool dt) { return !dt && dim / 128 <= kIcMaxSplit; }
-
-extern "C" long long vm_in_proj_conv_proj_counter_bytes(int batch, int out_len) {
-  if (batch < 1 || out_len < 1) return 0;
-  const long long ntok = static_cast<long long>(batch) * out_len;
-  return ((ntok + kIcOut - 1) / kIcOut * 4 + 63) / 64 * 64;
-}
-
 extern "C" int vm_in_proj_conv_proj_fits(int k, int batch, int out_len, int dim, int e, int e_pad,
                                          int r_pad, int width, int has_dt) {
   ConvProjTmArgs a{};
@@ -580,7 +487,7 @@ extern "C" int vm_in_proj_conv_proj_fwd(
     const void* wx_pad, int e, int e_pad, const void* wdt_pad, int r, int r_pad,
     void* u, long long u_tl, void* xdbl, long long xd_tl, void* dt, long long dt_tl,
     int out_len, int batch, int dim, int seqlen, int width, void* workspace,
-    long long workspace_bytes, void* counters, long long counter_bytes, vm_stream_t stream) {
+    long long workspace_bytes, vm_stream_t stream) {
   if (!hn || !w_in || !z || !conv_weight || !wx_pad || !u || !xdbl || (dt && !wdt_pad)) {
     vmhost::set_error("vm_in_proj_conv_proj_fwd: null required pointer");
     return VM_E_INVALID;
@@ -621,23 +528,12 @@ extern "C" int vm_in_proj_conv_proj_fwd(
                       "(vm_in_proj_conv_proj_workspace_bytes)", need);
     return VM_E_INVALID;
   }
-  if (counters && counter_bytes < vm_in_proj_conv_proj_counter_bytes(batch, out_len)) {
-    vmhost::set_error("vm_in_proj_conv_proj_fwd: needs %lld counter bytes "
-                      "(vm_in_proj_conv_proj_counter_bytes)",
-                      vm_in_proj_conv_proj_counter_bytes(batch, out_len));
-    return VM_E_INVALID;
-  }
-  if (counters && (reinterpret_cast<uintptr_t>(counters) & 3)) {
-    vmhost::set_error("vm_in_proj_conv_proj_fwd: counters must be 4-byte aligned");
-    return VM_E_INVALID;
-  }
   InConvParams q{};
   q.x = static_cast<const bf16_t*>(hn); q.ldx = ldh;
   q.w = static_cast<const bf16_t*>(w_in); q.ldw = ldw;
   q.z = static_cast<bf16_t*>(z); q.ldz = ldz;
   q.a = a;
   q.part = static_cast<float*>(workspace);
-  q.cnt = (counters && ic_fused_sum(dim, dt != nullptr)) ? static_cast<unsigned*>(counters) : nullptr;
   q.ntok = static_cast<int>(ntok);
   q.nsplit = dim / 128;
   q.ep = (e + 3) / 4 * 4;
@@ -648,7 +544,7 @@ extern "C" int vm_in_proj_conv_proj_fwd(
   inproj_conv_launch(q, s);
   if (dt) {
     conv_proj_sk_reduce_launch(a, q.part, s);
-  } else if (!q.cnt) {
+  } else {
     const unsigned blocks = static_cast<unsigned>((ntok * ((e + 3) / 4) + 255) / 256);
     switch (q.nsplit) {
 #define VM_XR(NS) case NS: hipLaunchKernelGGL(xdbl_reduce_kernel<NS>, dim3(blocks), dim3(256), 0, s, q); break;

@@ -99,7 +99,7 @@ class StreamingChunkGraph:
         self._tpos_offset = None  # temporal offset whose embedding slice static_tpos holds
         self._ws = None  # scan scratch owned by the captured graphs
         self._sync = None  # the one-launch scan's sync buffer (zeroed once; replays keep it valid)
-        self._cnt = None  # fused out_proj + norm / in_proj + conv counters (zeroed, left zeroed)
+        self._cnt = None  # vm_linear_add_norm_fwd hand-off counters (zeroed, left zeroed)
 
     # ------------------------------------------------------------------ state
     def _state_at(self, parity: int) -> List[Tuple[Tensor, Tensor]]:
@@ -170,9 +170,7 @@ class StreamingChunkGraph:
         if self._sync is None or self._sync.numel() < max(sync_need, 1):
             self._sync = torch.zeros(max(sync_need, 4096), dtype=torch.uint8, device=self.device)
         Lp = (self.tt * gh * gw + 1 + 7) // 8 * 8
-        # vm_linear_add_norm_fwd's counters, then vm_in_proj_conv_proj_fwd's after them
-        ic_off, ic_bytes = K.in_proj_conv_counter_span(self.batch, Lp)
-        cnt_need = max(K.linear_add_norm_counter_bytes(self.batch * Lp), ic_off + ic_bytes)
+        cnt_need = K.linear_add_norm_counter_bytes(self.batch * Lp)
         if self._cnt is None or self._cnt.numel() < max(cnt_need, 1):
             self._cnt = torch.zeros(max(cnt_need, 4096), dtype=torch.uint8, device=self.device)
         return self._ws

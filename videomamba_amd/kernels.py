@@ -410,22 +410,15 @@ def in_proj_conv_proj_fits(k: int, batch: int, out_len: int, dim: int, e: int, e
 
 
 def in_proj_conv_proj_raw(hn, w_in, z, cw32, cb32, cs_in, csi_s, cs_out, cso_s, wx_pad, e,
-                          wdt_pad, r, u, xdbl, dt, out_len, batch, dim, seqlen, width, stream,
-                          in_kernel_sum: bool = True):
+                          wdt_pad, r, u, xdbl, dt, out_len, batch, dim, seqlen, width, stream):
     """in_proj + conv1d + SiLU -> x_proj [-> dt_proj] in two launches (bf16, small batches,
     token-major): hn (n, k), w_in (2 dim, k); z (n, dim) receives in_proj's z half (any row
     stride, e.g. the right half of an (n, 2 dim) xz), u (n, dim), xdbl (n, e), dt (n, dim) or
     None (the scan computes dt).  Bit-identical to ``linear`` + :func:`conv_proj_raw`.
-    Scratch for the x_proj partials comes from :func:`scratch`; the row tiles' arrival
-    counters (ABI v15: without dt rows the last split of a row tile sums the partials, one
-    launch) live in the stream's counter buffer (:func:`counter_buffer`) past the region
-    ``vm_linear_add_norm_fwd`` uses at this row count, so the two never share a word.
-    ``in_kernel_sum=False`` passes no counters: the second launch sums (same bits)."""
+    Scratch for the x_proj partials comes from :func:`scratch`."""
     lib = _lib.load()
     nbytes = int(lib.vm_in_proj_conv_proj_workspace_bytes(batch, out_len, dim, e))
     ws = scratch(hn.device, int(stream), nbytes)
-    cnt_off, cnt_bytes = in_proj_conv_counter_span(batch, out_len)
-    cbuf = counter_buffer(hn.device, int(stream), cnt_off + cnt_bytes)
     rc = lib.vm_in_proj_conv_proj_fwd(
         _p(hn), hn.stride(0), _p(w_in), w_in.stride(0), hn.shape[1], _p(z), z.stride(0),
         _p(cw32), _p(cb32),
@@ -435,17 +428,8 @@ def in_proj_conv_proj_raw(hn, w_in, z, cw32, cb32, cs_in, csi_s, cs_out, cso_s, 
         wdt_pad.shape[1] if (wdt_pad is not None and dt is not None) else 0,
         _p(u), u.stride(0), _p(xdbl), xdbl.stride(0), _p(dt),
         dt.stride(0) if dt is not None else 0, out_len, batch, dim, seqlen, width,
-        _p(ws), nbytes, (cbuf.data_ptr() + cnt_off) if in_kernel_sum else None,
-        cnt_bytes if in_kernel_sum else 0, stream)
+        _p(ws), nbytes, stream)
     _lib.check(rc, "vm_in_proj_conv_proj_fwd")
-
-
-def in_proj_conv_counter_span(batch: int, out_len: int) -> Tuple[int, int]:
-    """(byte offset, bytes) of ``vm_in_proj_conv_proj_fwd``'s arrival counters in a counter
-    buffer: right after the region ``vm_linear_add_norm_fwd`` uses for batch * out_len rows."""
-    lib = _lib.load()
-    off = int(lib.vm_linear_add_norm_counter_bytes(batch * out_len))
-    return (off + 63) // 64 * 64, int(lib.vm_in_proj_conv_proj_counter_bytes(batch, out_len))
 
 
 def conv_proj_fits(batch: int, out_len: int, seqlen: int, dim: int, e: int, r_pad: int,
