@@ -11,6 +11,11 @@ from videomamba_amd.graphs import StreamingChunkGraph  # noqa: E402
 from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+for kv in list(sys.argv[2:]):  # lib=<path>: a probe build of the library (A/B)
+    if kv.startswith("lib="):
+        import videomamba_amd._lib as L
+        L.LIB_PATH = os.path.abspath(kv[4:])
+        sys.argv.remove(kv)
 if len(sys.argv) > 2:  # option overrides, e.g. small_gemm_max_n=4096
     from videomamba_amd import options
     for kv in sys.argv[2:]:
