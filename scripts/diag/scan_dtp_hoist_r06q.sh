@@ -3,7 +3,7 @@
 # round trip fewer per 16 steps) against the committed HEAD build (tools/probes/ab/base_head,
 # VARIANT_DIR=ab build_variant.py --rev HEAD base_head): scan parity tests, then the B = 1
 # chunk graph alternating ("^ " = this build, "^ lib=..." = HEAD).  Ran against the working
-# tree of commit 3f... (reverted: DESIGN §7).
+# tree before commit fe2d7dc (the hoist was reverted there, never committed: DESIGN §7).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r06q}
