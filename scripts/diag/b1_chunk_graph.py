@@ -11,7 +11,11 @@ from videomamba_amd.graphs import StreamingChunkGraph  # noqa: E402
 from videomamba_amd.videomamba import PretrainVideoMamba  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-for kv in list(sys.argv[2:]):  # lib=<path>: a probe build of the library (A/B)
+batch = 1
+for kv in list(sys.argv[2:]):  # lib=<path>: a probe build of the library (A/B); batch=<clips>
+    if kv.startswith("batch="):
+        batch = int(kv[6:])
+        sys.argv.remove(kv)
     if kv.startswith("lib="):
         import videomamba_amd._lib as L
         L.LIB_PATH = os.path.abspath(kv[4:])
@@ -25,8 +29,8 @@ if len(sys.argv) > 2:  # option overrides, e.g. small_gemm_max_n=4096
         options._OPTS = options.dataclasses.replace(options.get(), **{k: val})
 torch.manual_seed(0)
 model = PretrainVideoMamba(depth=32, embed_dim=576, num_frames=16).cuda().to(torch.bfloat16).eval()
-x = torch.randn(1, 3, 16, 224, 224, device="cuda").to(torch.bfloat16)
-runner = StreamingChunkGraph(model, batch=1, frames=16)
+x = torch.randn(batch, 3, 16, 224, 224, device="cuda").to(torch.bfloat16)
+runner = StreamingChunkGraph(model, batch=batch, frames=16)
 with torch.no_grad():
     for _ in range(2):  # captures both conv-state buffer parities
         runner.run(x, temporal_pos_offset=0)

@@ -39,6 +39,19 @@ VARIANTS = {
     # dt_proj-in-scan kernel with the inline-asm d16_hi u / z loads and fp32 dt block (the
     # round-5 A/B, measured slower: DESIGN.md §3.1.1; built from LEGACY_REV)
     "dtp_d16": [("vm_scan_seq.hip", "constexpr bool kDtpD16 = false;", "constexpr bool kDtpD16 = true;")],
+    # chunked scan: the two waves of each SIMD (w, w + 4) swap the raised issue priority
+    # every kPF steps, so neither finishes its step loop far ahead of the other (round 6)
+    "ch_prio_toggle": [("vm_scan_seq.hip",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n      if ((((tg - t_beg) / kPF) + (wave >> 2)) & 1) __builtin_amdgcn_s_setprio(1);\n      else __builtin_amdgcn_s_setprio(0);\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;")],
+    # the same with a swap every 2 kPF steps
+    "ch_prio_toggle2": [("vm_scan_seq.hip",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n      if ((((tg - t_beg) / (2 * kPF)) + (wave >> 2)) & 1) __builtin_amdgcn_s_setprio(1);\n      else __builtin_amdgcn_s_setprio(0);\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;")],
+    # the same with one swap, at the middle of the segment
+    "ch_prio_half": [("vm_scan_seq.hip",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;",
+                        "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n      if ((2 * (tg - t_beg) + kPF >= t_end - t_beg) != ((wave >> 2) & 1)) __builtin_amdgcn_s_setprio(1);\n      else __builtin_amdgcn_s_setprio(0);\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],

@@ -1232,6 +1232,15 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     float dl_nx = delta_of(rd[0]);
     float g_nx = GA ? gate_of(rz[0]) : 0.0f;
     for (int tg = t_beg; tg < t_end; tg += kPF) {
+      // The two waves of a SIMD (w, w + 4) share its issue slots, and the hardware favours
+      // the older one: left alone, one wave finished its loop ~1.7x before the other, which
+      // then ran its rest alone at a wave's latency-bound rate while the block waited at its
+      // next barrier (r05 stamps: 7.2 vs 12.4 us in PASS 1).  Each wave raises its priority
+      // for one half of the segment and its SIMD partner for the other, so the two finish
+      // together: B = 1 chunk -2.5 to -3 %, B = 2 -2.4 % (r06r).  Issue order
+      // only: every value is unchanged.
+      if ((2 * (tg - t_beg) + kPF >= t_end - t_beg) != ((wave >> 2) & 1)) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int j = 0; j < kPF; ++j) {
         const int t = tg + j;
