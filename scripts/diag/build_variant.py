@@ -285,8 +285,8 @@ VARIANTS = {
          "  VM_STAMP(7)\n  f2 A2[kMaxN / 2], h[kMaxN / 2];\n#pragma unroll\n  for (int q = 0; q < kMaxN / 2; ++q) {\n    A2[q] = f2{sA[2 * q][lane], sA[2 * q + 1][lane]};"),
         ("vm_scan_seq.hip", "  const int nch = min(64, p.dim - d0);  // live channels of this group\n",
          "  const int nch = min(64, p.dim - d0);  // live channels of this group\n  VM_STAMP(0)\n"),
-        ("vm_scan_seq.hip", "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n",
-         "  // they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n  VM_STAMP(1)\n"),
+        ("vm_scan_seq.hip", "  // pending they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n",
+         "  // pending they would merge into the step loop's header waits\n  __builtin_amdgcn_s_waitcnt(0);\n  VM_STAMP(1)\n"),
         ("vm_scan_seq.hip", "  run_steps(BoolTag<false>{});\n#pragma unroll\n",
          "  run_steps(BoolTag<false>{});\n  VM_STAMP(2)\n#pragma unroll\n"),
         ("vm_scan_seq.hip", "    // every wave's E_j is in sH (an LDS-only barrier: the granule stores need no drain)",

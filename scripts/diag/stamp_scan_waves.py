@@ -10,6 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 import videomamba_amd._lib as L  # noqa: E402
 L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "var", "sc_stampw", "libvideomamba_hip.so")
+if not os.path.exists(L.LIB_PATH):  # a build pushed to the GPU box (VARIANT_DIR=ab)
+    L.LIB_PATH = os.path.join(ROOT, "tools", "probes", "ab", "sc_stampw", "libvideomamba_hip.so")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from bench import scan_roofline  # noqa: E402
