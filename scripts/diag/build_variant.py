@@ -52,6 +52,11 @@ VARIANTS = {
     "ch_prio_half": [("vm_scan_seq.hip",
                         "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;",
                         "    for (int tg = t_beg; tg < t_end; tg += kPF) {\n      if ((2 * (tg - t_beg) + kPF >= t_end - t_beg) != ((wave >> 2) & 1)) __builtin_amdgcn_s_setprio(1);\n      else __builtin_amdgcn_s_setprio(0);\n#pragma unroll\n      for (int j = 0; j < kPF; ++j) {\n        const int t = tg + j;\n        const bool live = t < t_end;")],
+    # bench scan with its LDS dynamic (the compiler's occupancy target ignores it) and a
+    # 5-waves-per-SIMD register target (96 VGPRs): at run time LDS still holds it to 4 waves
+    # per SIMD, which leaves 128 registers per SIMD for the other sub-batch stream's
+    # add + RMSNorm waves (40 each) beside it (round 6)
+    "dtp_dyn5": [('vm_scan_seq.hip', '  __shared__ __attribute__((aligned(16))) bf16_t sW[NW][64 * KP];\n  constexpr int DR = kDtRow;\n  __shared__ __attribute__((aligned(16))) uint32_t sD[NW][64 * DR];\n', '  constexpr int DR = kDtRow;\n  extern __shared__ __attribute__((aligned(16))) char dtp_dsm[];\n  auto& sW = *reinterpret_cast<bf16_t (*)[NW][64 * KP]>(dtp_dsm);\n  auto& sD = *reinterpret_cast<uint32_t (*)[NW][64 * DR]>(dtp_dsm + sizeof(bf16_t) * NW * 64 * KP);\n'), ('vm_scan_seq.hip', 'template <int NKS>\n__global__ __launch_bounds__(64 * kSeqNW) void scan_seq_dtp_kernel', 'static size_t dtp_lds(int nks) { return kSeqNW * 64 * ((16 * nks + 4) * 2 + kDtRow * 4); }\n\ntemplate <int NKS>\n__global__ __launch_bounds__(64 * kSeqNW) __attribute__((amdgpu_waves_per_eu(5))) void scan_seq_dtp_kernel'), ('vm_scan_seq.hip', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<1>, grid, dim3(64 * kSeqNW), 0, s, p, q)', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<1>, grid, dim3(64 * kSeqNW), dtp_lds(1), s, p, q)'), ('vm_scan_seq.hip', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<2>, grid, dim3(64 * kSeqNW), 0, s, p, q)', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<2>, grid, dim3(64 * kSeqNW), dtp_lds(2), s, p, q)'), ('vm_scan_seq.hip', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), 0, s, p, q)', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<3>, grid, dim3(64 * kSeqNW), dtp_lds(3), s, p, q)'), ('vm_scan_seq.hip', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<4>, grid, dim3(64 * kSeqNW), 0, s, p, q)', 'hipLaunchKernelGGL(scan_seq_dtp_kernel<4>, grid, dim3(64 * kSeqNW), dtp_lds(4), s, p, q)')],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],
