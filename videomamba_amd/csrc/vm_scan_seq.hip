@@ -823,6 +823,12 @@ constexpr int kChW = 8;  // segments (waves) per workgroup
 // ahead (its C rows double the ring: SGPR spills in its loop cost more than the wait saves)
 constexpr bool kChBcPairs = true;
 constexpr int kChSPW = kMaxN / kChW;  // states a wave composes / publishes / walks
+// LBC (one-launch bf16 B|C rows, blocks of at most kChLbcRows steps): the block's B|C rows
+// staged once into LDS as fp32, read per step by a broadcast ds_read one step ahead instead
+// of scalar loads (out-of-order returns, so the SGPR ring could not run deeper than a pair)
+// and their SALU unpacking
+constexpr int kChLbcRows = 256;
+constexpr int kChLbcPer = kChLbcRows * 4 / (64 * kChW);  // 16-byte row pieces per thread
 constexpr int kChPoll = kChSPW == 2 ? 8 : 4;  // preceding blocks polled per round (one-launch)
 static_assert(kMaxN % kChW == 0 && (kChSPW == 1 || kChSPW == 2), "1 or 2 states per wave");
 
@@ -855,13 +861,15 @@ constexpr int kChDtpT = 64;              // max segment length with dt_proj insi
 constexpr int kChDtpPitch = kChDtpT + 8;  // bf16 per channel row of a wave's dt block
 constexpr int kChDtpWPitch = 64 + 8;      // bf16 per W_dt row in LDS (r_pad <= 64)
 
-template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false>
+template <typename T, int PASS, bool SP, bool HZ, bool BC1, bool PAIR, bool DTP = false,
+          bool LBC = false>
 __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams p, const ChunkWork w,
                                                                const DtpArgs q) {
   typedef __attribute__((address_space(4))) const uint32_t* cptr;
   constexpr int NWD = kMaxN * sizeof(T) / 4;  // 32-bit words per B (or C) row
   constexpr int ES = sizeof(T);
   static_assert(!DTP || sizeof(T) == 2, "dt_proj inside the scan is bf16 only");
+  static_assert(!LBC || (PASS == 3 && BC1 && sizeof(T) == 2), "LDS B|C rows: one launch, bf16 B|C");
   // sH: PASS 1 segment end states; PASS 2 the staged block aggregates, then H_blk in sH[0].
   // sA: A of the workgroup's 64 channels, transposed to [state][channel].
   __shared__ float sH[kChW][kMaxN][64];
@@ -872,6 +880,8 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // DTP: the group's W_dt rows [channel][r_pad] and each wave's dt block [channel][step]
   __shared__ __attribute__((aligned(16))) bf16_t sWd[DTP ? 64 * kChDtpWPitch : 8];
   __shared__ __attribute__((aligned(16))) bf16_t sDT[DTP ? kChW * 64 * kChDtpPitch : 8];
+  // LBC: the block's B|C rows (step t at row t - block start), fp32
+  __shared__ __attribute__((aligned(16))) float sBC[LBC ? kChLbcRows : 1][2 * kMaxN];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1022,8 +1032,22 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // the start-up loads): the per-step scalar row loads, one step ahead, then hit L2 instead
   // of paying an infinity-cache / HBM round trip every step.
   uint32_t warm[2] = {0u, 0u};
-  {
-    const int bt0 = blk * kChW * w.T;
+  const int blk_t0 = blk * kChW * w.T;
+  typedef __attribute__((ext_vector_type(4))) unsigned lbc_u4;
+  lbc_u4 lbcv[LBC ? kChLbcPer : 1];
+  if constexpr (LBC) {  // the block's B|C rows, 16-byte pieces, consumed after the start-up wait
+    const int bt1 = min(L, blk_t0 + kChW * w.T);
+    const char* base = reinterpret_cast<const char*>(Bq) + static_cast<long long>(blk_t0) * bsl;
+    const int span = bt1 > blk_t0 ? (bt1 - blk_t0 - 1) * static_cast<int>(bsl) + 2 * kMaxN * ES : 0;
+    const auto lr = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, span, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kChLbcPer; ++k) {
+      const int pc = static_cast<int>(threadIdx.x) + k * 64 * kChW;
+      lbcv[k] = __builtin_bit_cast(lbc_u4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               lr, (pc >> 2) * static_cast<int>(bsl) + (pc & 3) * 16, 0, 0));
+    }
+  } else {
+    const int bt0 = blk_t0;
     const int bt1 = min(L, bt0 + kChW * w.T);
     if (bt1 > bt0) {
       const char* base = reinterpret_cast<const char*>(Bq) + static_cast<long long>(bt0) * bsl;
@@ -1045,8 +1069,10 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   uint32_t ru[kPF], rd[kPF], rz[kPF];
   float sdel = 0.0f;
   if (t_beg < t_end) {
-    bc_load(t_beg, bcw[0]);
-    if constexpr (kChBcPairs) bc_load(min(t_beg + 1, tlast), bcw[1]);
+    if constexpr (!LBC) {
+      bc_load(t_beg, bcw[0]);
+      if constexpr (kChBcPairs) bc_load(min(t_beg + 1, tlast), bcw[1]);
+    }
 #pragma unroll
     for (int j = 0; j < kPF; ++j) {
       const int t = min(t_beg + j, tlast);
@@ -1085,6 +1111,19 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
   // pending they would merge into the step loop's header waits
   __builtin_amdgcn_s_waitcnt(0);
   asm volatile("" ::"v"(warm[0]), "v"(warm[1]));  // the L2 warm-up loads are not dead
+  if constexpr (LBC) {  // bf16 -> fp32 (exact), into sBC before the start-up barrier
+#pragma unroll
+    for (int k = 0; k < kChLbcPer; ++k) {
+      const int pc = static_cast<int>(threadIdx.x) + k * 64 * kChW;
+      float* dst = &sBC[pc >> 2][(pc & 3) * 8];
+      *reinterpret_cast<float4*>(dst) =
+          make_float4(__uint_as_float(lbcv[k][0] << 16), __uint_as_float(lbcv[k][0] & 0xffff0000u),
+                      __uint_as_float(lbcv[k][1] << 16), __uint_as_float(lbcv[k][1] & 0xffff0000u));
+      *reinterpret_cast<float4*>(dst + 4) =
+          make_float4(__uint_as_float(lbcv[k][2] << 16), __uint_as_float(lbcv[k][2] & 0xffff0000u),
+                      __uint_as_float(lbcv[k][3] << 16), __uint_as_float(lbcv[k][3] & 0xffff0000u));
+    }
+  }
   if constexpr (DTP) {
     const int row = tid / wdt_ppr, pc = tid - row * wdt_ppr;
     if (tid < 64 * wdt_ppr) *reinterpret_cast<wv4*>(&sWd[row * kChDtpWPitch + pc * 8]) = wdt_piece;
@@ -1231,6 +1270,20 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     };
     float dl_nx = delta_of(rd[0]);
     float g_nx = GA ? gate_of(rz[0]) : 0.0f;
+    // LBC: the next step's B (and, emitting, C) row from LDS, one step ahead
+    constexpr int NBC = EMIT ? 2 * kMaxN : kMaxN;
+    float bcn[LBC ? NBC : 1];
+    auto lbc_read = [&](int t) {
+      if constexpr (LBC) {
+        const float* src = &sBC[t - blk_t0][0];
+#pragma unroll
+        for (int i = 0; i < NBC / 4; ++i) {
+          const float4 v = *reinterpret_cast<const float4*>(src + 4 * i);
+          bcn[4 * i] = v.x; bcn[4 * i + 1] = v.y; bcn[4 * i + 2] = v.z; bcn[4 * i + 3] = v.w;
+        }
+      }
+    };
+    if constexpr (LBC) lbc_read(min(t_beg, t_end - 1));
     for (int tg = t_beg; tg < t_end; tg += kPF) {
       // The two waves of a SIMD (w, w + 4) share its issue slots, and the hardware favours
       // the older one: left alone, one wave finished its loop ~1.7x before the other, which
@@ -1251,7 +1304,12 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
         ru[j] = bload<T>(ur, voff, tn * us);
         if constexpr (!DTP) rd[j] = bload<T>(dr_, voff, tn * ds);
         if (HZ && EMIT) rz[j] = bload<T>(zr, voff, tn * zs);
-        if constexpr (kChBcPairs && !EMIT) {
+        float bcc[LBC ? NBC : 1];
+        if constexpr (LBC) {  // this step's row (read a step ago); fetch the next one
+#pragma unroll
+          for (int i = 0; i < NBC; ++i) bcc[i] = bcn[i];
+          lbc_read(min(t + 1, t_end - 1));
+        } else if constexpr (kChBcPairs && !EMIT) {
           if ((j & 1) == 0) {  // a pair starts: its two rows have landed; fetch the next pair's
             __builtin_amdgcn_s_waitcnt(0xC07F);
             bc_load(min(t + 2, tlast), bcw[(j + 2) & 3]);
@@ -1279,7 +1337,10 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
 #pragma unroll
         for (int q = 0; q < kMaxN / 2; ++q) {
           f2 Bp, Cp;
-          if constexpr (sizeof(T) == 2) {
+          if constexpr (LBC) {
+            Bp = f2{bcc[2 * q], bcc[2 * q + 1]};
+            Cp = EMIT ? f2{bcc[(NBC / 2) + 2 * q], bcc[(NBC / 2) + 2 * q + 1]} : Bp;
+          } else if constexpr (sizeof(T) == 2) {
             Bp = f2{__uint_as_float(cw[q] << 16), __uint_as_float(cw[q] & 0xffff0000u)};
             Cp = f2{__uint_as_float(cw[NWD + q] << 16), __uint_as_float(cw[NWD + q] & 0xffff0000u)};
           } else {
@@ -1404,7 +1465,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     // PASS 2 operands of the first kPF steps, in flight during the wait
     if (t_beg < t_end) {
-      bc_load(t_beg, bcw[0]);
+      if constexpr (!LBC) bc_load(t_beg, bcw[0]);
 #pragma unroll
       for (int j = 0; j < kPF; ++j) {
         const int t = min(t_beg + j, tlast);
@@ -1687,6 +1748,13 @@ static void launch_chunk_p(const ScanParams& p, const ChunkWork& w, hipStream_t 
                            const DtpArgs& q = DtpArgs{}) {
   dim3 grid((p.dim + 63) / 64, w.nblk, p.batch);
   if (w.gran) {  // one launch: blocks hand their aggregates on through the sync buffer
+    if constexpr (DTP && BC1 && sizeof(T) == 2) {
+      if (kChW * w.T <= kChLbcRows) {  // the block's B|C rows fit the LDS staging block
+        hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR, DTP, true>), grid,
+                           dim3(64 * kChW), 0, s, p, w, q);
+        return;
+      }
+    }
     hipLaunchKernelGGL((scan_chunk_kernel<T, 3, SP, HZ, BC1, PAIR, DTP>), grid, dim3(64 * kChW),
                        0, s, p, w, q);
     return;
