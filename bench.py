@@ -230,7 +230,8 @@ def scan_roofline(batch, reps, device, layout="tm", dtp=False):
 
 # the committed rocprofv3 --kernel-trace --stats summary of a default bench command, whose
 # scan launches all ran inside the two-stream step (scripts/round_evidence.sh PART=1)
-IN_STEP_TRACES = ("profiles/r06j_bench_kernel_stats.csv", "profiles/r05zzp_bench_kernel_stats.csv")
+IN_STEP_TRACES = ("profiles/r06v_bench_kernel_stats.csv", "profiles/r06j_bench_kernel_stats.csv",
+                  "profiles/r05zzp_bench_kernel_stats.csv")
 
 
 def _trace_in_step(algo, kname="scan_seq_dtp_kernel"):
