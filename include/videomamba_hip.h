@@ -26,8 +26,6 @@
  *                                 layout (mamba_simple.py:381-416)
  *   vm_add_norm_fwd            <- mamba_ssm rms_norm_fn / layer_norm_fn
  *                                 (models/videomamba/videomamba.py:152-166, :904-918)
- *   vm_residual_add_fwd        <- the residual add of rms_norm_fn (videomamba.py:141-166)
- *                                 issued on its own, ahead of the norm
  *   vm_norm_pool_fwd           <- final add + norm (videomamba.py:896-918) with the
  *                                 per-frame / whole-clip column sums of the pooling
  *   vm_pool_finish_fwd         <- the pooling tail: means, CLS add / concat and pool_norm
@@ -62,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VM_ABI_VERSION 15
+#define VM_ABI_VERSION 14
 
 #define VM_DTYPE_F32 0
 #define VM_DTYPE_BF16 1
@@ -368,16 +366,6 @@ int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual, int res_dt
                     const float* weight, const float* bias, void* out, int out_dtype,
                     void* residual_out, int res_out_dtype, long long rows, int cols,
                     float eps, int is_rms, vm_stream_t stream);
-
-/*
- * ABI v15.  residual += h elementwise (fp32 += bf16, n elements, n % 8 == 0, 16-byte aligned):
- * the add of the fused add + RMSNorm (videomamba.py:141-166; mamba-ssm rms_norm_fn's
- * x + residual) on its own, so a caller can issue it apart from the norm.  With this add done,
- * vm_add_norm_fwd(x = the fp32 residual, residual = NULL) gives bit for bit the out of
- * vm_add_norm_fwd(x = h, residual) (the same fp32 sums, the same reduction order).
- */
-int vm_residual_add_fwd(const void* h, int h_dtype, float* residual, long long n,
-                        vm_stream_t stream);
 
 /*
  * Final add + norm fused with the pooling front half.  Per batch row b, rows

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6: options.stream_post_add (the residual add issued after out_proj, in the scan's
 # phase; the next pre phase only normalises): tests, then the 1344-clip step with it on and
-# off, alternating in separate processes, then a kernel trace of each.
+# off, alternating in separate processes, then a kernel trace of each.  Ran at commit
+# 6ca05ae (the option and its kernels were reverted after it: DESIGN §7).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r06y}

@@ -1388,46 +1388,3 @@ def test_in_proj_conv_epilogue_is_bitwise_the_two_kernel_model(bsz):
             gv, gp = runner.run(x, temporal_pos_offset=0)
         assert torch.equal(gv, ev) and torch.equal(gp, ep)
     assert isinstance(model.layers[0].mixer, Mamba)
-
-
-@pytest.mark.parametrize("post_add", [True, False])
-def test_stream_post_add_runs_in_the_locked_split_and_keeps_the_bits(post_add):
-    """options.stream_post_add: in a phase-locked sub-batch forward every block but the last
-    adds its output into the residual right after its out_proj (vm_residual_add_fwd) and the
-    next block only normalises the residual; x_vis, x_pool and the states are bit-equal to the
-    one-stream forward, and the add runs (depth - 1) times per part and chunk (0 when off)."""
-    torch.manual_seed(11)
-    model = PretrainVideoMamba(img_size=32, patch_size=16, depth=4, embed_dim=192, channels=3,
-                               kernel_size=1, num_frames=4, pool_type="avg",
-                               fused_add_norm=True, rms_norm=True, residual_in_fp32=True)
-    model = model.to(DEV).to(torch.bfloat16).eval()
-    B = 6
-    x = torch.randn(B, 3, 4, 32, 32, device=DEV).to(torch.bfloat16)
-    calls = []
-    orig = K.residual_add
-
-    def counting(h, r):
-        calls.append(1)
-        return orig(h, r)
-
-    def run(parts):
-        st = model.allocate_state(B, dtype=torch.bfloat16, device=DEV)
-        outs = []
-        with options.override(batch_streams=parts, batch_stream_min_clips=2,
-                              batch_stream_min_work=0, batch_stream_lock=True,
-                              stream_post_add=post_add), torch.no_grad():
-            for off in (0, 2):
-                xv, xp, st = model(x[:, :, off:off + 2], ssm_state=st, temporal_pos_offset=off)
-                outs += [xv.clone(), xp.clone()]
-        torch.cuda.synchronize()
-        return outs + [t.clone() for pair in st for t in pair]
-
-    ref = run(1)
-    K.residual_add = counting
-    try:
-        got = run(2)
-    finally:
-        K.residual_add = orig
-    assert len(calls) == ((model.depth - 1) * 2 * 2 if post_add else 0)
-    for a, b in zip(ref, got):
-        assert torch.equal(a, b)

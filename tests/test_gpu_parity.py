@@ -1274,32 +1274,3 @@ def test_in_proj_conv_proj_rejects_unsupported_shapes():
     assert not K.in_proj_conv_proj_fits(576, 1, 3144, 1088, 68, 80, 64, 4, False)
     assert not K.in_proj_conv_proj_fits(640, 1, 3144, 1152, 68, 80, 64, 4, False)
 
-
-
-@pytest.mark.parametrize("rows,cols", [(1, 192), (37, 192), (301, 576), (64, 1024), (9, 384)])
-def test_residual_add_then_norm_is_bitwise_the_fused_add_norm(rows, cols):
-    """vm_residual_add_fwd (residual += h, fp32 += bf16) followed by vm_add_norm_fwd on the
-    fp32 residual alone (the fp32-input form of add_rms_bf16_kernel) — the split the locked
-    sub-batch forward uses (options.stream_post_add) — against the fused add + RMSNorm
-    (rms_norm_fn with residual, prenorm, residual_in_fp32; videomamba.py:141-166): the
-    residual and the normalised rows are bit-identical."""
-    g = torch.Generator(device=DEV).manual_seed(rows * 7 + cols)
-    h = (torch.randn(rows, cols, device=DEV, generator=g) * 3).to(torch.bfloat16)
-    res = torch.randn(rows, cols, device=DEV, generator=g) * 5
-    w = (torch.randn(cols, device=DEV, generator=g) * 0.2 + 1).to(torch.bfloat16)
-    y0, r0 = K.rms_norm_fn(h, w, None, residual=res.clone(), prenorm=True, residual_in_fp32=True,
-                           eps=1e-5)
-    r1 = K.residual_add(h, res.clone())
-    y1 = K._norm(r1, w, None, None, False, True, 1e-5, True,
-                 out=torch.empty(rows, cols, dtype=torch.bfloat16, device=DEV))
-    torch.cuda.synchronize()
-    assert torch.equal(r0, r1)
-    assert torch.equal(y0, y1)
-
-
-def test_residual_add_rejects_bad_operands():
-    h = torch.zeros(4, 192, device=DEV, dtype=torch.bfloat16)
-    with pytest.raises(ValueError):
-        K.residual_add(h, torch.zeros(4, 192, device=DEV, dtype=torch.bfloat16))
-    with pytest.raises(ValueError):
-        K.residual_add(h, torch.zeros(4, 96, device=DEV))

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 VM_DTYPE_F32 = 0
 VM_DTYPE_BF16 = 1
-ABI_VERSION = 15
+ABI_VERSION = 14
 
 _P = c_void_p
 _LL = c_longlong
@@ -96,7 +96,6 @@ _SIGNATURES = {
          _I, _I, _I, _I, _I,                      # out_len, batch, dim, seqlen, width
          _P, _LL, _P], _I),                       # workspace, bytes, stream
     "vm_in_proj_conv_proj_workspace_bytes": ([_I, _I, _I, _I], _LL),
-    "vm_residual_add_fwd": ([_P, _I, _P, _LL, _P], _I),
     "vm_in_proj_conv_proj_fits": ([_I, _I, _I, _I, _I, _I, _I, _I, _I], _I),
     "vm_conv_proj_cm_fwd": (
         [_P, _LL, _P, _P,                         # xz (row stride), conv weight / bias

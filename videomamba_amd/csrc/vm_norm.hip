@@ -60,19 +60,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base
 // (no early exit for the rows past the end: their buffers have 0-byte ranges, so every
 // access is a no-op, and the kernel-argument loads are not split by a branch into two
 // dependent rounds before the first global load)
-// X32: x is fp32 (the residual stream itself, already added to by vm_residual_add_fwd): the
-// same v, so the same sum of squares and outputs bit for bit
-template <int CPL, bool RES, bool RO, bool X32 = false>
+template <int CPL, bool RES, bool RO>
 __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
-  static_assert(!X32 || !RES, "fp32 x: the norm of an already added residual");
   const long long row0 = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool live = row0 < p.rows;
   const long long row = live ? row0 : 0;
   const int lane = threadIdx.x & 63;
   const long long base = row * p.cols;
   const int cb2 = live ? p.cols * 2 : 0, cb4 = live ? p.cols * 4 : 0;
-  const auto xr = X32 ? norm_row_rsrc(static_cast<const float*>(p.x) + base, cb4)
-                      : norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, cb2);
+  const auto xr = norm_row_rsrc(static_cast<const bf16_t*>(p.x) + base, cb2);
   const auto rr = norm_row_rsrc(RES ? static_cast<const float*>(p.res) + base : p.w, cb4);
   const auto wr = norm_row_rsrc(p.w, p.cols * 4);
   const auto orr = norm_row_rsrc(static_cast<bf16_t*>(p.out) + base, cb2);
@@ -87,13 +83,9 @@ __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
   v4f rq[CPL], wq[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    if constexpr (X32) {
-      rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(xr, off(j, 4), 0, 0));
-    } else {
-      const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
-      xq[j][0] = q[0];
-      xq[j][1] = q[1];
-    }
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(xr, off(j, 2), 0, 0);
+    xq[j][0] = q[0];
+    xq[j][1] = q[1];
     if constexpr (RES) rq[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rr, off(j, 4), 0, 0));
   }
 #pragma unroll
@@ -103,11 +95,6 @@ __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
   float v[CPL][4];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    if constexpr (X32) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[j][i] = rq[j][i];
-      continue;
-    }
     v[j][0] = __uint_as_float(xq[j][0] << 16); v[j][1] = __uint_as_float(xq[j][0] & 0xffff0000u);
     v[j][2] = __uint_as_float(xq[j][1] << 16); v[j][3] = __uint_as_float(xq[j][1] & 0xffff0000u);
     if constexpr (RES) {
@@ -758,15 +745,6 @@ extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual,
   const bool vec = cols % 4 == 0 && vmhost::aligned16(x) && vmhost::aligned16(out) &&
                    vmhost::aligned16(weight) && (!residual || vmhost::aligned16(residual)) &&
                    (!residual_out || vmhost::aligned16(residual_out));
-  if (vec && is_rms && !bias && x_dtype == VM_DTYPE_F32 && out_dtype == VM_DTYPE_BF16 &&
-      !residual && !residual_out && cols <= 256 * 4) {  // the norm of an added residual stream
-    const int cpl = (cols + 255) / 256;
-    if (cpl <= 1) hipLaunchKernelGGL((add_rms_bf16_kernel<1, false, false, true>), grid, dim3(256), 0, s, p);
-    else if (cpl <= 2) hipLaunchKernelGGL((add_rms_bf16_kernel<2, false, false, true>), grid, dim3(256), 0, s, p);
-    else if (cpl <= 3) hipLaunchKernelGGL((add_rms_bf16_kernel<3, false, false, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((add_rms_bf16_kernel<4, false, false, true>), grid, dim3(256), 0, s, p);
-    return vmhost::launch_status("vm_add_norm_fwd");
-  }
   if (vec && is_rms && !bias && x_dtype == VM_DTYPE_BF16 && out_dtype == VM_DTYPE_BF16 &&
       (!residual || res_dtype == VM_DTYPE_F32) && (!residual_out || res_out_dtype == VM_DTYPE_F32) &&
       cols <= 256 * 4) {
@@ -801,43 +779,4 @@ extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual,
   else if (vpl <= 16) hipLaunchKernelGGL(add_norm_kernel<16>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(add_norm_kernel<32>, grid, dim3(256), 0, s, p);
   return vmhost::launch_status("vm_add_norm_fwd");
-}
-
-// residual += h (fp32 += bf16), 8 elements per thread: the residual add of the fused add +
-// RMSNorm (videomamba.py:141-166, mamba-ssm rms_norm_fn's x + residual) run on its own, so
-// the sub-batch forward can issue it in the scan's phase and leave the norm (fp32 x, above)
-// to the next layer's in_proj phase.  The same fp32 addition, so the same residual bits.
-__global__ __launch_bounds__(256) void residual_add_bf16_kernel(const bf16_t* __restrict__ h,
-                                                                float* __restrict__ res,
-                                                                long long n8) {
-  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= n8) return;
-  const uint4 hv = reinterpret_cast<const uint4*>(h)[i];
-  float4* r = reinterpret_cast<float4*>(res) + 2 * i;
-  float4 a = r[0], b = r[1];
-  a.x += __uint_as_float(hv.x << 16); a.y += __uint_as_float(hv.x & 0xffff0000u);
-  a.z += __uint_as_float(hv.y << 16); a.w += __uint_as_float(hv.y & 0xffff0000u);
-  b.x += __uint_as_float(hv.z << 16); b.y += __uint_as_float(hv.z & 0xffff0000u);
-  b.z += __uint_as_float(hv.w << 16); b.w += __uint_as_float(hv.w & 0xffff0000u);
-  r[0] = a;
-  r[1] = b;
-}
-
-extern "C" int vm_residual_add_fwd(const void* h, int h_dtype, float* residual, long long n,
-                                   vm_stream_t stream) {
-  if (!h || !residual) {
-    vmhost::set_error("vm_residual_add_fwd: null required pointer");
-    return VM_E_INVALID;
-  }
-  if (h_dtype != VM_DTYPE_BF16 || n < 0 || n % 8 || !vmhost::aligned16(h) ||
-      !vmhost::aligned16(residual)) {
-    vmhost::set_error("vm_residual_add_fwd: bf16 h, fp32 residual, n %% 8 == 0, 16-byte aligned");
-    return VM_E_INVALID;
-  }
-  if (n == 0) return VM_OK;
-  const long long n8 = n / 8;
-  hipLaunchKernelGGL(residual_add_bf16_kernel, dim3(static_cast<unsigned>((n8 + 255) / 256)),
-                     dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const bf16_t*>(h), residual, n8);
-  return vmhost::launch_status("vm_residual_add_fwd");
 }

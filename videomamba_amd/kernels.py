@@ -482,20 +482,6 @@ def add_norm_raw(x, residual, w32, b32, out, residual_out, rows, cols, eps, is_r
     _lib.check(rc, "vm_add_norm_fwd")
 
 
-def residual_add(h: Tensor, residual: Tensor) -> Tensor:
-    """residual += h in place (fp32 += bf16, ``vm_residual_add_fwd``): the add of the fused
-    add + RMSNorm on its own; :func:`_norm` on the fp32 residual alone then gives the bits the
-    fused call would have.  Returns ``residual``."""
-    require_gpu(h, residual, what="residual_add")
-    if (h.dtype != torch.bfloat16 or residual.dtype != torch.float32 or h.shape != residual.shape
-            or not h.is_contiguous() or not residual.is_contiguous()):
-        raise ValueError("residual_add: contiguous bf16 h and fp32 residual of one shape")
-    rc = _lib.load().vm_residual_add_fwd(_p(h), dtype_code(h.dtype), _p(residual), h.numel(),
-                                         _stream(h))
-    _lib.check(rc, "vm_residual_add_fwd")
-    return residual
-
-
 LINEAR_FORMS = {"auto": 0, "dma": 1, "persistent": 2}
 
 

@@ -76,13 +76,6 @@ documented options object; tests and sweeps change them with :func:`override`.
                      672 clips.  C2 (Ti-8f, 512 clips) on one stream: 13.65-13.67 M
                      video-tokens/s against 13.51-13.53 M as two locked streams
                      (profiles/r05zzw_c2_streams_ab.jsonl).
-    stream_post_add  True (default): in a phase-locked sub-batch forward, each block's
-                     residual add (residual += mixer output, fp32) is issued right after its
-                     out_proj, in the scan's phase, and the next block's pre phase only
-                     normalises the residual (``vm_residual_add_fwd`` + ``vm_add_norm_fwd`` on
-                     the fp32 residual): the same sums, so the same bits.  It moves 12 of the
-                     add + norm's 15 GB per 672-clip half-layer out of the pre phase, the one
-                     the lock serialises.
     in_proj_z_stream False (default): True makes the mixer at streaming batches (at most
                      ``in_proj_split_clips`` clips, default 8) run in_proj as two launches,
                      the x half on the current stream and the z half (read only by the scan's
@@ -133,7 +126,6 @@ class Options:
     fuse_out_norm: bool = False
     batch_streams: int = 2
     batch_stream_lock: bool = True
-    stream_post_add: bool = True
     in_proj_z_stream: bool = False
     in_proj_split_clips: int = 8
     in_proj_conv_clips: int = 2

@@ -136,27 +136,17 @@ class Block(nn.Module):
         hidden = self.mixer(hidden, inference_params=inference_params, ssm_state=ssm_state)
         return hidden, residual
 
-    def forward_padded(self, hidden: Optional[Tensor], residual: Optional[Tensor], seqlen: int,
+    def forward_padded(self, hidden: Tensor, residual: Optional[Tensor], seqlen: int,
                        state=None, ssm_state=None, return_state: bool = False, conv_out=None,
-                       pre: Optional["NextNorm"] = None, next_norm: Optional["NextNorm"] = None,
-                       post_add: bool = False):
+                       pre: Optional["NextNorm"] = None, next_norm: Optional["NextNorm"] = None):
         """Model-internal: same as ``forward`` on the padded (B, Lp, C) buffers.  ``pre``: the
         previous block's out_proj already ran this block's add + norm (``pre.done``): use its
         normalised rows and updated residual.  ``next_norm``: offer the NEXT block's norm to
-        this block's out_proj (vm_linear_add_norm_fwd).  ``hidden`` None: the previous block
-        already added its output into ``residual`` (its ``post_add``), so only the norm runs.
-        ``post_add``: add this block's output into ``residual`` right after the mixer (the
-        scan's phase of a locked sub-batch forward, options.stream_post_add) and return None
-        for it."""
+        this block's out_proj (vm_linear_add_norm_fwd)."""
         idx = getattr(self, "layer_idx", None)
         _phase.pre_start(idx)  # sub-batch streams: after the previous part's pre phase
         if pre is not None and pre.done:
             hn, residual = pre.hn, pre.residual
-        elif hidden is None:  # residual already holds residual + the previous output
-            nw = self.norm.weight
-            hn = K._norm(residual, nw, self.norm.bias, None, False, True, self.norm.eps, True,
-                         out=torch.empty(residual.shape, dtype=torch.bfloat16, device=residual.device),
-                         owner=self.norm)
         else:
             hn, residual = self._add_norm(hidden, residual, inplace=True)
         if next_norm is not None:
@@ -166,11 +156,9 @@ class Block(nn.Module):
                                         return_state=return_state, conv_out=conv_out,
                                         next_norm=next_norm)
         _phase.pre_done(idx)  # (the token-major mixer marked it after conv_proj already)
-        out = res[0] if return_state else res
-        if post_add:
-            K.residual_add(out, residual)
-            out = None
-        return out, residual, (res[1] if return_state else None)
+        if return_state:
+            return res[0], residual, res[1]
+        return res, residual, None
 
     def allocate_inference_cache(self, batch_size: int, max_seqlen: int, dtype=None, **kwargs):
         return self.mixer.allocate_inference_cache(batch_size, max_seqlen, dtype=dtype, **kwargs)
@@ -525,10 +513,8 @@ class PretrainVideoMamba(nn.Module):
         new_states = None
         tuple_out = False
         fuse = self._fuse_out_norm_ok(h)
-        post = not fuse and self._post_add_ok(h)
         pending = None
         for idx, layer in enumerate(self.layers):
-            pa = post and idx + 1 < len(self.layers)
             nxt = None
             if fuse and idx + 1 < len(self.layers):
                 nn_ = self.layers[idx + 1].norm
@@ -545,31 +531,14 @@ class PretrainVideoMamba(nn.Module):
                 h, residual, layer_state = layer.forward_padded(
                     h, residual, L, state=tuple(layer_state), return_state=True,
                     conv_out=None if conv_out is None else conv_out[idx], pre=pending,
-                    next_norm=nxt, post_add=pa)
+                    next_norm=nxt)
             else:
                 h, residual, _ = layer.forward_padded(h, residual, L, ssm_state=layer_state,
-                                                      pre=pending, next_norm=nxt, post_add=pa)
+                                                      pre=pending, next_norm=nxt)
             if new_states is not None:
                 new_states[idx] = layer_state
             pending = nxt
         return h, residual, new_states, tuple_out
-
-    def _post_add_ok(self, h: Tensor) -> bool:
-        """Inside a phase-locked sub-batch forward (this host thread is bound to a part),
-        each block's residual add may move to right after its out_proj
-        (``options.stream_post_add``): every block uses the fused RMSNorm (no bias) with an
-        fp32 residual on bf16 activations and no stochastic depth is active, so the next
-        block's norm of the added residual alone gives the fused call's bits."""
-        if not options.get().stream_post_add or _phase.current()[0] is None:
-            return False
-        if h.dtype != torch.bfloat16 or self.embed_dim % 8 or self.embed_dim > 1024:
-            return False
-        for layer in self.layers:
-            if not (layer.fused_add_norm and layer.residual_in_fp32 and _norm_kind(layer.norm)
-                    and getattr(layer.norm, "bias", None) is None
-                    and (isinstance(layer.drop_path, nn.Identity) or not layer.training)):
-                return False
-        return True
 
     def _fuse_out_norm_ok(self, h: Tensor) -> bool:
         """Every block's add + norm after the first may run inside the previous block's
