@@ -93,6 +93,9 @@ def _args():
                     help="options.scan_dt_proj: dt_proj inside the scan at chip-filling batches")
     ap.add_argument("--batch-streams", type=int, default=0,
                     help="options.batch_streams (sub-batch HIP streams per forward; 0: default)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path with several ranks on one GPU)")
     ap.add_argument("--full-sequence", action="store_true",
                     help="stateless full-sequence forward (C2) instead of a stateful chunk")
     a = ap.parse_args()
@@ -230,15 +233,20 @@ def scan_roofline(batch, reps, device, layout="tm", dtp=False):
 
 # the committed rocprofv3 --kernel-trace --stats summary of a default bench command, whose
 # scan launches all ran inside the two-stream step (scripts/round_evidence.sh PART=1)
-IN_STEP_TRACES = ("profiles/r06v_bench_kernel_stats.csv", "profiles/r06j_bench_kernel_stats.csv",
-                  "profiles/r05zzp_bench_kernel_stats.csv")
+# (each a default C3 bench at 1344 clips: 672-clip scan launches)
+IN_STEP_TRACES = (("profiles/r06v_bench_kernel_stats.csv", 672),
+                  ("profiles/r06j_bench_kernel_stats.csv", 672),
+                  ("profiles/r05zzp_bench_kernel_stats.csv", 672))
 
 
-def _trace_in_step(algo, kname="scan_seq_dtp_kernel"):
+def _trace_in_step(algo, batch, kname="scan_seq_dtp_kernel"):
     """The scan's average launch in the newest committed bench trace (its own begin-end
-    times) and the HBM fraction on the same bytes; None when no trace is committed."""
+    times) and the HBM fraction on the same bytes; None when no trace of launches of this
+    many clips is committed (another --batch prices nothing against it)."""
     import csv
-    for rel in IN_STEP_TRACES:
+    for rel, tb in IN_STEP_TRACES:
+        if tb != batch:
+            continue
         path = os.path.join(ROOT, rel)
         if not os.path.exists(path):
             continue
@@ -273,7 +281,7 @@ def scan_in_step(step, L=3137, D=1152, N=16):
     med = statistics.median(us)
     mean = sum(us) / len(us)
     return {"batch_per_launch": batch,
-            "trace": _trace_in_step(algo),
+            "trace": _trace_in_step(algo, batch),
             "events": {"launches": len(us), "median_us": round(med, 2), "mean_us": round(mean, 2),
                        "min_us": round(us[0], 2), "max_us": round(us[-1], 2),
                        "frac": round(algo / (med * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
@@ -663,10 +671,16 @@ def main():
     from videomamba_amd.sharding import dist_env, shard_range
 
     rank, local, world = dist_env()
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one rank per GPU (local rank = device); a gloo rehearsal on a box with fewer GPUs than
+    # ranks shares them round-robin
+    dev_index = local if args.dist_backend == "nccl" else local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     from videomamba_amd import options
     from videomamba_amd.videomamba import PretrainVideoMamba

@@ -235,13 +235,14 @@ def test_in_step_scan_fraction_reproduces_from_committed_trace():
     import bench
     algo = 672 * 1152 * 3137 * 4 * 2 + 2 * 672 * 16 * 3137 * 2 + 4 * 1152 * 16 + 8 * 1152 \
         + 2 * 672 * 1152 * 16 * 2
-    tr = bench._trace_in_step(algo)
-    assert tr is not None and tr["source"] == bench.IN_STEP_TRACES[0]
+    tr = bench._trace_in_step(algo, 672)
+    assert tr is not None and tr["source"] == bench.IN_STEP_TRACES[0][0]
+    assert bench._trace_in_step(algo, 112) is None  # no committed trace of 112-clip launches
     out = subprocess.run([sys.executable, os.path.join(root, "scripts", "traffic_summary.py"),
                           "in-step", os.path.join(root, tr["source"]), "672"],
                          capture_output=True, text=True, check=True).stdout
     rec = json.loads(out)
     assert rec["bytes_per_launch"] == algo
     assert abs(rec["trace_frac"] - tr["frac"]) < 1e-4 and abs(rec["trace_avg_us"] - tr["avg_us"]) < 0.01
-    line = json.load(open(os.path.join(root, "profiles", "r06j_bench.json")))
+    line = json.load(open(os.path.join(root, "profiles", "r06v_bench.json")))
     assert line["roofline"]["frac"] > tr["frac"]

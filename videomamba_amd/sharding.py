@@ -45,7 +45,9 @@ def max_over_ranks(value: float, device: torch.device) -> float:
     """Max of a host scalar over all ranks (identity without a process group)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    # (gloo reduces host tensors: the multi-rank rehearsal on one GPU, and the CPU tests)
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
