@@ -51,7 +51,7 @@ print(json.dumps({"cus": cus}), flush=True)
 with torch.no_grad():
     ref = None
     for mode, ss in modes.items():
-        V._SIDE_STREAMS[key] = ss
+        V._SIDE_STREAMS.by_device = {key: ss}  # this thread's side streams
         fresh = model.allocate_state(B, dtype=torch.bfloat16, device=dev)
         out = model(x, ssm_state=fresh, temporal_pos_offset=0)[1].float()
         del fresh
@@ -61,7 +61,7 @@ with torch.no_grad():
               flush=True)
     for r in range(2):
         for mode, ss in modes.items():
-            V._SIDE_STREAMS[key] = ss
+            V._SIDE_STREAMS.by_device = {key: ss}  # this thread's side streams
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(3):

@@ -25,11 +25,11 @@ lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "prior
 prio = [torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev, priority=0)]
 with torch.no_grad():
     for mode, ss in (("plain", plain), ("prio", prio)):
-        V._SIDE_STREAMS[key] = ss
+        V._SIDE_STREAMS.by_device = {key: ss}  # this thread's side streams
         model(x, ssm_state=st, temporal_pos_offset=0)
     for r in range(3):
         for mode, ss in (("plain", plain), ("prio", prio)):
-            V._SIDE_STREAMS[key] = ss
+            V._SIDE_STREAMS.by_device = {key: ss}  # this thread's side streams
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(3):

@@ -1388,3 +1388,85 @@ def test_in_proj_conv_epilogue_is_bitwise_the_two_kernel_model(bsz):
             gv, gp = runner.run(x, temporal_pos_offset=0)
         assert torch.equal(gv, ev) and torch.equal(gp, ep)
     assert isinstance(model.layers[0].mixer, Mamba)
+
+
+def test_concurrent_callers_are_bitwise_their_serial_runs():
+    """callers on several host threads at once.  Two models each run a
+    forward split into two phase-locked sub-batch streams (so each caller thread starts its
+    own issue thread) over two stateful chunks, each caller on a stream of its own, while a
+    third thread captures and replays a StreamingChunkGraph of a third model (its capture's
+    scratch / sync / counter overrides are per thread, kernels._Slot, and the capture is
+    thread-local, graphs.py).  Every output and carried state is bit-equal to the same work
+    run alone, one caller after another; three concurrent rounds, the threads released
+    together by a barrier."""
+    import threading
+    from videomamba_amd.graphs import StreamingChunkGraph
+
+    def small(seed):
+        torch.manual_seed(seed)
+        return PretrainVideoMamba(img_size=32, patch_size=16, depth=3, embed_dim=192, channels=3,
+                                  kernel_size=1, num_frames=4, pool_type="avg",
+                                  fused_add_norm=True, rms_norm=True,
+                                  residual_in_fp32=True).to(DEV).to(torch.bfloat16).eval()
+
+    models = [small(11), small(12), small(13)]
+    g = torch.Generator(device=DEV).manual_seed(14)
+    xs = [torch.randn(b, 3, 4, 32, 32, device=DEV, generator=g).to(torch.bfloat16)
+          for b in (7, 6, 1)]
+
+    def split_job(i):
+        model, x = models[i], xs[i]
+        assert model._stream_parts(x[:, :, :2], None, None, None) == 2
+        st = model.allocate_state(x.shape[0], dtype=torch.bfloat16, device=DEV)
+        outs = []
+        for off in (0, 2):
+            xv, xp, st = model(x[:, :, off:off + 2], ssm_state=st, temporal_pos_offset=off)
+            outs += [xv.clone(), xp.clone()] + [t.clone() for c in st for t in c]
+        return outs
+
+    def graph_job(i):
+        runner = StreamingChunkGraph(models[i], batch=1, frames=2, height=32, width=32)
+        outs = []
+        for off in (0, 2):
+            res = runner.run(xs[i][:, :, off:off + 2], temporal_pos_offset=off)
+            outs += [t.clone() for t in (res if isinstance(res, tuple) else (res,))]
+        outs += [t.clone() for c in runner.state for t in c]
+        return outs
+
+    jobs = [split_job, split_job, graph_job]
+
+    def on_stream(i, barrier=None):
+        with torch.no_grad(), torch.cuda.stream(torch.cuda.Stream(DEV)):
+            if barrier is not None:
+                barrier.wait()
+            outs = jobs[i](i)
+            torch.cuda.current_stream().synchronize()
+        return outs
+
+    with options.override(batch_streams=2, batch_stream_min_clips=2, batch_stream_min_work=0,
+                          batch_stream_lock=True):
+        serial = [on_stream(i) for i in range(3)]
+        for _ in range(3):
+            results, errors = [None] * 3, []
+            barrier = threading.Barrier(3)
+
+            def worker(i):
+                try:
+                    results[i] = on_stream(i, barrier)
+                except BaseException as e:  # noqa: BLE001 - re-raised on the test thread
+                    errors.append(e)
+                    barrier.abort()
+
+            threads = [threading.Thread(target=worker, args=(i,)) for i in range(3)]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join(timeout=120)
+            assert not any(t.is_alive() for t in threads)
+            if errors:
+                raise errors[0]
+            for i in range(3):
+                assert len(results[i]) == len(serial[i])
+                for a, b in zip(results[i], serial[i]):
+                    assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())
+    K.check_scan_sync()

@@ -246,16 +246,26 @@ class PatchEmbed(nn.Module):
 
 
 # ----------------------------------------------------------------------------- encoder
-_SIDE_STREAMS: Dict[Any, List[torch.cuda.Stream]] = {}
+class _ThreadStreams(threading.local):
+    by_device: Optional[Dict[Any, List[torch.cuda.Stream]]] = None
+
+
+_SIDE_STREAMS = _ThreadStreams()
 
 
 def _side_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
-    """n persistent HIP streams of ``device`` for sub-batch forwards (created once).  The
-    first runs at high priority: its kernels dispatch first, so the halves drift apart and
-    one's scan meets the other's memory-bound kernels more often (B = 896: 825-831 vs
-    838-843 ms per step, profiles/r05zn_stream_priority.jsonl)."""
+    """n persistent HIP streams of ``device`` for sub-batch forwards, created once per
+    calling host thread.  Per thread because two callers' split forwards on shared streams
+    could deadlock the device: each part waits on its partner's phase events, and with both
+    callers' parts interleaved on the same two streams a wait of one caller can sit behind
+    the other caller's wait on work queued after it.  The first runs at high priority: its
+    kernels dispatch first, so the halves drift apart and one's scan meets the other's
+    memory-bound kernels more often (B = 896: 825-831 vs 838-843 ms per step,
+    profiles/r05zn_stream_priority.jsonl)."""
+    if _SIDE_STREAMS.by_device is None:
+        _SIDE_STREAMS.by_device = {}
     key = (device.type, device.index)
-    have = _SIDE_STREAMS.setdefault(key, [])
+    have = _SIDE_STREAMS.by_device.setdefault(key, [])
     while len(have) < n:
         have.append(torch.cuda.Stream(device, priority=-1 if not have else 0))
     return have[:n]
