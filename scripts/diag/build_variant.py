@@ -97,6 +97,34 @@ VARIANTS = {
                    "            b0 = tg_conv_silu(b0, p2, wb + 0.002f);\n"
                    "            b1 = tg_conv_silu(b1, p3, wb + 0.003f);\n"
                    "          }\n")],
+    # B = 1 kernel boundaries: in_proj + conv's u / z / x_proj-partial stores write-through
+    # (sc1), so the ~22 MB they leave dirty in L2 drains during the kernel instead of at the
+    # boundary (MI355X_MICROARCH.md "boundary": + bytes / 6 TB/s)
+    "wt_ic": [("vm_inproj_conv.hip",
+               "        *reinterpret_cast<uint4*>(q.z + (long long)gm * q.ldz + (n0 - p.dim) + cq * 8) =\n"
+               "            *reinterpret_cast<const uint4*>(&sO[row * kIcPitch + cq * 8]);",
+               "        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const int __attribute__((ext_vector_type(4)))*>(&sO[row * kIcPitch + cq * 8]),\n"
+               "            __builtin_amdgcn_make_buffer_rsrc(q.z, 0, 0x7ffffff0, 0x00020000), static_cast<int>(((long long)gm * q.ldz + (n0 - p.dim) + cq * 8) * 2), 0, 16);"),
+              ("vm_inproj_conv.hip",
+               "    if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c) = upk[i];",
+               "    if (tok < q.ntok) __hip_atomic_store(reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c), upk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);"),
+              ("vm_inproj_conv.hip",
+               "        *reinterpret_cast<float4*>(q.part + ((long long)sp * q.ntok + tok) * q.ep + 4 * qd) =\n"
+               "            *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd]);",
+               "        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const int __attribute__((ext_vector_type(4)))*>(&sP[r * kPP + 4 * qd]),\n"
+               "            __builtin_amdgcn_make_buffer_rsrc(q.part, 0, 0x7ffffff0, 0x00020000), static_cast<int>((((long long)sp * q.ntok + tok) * q.ep + 4 * qd) * 4), 0, 16);")],
+    # the same for add + RMSNorm's hn / residual stores, the scans' y stores and the
+    # 128-row GEMM's output stores (wt_all = all four kernels of the B = 1 layer)
+    "wt_rest": [("vm_norm.hip", "    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);",
+                 "    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 16);"),
+                ("vm_norm.hip", "      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);",
+                 "      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 16);"),
+                ("vm_scan_seq.hip", "    __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, 0);",
+                 "    __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, 16);"),
+                ("vm_gemm.hip", "        *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) = v;",
+                 "        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4w;\n"
+                 "        __builtin_amdgcn_raw_buffer_store_b128(v4w{(int)v.x, (int)v.y, (int)v.z, (int)v.w},\n"
+                 "            __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7ffffff0, 0x00020000), static_cast<int>(((long long)gm * p.ldo + gn) * 2), 0, 16);")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],
@@ -509,6 +537,9 @@ def build(name, rev=None):
     os.makedirs(out, exist_ok=True)
     subprocess.check_call(["make", "-C", work, "-j8", f"OUT={out}/libvideomamba_hip.so",
                            f"BUILD={os.path.join(ROOT, 'build', 'var', name, 'obj')}"])
+
+
+VARIANTS["wt_all"] = VARIANTS["wt_ic"] + VARIANTS["wt_rest"]
 
 
 if __name__ == "__main__":
