@@ -125,6 +125,12 @@ VARIANTS = {
                  "        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4w;\n"
                  "        __builtin_amdgcn_raw_buffer_store_b128(v4w{(int)v.x, (int)v.y, (int)v.z, (int)v.w},\n"
                  "            __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7ffffff0, 0x00020000), static_cast<int>(((long long)gm * p.ldo + gn) * 2), 0, 16);")],
+    # x_dbl reduce at B = 1: each block sums the tokens of the row tiles in_proj + conv ran on
+    # its own XCD, so the split partials it loads sit in that XCD's L2 (same bits)
+    "xr_xcd": [("vm_inproj_conv.hip", "// x_dbl = bf16(sum of the split partials in split order) — xdbl_dt_tm_kernel's sum (from\n// 0, split 0 first, fp32) without its dt phase, one thread per (token, 4 columns) so the\n// whole reduction is one round of loads (that kernel's 64-token tiles take two dependent\n// rounds on a 50-workgroup grid at B = 1).  dt == NULL only (the scan computes dt).\ntemplate <int NSPL>\n__global__ __launch_bounds__(256) void xdbl_reduce_kernel(const InConvParams q) {\n  const ConvProjTmArgs& p = q.a;\n  const int q4 = (p.e + 3) >> 2;\n  const int it = blockIdx.x * 256 + threadIdx.x;\n  if (it >= q.ntok * q4) return;\n  const int t = it / q4, e0 = (it - t * q4) * 4;",
+                "// The token range [lo, hi) of the row tiles whose split 0 ran on XCD x in inproj_conv_kernel\n// (its XCD-contiguous numbering of the x tiles: XCD x took logical tiles [start, start + count))\n__device__ __forceinline__ void ic_xcd_tokens(const InConvParams& q, int x, int& lo, int& hi) {\n  const int nwg = q.nxr * q.nsplit, qq = nwg >> 3, rr = nwg & 7;\n  const int start = x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;\n  const int end = start + qq + (x < rr ? 1 : 0);\n  const int rt_a = (start + q.nsplit - 1) / q.nsplit, rt_b = (end + q.nsplit - 1) / q.nsplit;\n  lo = min(rt_a * kIcOut, q.ntok);\n  hi = min(rt_b * kIcOut, q.ntok);\n}\n\n// x_dbl = bf16(sum of the split partials in split order) — xdbl_dt_tm_kernel's sum (from\n// 0, split 0 first, fp32) without its dt phase, one thread per (token, 4 columns) so the\n// whole reduction is one round of loads (that kernel's 64-token tiles take two dependent\n// rounds on a 50-workgroup grid at B = 1).  dt == NULL only (the scan computes dt).  Block b\n// runs on XCD b % 8 (round-robin dispatch; placement is a speed choice only) and sums the\n// tokens of the row tiles inproj_conv_kernel ran there, so its partial loads hit that XCD's L2.\ntemplate <int NSPL>\n__global__ __launch_bounds__(256) void xdbl_reduce_kernel(const InConvParams q) {\n  const ConvProjTmArgs& p = q.a;\n  const int q4 = (p.e + 3) >> 2;\n  int lo, hi;\n  ic_xcd_tokens(q, blockIdx.x & 7, lo, hi);\n  const int it = lo * q4 + (blockIdx.x >> 3) * 256 + threadIdx.x;\n  if (it >= hi * q4) return;\n  const int t = it / q4, e0 = (it - t * q4) * 4;"),
+               ("vm_inproj_conv.hip", '    const unsigned blocks = static_cast<unsigned>((ntok * ((e + 3) / 4) + 255) / 256);',
+                "    // 8 x (the most tokens any XCD's row tiles hold) threads, in 256-thread blocks\n    int most = 0;\n    {\n      const int nwg = q.nxr * q.nsplit, qq = nwg >> 3, rr = nwg & 7;\n      for (int x = 0; x < 8; ++x) {\n        const int start = x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;\n        const int end = start + qq + (x < rr ? 1 : 0);\n        const long long lo = std::min<long long>((start + q.nsplit - 1) / q.nsplit * (long long)kIcOut, ntok);\n        const long long hi = std::min<long long>((end + q.nsplit - 1) / q.nsplit * (long long)kIcOut, ntok);\n        most = std::max(most, static_cast<int>(hi - lo));\n      }\n    }\n    const unsigned blocks = 8u * static_cast<unsigned>((most * ((e + 3) / 4) + 255) / 256);")],
     # small-batch conv_proj: the two-launch split-K form instead of the fused kernel
     "cp_splitk": [("vm_conv_proj.hip", "    if (conv_proj_fused_ok(a)) conv_proj_fused_launch(a, st);",
                    "    if (false) conv_proj_fused_launch(a, st);")],
