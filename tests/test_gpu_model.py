@@ -1393,12 +1393,15 @@ def test_in_proj_conv_epilogue_is_bitwise_the_two_kernel_model(bsz):
 def test_concurrent_callers_are_bitwise_their_serial_runs():
     """callers on several host threads at once.  Two models each run a
     forward split into two phase-locked sub-batch streams (so each caller thread starts its
-    own issue thread) over two stateful chunks, each caller on a stream of its own, while a
-    third thread captures and replays a StreamingChunkGraph of a third model (its capture's
-    scratch / sync / counter overrides are per thread, kernels._Slot, and the capture is
-    thread-local, graphs.py).  Every output and carried state is bit-equal to the same work
+    own issue thread, on its own side streams: videomamba._side_streams) over two stateful
+    chunks, each caller on a stream of its own, while a third thread replays a third model's
+    StreamingChunkGraph over two chunks (its scratch / sync / counter overrides are per
+    thread, kernels._Slot).  Every output and carried state is bit-equal to the same work
     run alone, one caller after another; three concurrent rounds, the threads released
-    together by a barrier."""
+    together by a barrier.  The runner's graphs are captured before the threads start: a
+    capture must not overlap other threads' GPU work (the default, global capture mode
+    refuses their unsafe calls; work they put on a pooled stream that aliases the capture
+    stream would be captured)."""
     import threading
     from videomamba_amd.graphs import StreamingChunkGraph
 
@@ -1413,6 +1416,7 @@ def test_concurrent_callers_are_bitwise_their_serial_runs():
     g = torch.Generator(device=DEV).manual_seed(14)
     xs = [torch.randn(b, 3, 4, 32, 32, device=DEV, generator=g).to(torch.bfloat16)
           for b in (7, 6, 1)]
+    runner = StreamingChunkGraph(models[2], batch=1, frames=2, height=32, width=32)
 
     def split_job(i):
         model, x = models[i], xs[i]
@@ -1425,7 +1429,6 @@ def test_concurrent_callers_are_bitwise_their_serial_runs():
         return outs
 
     def graph_job(i):
-        runner = StreamingChunkGraph(models[i], batch=1, frames=2, height=32, width=32)
         outs = []
         for off in (0, 2):
             res = runner.run(xs[i][:, :, off:off + 2], temporal_pos_offset=off)
@@ -1445,8 +1448,11 @@ def test_concurrent_callers_are_bitwise_their_serial_runs():
 
     with options.override(batch_streams=2, batch_stream_min_clips=2, batch_stream_min_work=0,
                           batch_stream_lock=True):
-        serial = [on_stream(i) for i in range(3)]
+        serial = [on_stream(i) for i in range(3)]  # the runner captures both chunk kinds here
+        assert runner._cur == 0 and (True, 0) in runner._graphs and (False, 1) in runner._graphs
         for _ in range(3):
+            runner.reset_state()
+            torch.cuda.synchronize()
             results, errors = [None] * 3, []
             barrier = threading.Barrier(3)
 
@@ -1463,10 +1469,13 @@ def test_concurrent_callers_are_bitwise_their_serial_runs():
             for t in threads:
                 t.join(timeout=120)
             assert not any(t.is_alive() for t in threads)
+            torch.cuda.synchronize()
             if errors:
                 raise errors[0]
+            assert len(runner._graphs) == 2  # replays only: nothing captured beside the threads
             for i in range(3):
                 assert len(results[i]) == len(serial[i])
                 for a, b in zip(results[i], serial[i]):
                     assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())
+    torch.cuda.synchronize()
     K.check_scan_sync()

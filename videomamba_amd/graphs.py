@@ -202,10 +202,7 @@ class StreamingChunkGraph:
                 self._body(has_cls, parity)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        # thread-local capture: callers on other host threads keep issuing (and allocating)
-        # while this thread captures; what the capture uses comes from per-thread slots
-        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"), \
-                K.scratch_override(ws), \
+        with torch.no_grad(), torch.cuda.graph(g, pool=self._pool), K.scratch_override(ws), \
                 K.sync_override(self._sync), K.counter_override(self._cnt):
             outs = self._body(has_cls, parity)
         self._pool = g.pool()
