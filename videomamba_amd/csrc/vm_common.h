@@ -85,6 +85,14 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x));
 __device__ __forceinline__ float softplus(float x) { return x <= 20.0f ? log1pf(__expf(x)) : x; }
 
 constexpr float kLog2e = 1.4426950408889634f;
+// Store policy of the streaming-chunk kernels (in_proj + conv, the chunked scan's y, the
+// 128-row GEMM, add + RMSNorm up to kSmallStoreRows rows): sc1, i.e. written through to
+// memory as they go.  A kernel that ends with B bytes dirty in L2 pays about B / 6 TB/s at
+// the next dependent boundary (MI355X_MICROARCH.md "boundary"); a B = 1 layer leaves ~40 MB
+// so, ~7 us.  Written through, they drain while the kernel runs: B = 1 M-16f chunk replay
+// 2.28-2.34 -> 2.17-2.19 ms (profiles/r06ah_b1_xr_xcd_wt_ab.txt; product build r06ai_b1_wt_ab.txt: 2.47-2.49 -> 2.37 ms run()).  Values are unchanged.
+constexpr int kSmallStoreWT = 16;
+constexpr long long kSmallStoreRows = 32768;
 constexpr float kLn2f = 0.6931471805599453f;
 
 // softplus / silu from the hardware exp2 / log2 / rcp.  softplus = ln2*log2(1 + 2^(x/ln2))

@@ -241,6 +241,11 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
   constexpr int kPieces = BM * BN / 8;
   const auto hr = __builtin_amdgcn_make_buffer_rsrc(
       p.out, 0, static_cast<int>((long long)p.m * p.ldo * 2), 0x00020000);
+  // this tile's rows (BM * ldo * 2 bytes at most: no 31-bit offset limit on the whole output)
+  const auto tr = __builtin_amdgcn_make_buffer_rsrc(
+      p.out + (long long)m0 * p.ldo, 0,
+      static_cast<int>(min(static_cast<long long>(p.m - m0), static_cast<long long>(BM)) * p.ldo * 2),
+      0x00020000);
 #pragma unroll
   for (int i = 0; i < (kPieces + NT - 1) / NT; ++i) {
     const int pc = tid + NT * i;
@@ -253,8 +258,10 @@ __global__ __launch_bounds__(128 * NWM) void linear_dma_kernel(const LinParams p
         typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
         __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, hr,
                                                (gm * static_cast<int>(p.ldo) + gn) * 2, 0, kSC1);
-      } else {
-        *reinterpret_cast<uint4*>(p.out + (long long)gm * p.ldo + gn) = v;
+      } else {  // write-through (sc1): see kSmallStoreWT
+        typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
+        __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, tr,
+                                               (row * static_cast<int>(p.ldo) + gn) * 2, 0, kSmallStoreWT);
       }
     }
   }

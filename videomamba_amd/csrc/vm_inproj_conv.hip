@@ -32,6 +32,7 @@ namespace vm {
 
 typedef __attribute__((__vector_size__(8 * sizeof(short)))) short ic_bf16x8;
 typedef __attribute__((__vector_size__(4 * sizeof(float)))) float ic_f32x4;
+typedef __attribute__((__vector_size__(4 * sizeof(int)))) int ic_i32x4;
 
 struct InConvParams {
   const bf16_t* x; long long ldx;  // hn (ntok, k)
@@ -234,14 +235,18 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
         sO[row * kIcPitch + col] = from_f32<bf16_t>(acc[i][j][r] + 0.0f);
       }
     }
-  if (!xt) {  // ---- z tile: 16-byte row stores (z column = n0 - dim) ----
+  if (!xt) {  // ---- z tile: 16-byte row stores (z column = n0 - dim), write-through ----
     ic_lds_barrier();
+    const auto zr = __builtin_amdgcn_make_buffer_rsrc(
+        q.z + (long long)m0 * q.ldz, 0,
+        static_cast<int>(max(0, min(q.ntok - m0, 128)) * q.ldz * 2), 0x00020000);
     for (int pc = tid; pc < 128 * 16; pc += NT) {
       const int row = pc >> 4, cq = pc & 15;
       const int gm = m0 + row;
       if (gm < q.ntok)
-        *reinterpret_cast<uint4*>(q.z + (long long)gm * q.ldz + (n0 - p.dim) + cq * 8) =
-            *reinterpret_cast<const uint4*>(&sO[row * kIcPitch + cq * 8]);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            *reinterpret_cast<const ic_i32x4*>(&sO[row * kIcPitch + cq * 8]), zr,
+            (row * static_cast<int>(q.ldz) + (n0 - p.dim) + cq * 8) * 2, 0, kSmallStoreWT);
     }
     return;
   }
@@ -355,7 +360,9 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
   for (int i = 0; i < kRows; ++i) {
     *reinterpret_cast<uint32_t*>(&sU[(wave * kRows + i) * kIcPitch + 2 * lane]) = upk[i];
     const int tok = tw + i;
-    if (tok < q.ntok) *reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c) = upk[i];
+    if (tok < q.ntok)  // write-through (agent-scope relaxed store: sc1)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(p.u + (long long)tok * p.u_tl + c), upk[i],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   ic_lds_barrier();
 
@@ -395,12 +402,15 @@ __global__ __launch_bounds__(512) void inproj_conv_kernel(const InConvParams q) 
   __builtin_amdgcn_wave_barrier();
   if (mw) {
     const int nq = q.ep >> 2;
+    const auto pr = __builtin_amdgcn_make_buffer_rsrc(
+        q.part, 0, static_cast<int>((long long)q.nsplit * q.ntok * q.ep * 4), 0x00020000);
     for (int i = lane; i < 16 * nq; i += 64) {
       const int r = i / nq, qd = i - r * nq;
       const int tok = tok_lo + wave * 16 + r;
       if (tok < q.ntok)
-        *reinterpret_cast<float4*>(q.part + ((long long)sp * q.ntok + tok) * q.ep + 4 * qd) =
-            *reinterpret_cast<const float4*>(&sP[r * kPP + 4 * qd]);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            *reinterpret_cast<const ic_i32x4*>(&sP[r * kPP + 4 * qd]), pr,
+            (((sp * q.ntok + tok) * q.ep) + 4 * qd) * 4, 0, kSmallStoreWT);
     }
   }
 }

@@ -60,7 +60,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t norm_row_rsrc(const void* base
 // (no early exit for the rows past the end: their buffers have 0-byte ranges, so every
 // access is a no-op, and the kernel-argument loads are not split by a branch into two
 // dependent rounds before the first global load)
-template <int CPL, bool RES, bool RO>
+template <int CPL, bool RES, bool RO, int ST = 0>
 __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
   const long long row0 = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool live = row0 < p.rows;
@@ -119,12 +119,12 @@ __global__ __launch_bounds__(256) void add_rms_bf16_kernel(const NormParams p) {
                                      (static_cast<uint32_t>(from_f32<bf16_t>(y[1])) << 16)),
                     static_cast<int>(static_cast<uint32_t>(from_f32<bf16_t>(y[2])) |
                                      (static_cast<uint32_t>(from_f32<bf16_t>(y[3])) << 16))};
-    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(o2, orr, off(j, 2), 0, ST);
     if constexpr (RO) {
       typedef __attribute__((__vector_size__(4 * sizeof(int)))) int v4i;
       const v4i r4 = {static_cast<int>(__float_as_uint(v[j][0])), static_cast<int>(__float_as_uint(v[j][1])),
                       static_cast<int>(__float_as_uint(v[j][2])), static_cast<int>(__float_as_uint(v[j][3]))};
-      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(r4, ror, off(j, 4), 0, ST);
     }
   }
 }
@@ -749,8 +749,12 @@ extern "C" int vm_add_norm_fwd(const void* x, int x_dtype, const void* residual,
       (!residual || res_dtype == VM_DTYPE_F32) && (!residual_out || res_out_dtype == VM_DTYPE_F32) &&
       cols <= 256 * 4) {
     const int cpl = (cols + 255) / 256;
+    // streaming-chunk row counts: the stores write through (kSmallStoreWT)
+    const bool wt = rows <= kSmallStoreRows;
 #define VM_RMS_BF16(CPLV)                                                                   \
-  if (residual && residual_out)                                                             \
+  if (residual && residual_out && wt)                                                       \
+    hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, true, kSmallStoreWT>), grid, dim3(256), 0, s, p); \
+  else if (residual && residual_out)                                                        \
     hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, true>), grid, dim3(256), 0, s, p);   \
   else if (residual)                                                                        \
     hipLaunchKernelGGL((add_rms_bf16_kernel<CPLV, true, false>), grid, dim3(256), 0, s, p);  \

@@ -80,12 +80,12 @@ __device__ __forceinline__ uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, in
   else
     return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
-template <typename T>
+template <typename T, int POL = 0>
 __device__ __forceinline__ void bstore(T v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
   if constexpr (sizeof(T) == 2)
-    __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, POL);
   else
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, POL);
 }
 template <typename T>
 __device__ __forceinline__ float raw_f32(uint32_t r) {
@@ -1366,7 +1366,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
             y = HZ ? y * (zz * __builtin_amdgcn_rcpf(
                                    fmaf(__builtin_amdgcn_exp2f(-zz * kLog2e), kLog2e, kLog2e)))
                    : y * kLn2f;
-          bstore<T>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
+          bstore<T, kSmallStoreWT>(from_f32<T>(y), orr, live ? voff_st : kSeqDead, ps.orow(t) * os);
         }
       }
     }
@@ -1381,7 +1381,7 @@ __global__ __launch_bounds__(64 * kChW) void scan_chunk_kernel(const ScanParams 
             store_dyn(ps.hl, ps.hb * p.hl_sb + d * p.hl_sd + n, p.hl_dtype,
                       ((n & 1) ? h[n >> 1].y : h[n >> 1].x) * kLn2f);
       }
-      for (int t = L; t < p.out_len; ++t) bstore<T>(from_f32<T>(0.0f), orr, voff, t * os);
+      for (int t = L; t < p.out_len; ++t) bstore<T, kSmallStoreWT>(from_f32<T>(0.0f), orr, voff, t * os);
     }
   };
 
